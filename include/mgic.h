@@ -1,0 +1,192 @@
+/*
+ * mgic.h -- C ABI of the MI355X-native multigrid library (libmgic.so).
+ *
+ * The drop-in boundary for the reference's hot path: eugenealim/MG_IC_code
+ * hands its V-cycle to Chombo through the operator-plugin API
+ *   defineOperatorFactory / VariableCoeffPoissonOperatorFactory
+ *     (Source/VariableCoeffPoissonOperatorFactory.H:22-117)
+ *   VariableCoeffPoissonOperator  (Source/VariableCoeffPoissonOperator.H:25-170)
+ * and the operator reaches its arithmetic through the ChomboFortran C ABI
+ * (Source/VariableCoeffPoissonOperatorF_F.H; those host drop-ins are declared
+ * in mgic_chf.h).  This header exposes the same surface with plain pointers
+ * and integers: every handle-level entry point below names the reference
+ * method it replaces.
+ *
+ * Conventions
+ *   - Boxes are 6 ints {lo0, lo1, lo2, hi0, hi1, hi2}, inclusive cell
+ *     indices in the level's global index space (Chombo Box).
+ *   - Every function returns 0 on success and a negative MGIC_E* code on
+ *     failure (the reference aborts through MayDay; this library never
+ *     aborts); mgic_last_error() describes the last failure of the thread.
+ *   - All device work is enqueued on the communicator's HIP stream; the
+ *     functions that return host scalars (dot, norm, iteration norms,
+ *     BiCGStab) synchronise that stream.
+ *   - Fields are fp64, one component, one ghost layer, device resident.
+ */
+#ifndef MGIC_H
+#define MGIC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGIC_API __attribute__((visibility("default")))
+
+#define MGIC_OK 0
+#define MGIC_EBADARG (-1)
+#define MGIC_EHIP (-2)
+#define MGIC_ERCCL (-3)
+#define MGIC_ESTATE (-4)
+#define MGIC_EUNKNOWN (-5)
+#define MGIC_UNIQUE_ID_BYTES 128
+
+typedef struct mgic_comm_s *mgic_comm;       /* one rank: RCCL comm + HIP stream */
+typedef struct mgic_grid_s *mgic_grid;       /* DisjointBoxLayout + ProblemDomain + dx */
+typedef struct mgic_field_s *mgic_field;     /* LevelData<FArrayBox> (1 comp, 1 ghost) */
+typedef struct mgic_factory_s *mgic_factory; /* VariableCoeffPoissonOperatorFactory */
+typedef struct mgic_op_s *mgic_op;           /* VariableCoeffPoissonOperator */
+typedef struct mgic_mg_s *mgic_mg;           /* AMRMultiGrid on one AMR level */
+
+/* Operator constants and ParseBC state (params.txt keys alpha, beta, bc_lo,
+ * bc_hi, bc_value, coefficient_average_type; [Chombo] statics). */
+typedef struct {
+  double alpha, beta;          /* default 0, -1 (Factory.cpp:317-322) */
+  int bc_lo[3], bc_hi[3];      /* 0 Dirichlet, 1 Neumann, 2 periodic flag */
+  double bc_value;
+  int coefficient_average_type; /* 0 arithmetic (default), 1 harmonic */
+  int prolong_type;             /* 0 piecewise constant, 1 linear (default) */
+  int relax_mode;               /* 1 GSRB (default), 4 Jacobi */
+  int fused_smoother;           /* 1: fused red+black sweep where valid */
+} mgic_op_params;
+
+/* MultiGrid / bottom-solver configuration (MultilevelLinearOp knobs:
+ * numMGsmooth, numMGIterations, preCondSolverDepth; BiCGStab defaults). */
+typedef struct {
+  int max_depth;         /* deepest MG depth, -1: as deep as coarsenable */
+  int n_pre, n_post, n_bottom;
+  int bottom_solver;     /* 0: relax(n_bottom), 1: BiCGStab */
+  int cycles;            /* 1 = V-cycle */
+  int agglomerate_below; /* gather to rank 0 once a box side < this; 0 off */
+  int bicg_imax;
+  double bicg_eps, bicg_reps, bicg_small;
+  int bicg_restarts, bicg_norm_type;
+} mgic_mg_params;
+
+MGIC_API const char *mgic_version(void);
+MGIC_API const char *mgic_last_error(void);
+MGIC_API int mgic_set_device(int device);
+MGIC_API int mgic_get_device_count(int *count);
+MGIC_API int mgic_device_synchronize(void);
+MGIC_API void mgic_op_params_default(mgic_op_params *p);
+MGIC_API void mgic_mg_params_default(mgic_mg_params *p);
+
+/* ---- communicator (MPI_Init / process group, Main_PoissonSolver.cpp:261) */
+MGIC_API int mgic_comm_unique_id(unsigned char id[MGIC_UNIQUE_ID_BYTES]);
+MGIC_API int mgic_comm_create(int rank, int size, const unsigned char *id, int force_rccl,
+                              mgic_comm *out);
+MGIC_API int mgic_comm_destroy(mgic_comm c);
+MGIC_API int mgic_comm_set_stream(mgic_comm c, void *hip_stream); /* NULL: own stream */
+MGIC_API int mgic_comm_get_stream(mgic_comm c, void **hip_stream);
+MGIC_API int mgic_comm_set_self_messages(mgic_comm c, int on);
+MGIC_API int mgic_comm_synchronize(mgic_comm c);
+MGIC_API int mgic_comm_rank(mgic_comm c, int *rank, int *size, int *uses_rccl);
+
+/* ---- grids (DisjointBoxLayout(boxes, procs, domain); set_grids,
+ *      Source/SetGrids.cpp:54-58) */
+MGIC_API int mgic_grid_create(mgic_comm c, const int domain[6], const int periodic[3], double dx,
+                              int nbox, const int *boxes, const int *owners, mgic_grid *out);
+MGIC_API int mgic_grid_destroy(mgic_grid g);
+MGIC_API int mgic_grid_num_local(mgic_grid g, int *n);
+MGIC_API int mgic_grid_local_box(mgic_grid g, int n, int lohi[6], int *global_index);
+MGIC_API int mgic_grid_coarsen(mgic_grid g, int ratio, mgic_grid *out);
+
+/* ---- fields (LevelData<FArrayBox>) */
+MGIC_API int mgic_field_create(mgic_grid g, mgic_field *out);
+MGIC_API int mgic_field_destroy(mgic_field f);
+/* device pointer of the valid-lo cell of local box n and its strides
+ * {1, sy, sz} in doubles */
+MGIC_API int mgic_field_device_ptr(mgic_field f, int n, double **valid_lo, long strides[3]);
+/* host <-> device, contiguous i-fastest over the valid box (with_ghosts=0)
+ * or over the valid box grown by one (with_ghosts=1); synchronous */
+MGIC_API int mgic_field_upload(mgic_field f, int n, const double *host, int with_ghosts);
+MGIC_API int mgic_field_download(mgic_field f, int n, double *host, int with_ghosts);
+MGIC_API int mgic_field_set_val(mgic_field f, double v);  /* valid cells */
+MGIC_API int mgic_field_set_zero(mgic_field f);           /* valid + ghosts */
+MGIC_API int mgic_field_exchange(mgic_field f);           /* LevelData::exchange */
+/* LevelData::copyTo: valid -> valid (+ dst face ghosts if with_faces) */
+MGIC_API int mgic_field_copy_to(mgic_field src, mgic_field dst, int with_faces);
+/* set_a_coef / set_rhs at psi = 1 (SetLevelData.cpp:73-127, :281-325);
+ * bh[13] = {domain_length, G_Newton, phi_amplitude, phi_wavelength,
+ *           bh1_bare_mass, bh2_bare_mass, bh1_spin, bh2_spin, bh1_offset,
+ *           bh2_offset, bh1_momentum, bh2_momentum, constant_K} */
+MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]);
+
+/* ---- operator factory (defineOperatorFactory, Factory.cpp:29-49) */
+MGIC_API int mgic_factory_define(mgic_grid g, const mgic_op_params *p, mgic_field aCoef,
+                                 mgic_field bCoef, mgic_factory *out);
+MGIC_API int mgic_factory_destroy(mgic_factory f);
+/* MGnewOp (Factory.cpp:139-234): returns 1 with *out = NULL when the layout
+ * is not coarsenable(2^depth * s_maxCoarse) */
+MGIC_API int mgic_factory_mg_new_op(mgic_factory f, int depth, mgic_op *out);
+MGIC_API int mgic_factory_amr_new_op(mgic_factory f, mgic_op *out); /* :236-295 */
+MGIC_API int mgic_factory_ref_to_finer(mgic_factory f, int *ratio); /* :297-314 */
+
+/* ---- operator (VariableCoeffPoissonOperator) */
+MGIC_API int mgic_op_destroy(mgic_op op);
+MGIC_API int mgic_op_grid(mgic_op op, mgic_grid *out);
+MGIC_API int mgic_op_coef(mgic_op op, int which /* 0 aCoef, 1 bCoef, 2 lambda */,
+                          mgic_field *out);
+MGIC_API int mgic_op_residual(mgic_op op, mgic_field lhs, mgic_field dpsi, mgic_field rhs,
+                              int homogeneous);                                  /* residualI */
+MGIC_API int mgic_op_apply_op(mgic_op op, mgic_field lhs, mgic_field dpsi, int homogeneous);
+MGIC_API int mgic_op_apply_op_no_boundary(mgic_op op, mgic_field lhs, mgic_field dpsi);
+MGIC_API int mgic_op_precond(mgic_op op, mgic_field cor, mgic_field res);        /* preCond */
+MGIC_API int mgic_op_relax(mgic_op op, mgic_field e, mgic_field r, int iterations);
+MGIC_API int mgic_op_level_gsrb(mgic_op op, mgic_field dpsi, mgic_field rhs);
+MGIC_API int mgic_op_level_jacobi(mgic_op op, mgic_field dpsi, mgic_field rhs);
+MGIC_API int mgic_op_restrict_residual(mgic_op fine, mgic_field resCoarse, mgic_field dpsiFine,
+                                       mgic_field rhsFine);
+MGIC_API int mgic_op_prolong_increment(mgic_op fine, mgic_field phiFine, mgic_field corCoarse);
+MGIC_API int mgic_op_set_alpha_beta(mgic_op op, double alpha, double beta);
+MGIC_API int mgic_op_set_coefs(mgic_op op, mgic_field aCoef, mgic_field bCoef, double alpha,
+                               double beta);
+MGIC_API int mgic_op_reset_lambda(mgic_op op);
+MGIC_API int mgic_op_set_time(mgic_op op, double t);
+MGIC_API int mgic_op_fill_bc(mgic_op op, mgic_field u, int homogeneous);         /* m_bc */
+MGIC_API int mgic_op_set_to_zero(mgic_op op, mgic_field x);
+MGIC_API int mgic_op_assign(mgic_op op, mgic_field lhs, mgic_field rhs);
+MGIC_API int mgic_op_incr(mgic_op op, mgic_field lhs, mgic_field x, double scale);
+MGIC_API int mgic_op_axby(mgic_op op, mgic_field lhs, mgic_field x, mgic_field y, double a,
+                          double b);
+MGIC_API int mgic_op_scale(mgic_op op, mgic_field lhs, double s);
+MGIC_API int mgic_op_dot(mgic_op op, mgic_field x, mgic_field y, double *out);
+MGIC_API int mgic_op_norm(mgic_op op, mgic_field x, int ord, double *out);
+/* BiCGStabSolver<LevelData>::solve with this op (bottom solver) */
+MGIC_API int mgic_op_bicgstab(mgic_op op, mgic_field phi, mgic_field rhs, int homogeneous,
+                              const mgic_mg_params *p, int *iterations);
+
+/* ---- multigrid (AMRMultiGrid on one AMR level + MultiGrid hierarchy) */
+MGIC_API int mgic_mg_create(mgic_factory f, const mgic_mg_params *p, mgic_mg *out);
+MGIC_API int mgic_mg_destroy(mgic_mg mg);
+MGIC_API int mgic_mg_num_depths(mgic_mg mg, int *n);
+MGIC_API int mgic_mg_op(mgic_mg mg, int depth, mgic_op *out);
+/* internal fields of depth >= 1: which 0 = correction e, 1 = residual r */
+MGIC_API int mgic_mg_level_field(mgic_mg mg, int depth, int which, mgic_field *out);
+MGIC_API int mgic_mg_one_cycle(mgic_mg mg, mgic_field e, mgic_field r); /* MultiGrid::oneCycle */
+/* e = 0; oneCycle(e, resid); phi += e; resid = rhs - L(phi); *norm (if
+ * norm_type >= 0, else not computed and nothing synchronised) */
+MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
+                               int norm_type, int homogeneous, double *norm);
+MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
+                                   mgic_field resid, int norm_type, int homogeneous,
+                                   double *norm);
+
+/* ---- instrumentation: hipEvents around every smoother launch on boxes of
+ * at least min_cells cells */
+MGIC_API int mgic_prof_smoother(int enable, long min_cells);
+MGIC_API int mgic_prof_smoother_read(int *launches, double *total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGIC_H */

@@ -1,0 +1,188 @@
+"""ctypes binding of libmgic.so (the C ABI declared in include/mgic.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc,
+gfx950).  There is no fallback: if the shared object is missing or fails to
+load, importing this module raises, so nothing can silently run on a CPU
+path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_long, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmgic.so")
+
+
+class MgicError(RuntimeError):
+    """A libmgic call returned a negative status."""
+
+    def __init__(self, func: str, code: int, msg: str):
+        super().__init__(f"{func} failed ({code}): {msg}")
+        self.code = code
+
+
+class OpParams(ctypes.Structure):
+    """mgic_op_params (include/mgic.h)."""
+
+    _fields_ = [
+        ("alpha", c_double),
+        ("beta", c_double),
+        ("bc_lo", c_int * 3),
+        ("bc_hi", c_int * 3),
+        ("bc_value", c_double),
+        ("coefficient_average_type", c_int),
+        ("prolong_type", c_int),
+        ("relax_mode", c_int),
+        ("fused_smoother", c_int),
+    ]
+
+
+class MGParams(ctypes.Structure):
+    """mgic_mg_params (include/mgic.h)."""
+
+    _fields_ = [
+        ("max_depth", c_int),
+        ("n_pre", c_int),
+        ("n_post", c_int),
+        ("n_bottom", c_int),
+        ("bottom_solver", c_int),
+        ("cycles", c_int),
+        ("agglomerate_below", c_int),
+        ("bicg_imax", c_int),
+        ("bicg_eps", c_double),
+        ("bicg_reps", c_double),
+        ("bicg_small", c_double),
+        ("bicg_restarts", c_int),
+        ("bicg_norm_type", c_int),
+    ]
+
+
+H = c_void_p  # every opaque handle
+PI = POINTER(c_int)
+PD = POINTER(c_double)
+PH = POINTER(c_void_p)
+
+# name -> argtypes (all return int status unless listed in _RESTYPE)
+SIGNATURES = {
+    "mgic_version": [],
+    "mgic_last_error": [],
+    "mgic_set_device": [c_int],
+    "mgic_get_device_count": [PI],
+    "mgic_device_synchronize": [],
+    "mgic_op_params_default": [POINTER(OpParams)],
+    "mgic_mg_params_default": [POINTER(MGParams)],
+    "mgic_comm_unique_id": [ctypes.c_char_p],
+    "mgic_comm_create": [c_int, c_int, ctypes.c_char_p, c_int, PH],
+    "mgic_comm_destroy": [H],
+    "mgic_comm_set_stream": [H, c_void_p],
+    "mgic_comm_get_stream": [H, PH],
+    "mgic_comm_set_self_messages": [H, c_int],
+    "mgic_comm_synchronize": [H],
+    "mgic_comm_rank": [H, PI, PI, PI],
+    "mgic_grid_create": [H, PI, PI, c_double, c_int, PI, PI, PH],
+    "mgic_grid_destroy": [H],
+    "mgic_grid_num_local": [H, PI],
+    "mgic_grid_local_box": [H, c_int, PI, PI],
+    "mgic_grid_coarsen": [H, c_int, PH],
+    "mgic_field_create": [H, PH],
+    "mgic_field_destroy": [H],
+    "mgic_field_device_ptr": [H, c_int, PH, POINTER(c_long)],
+    "mgic_field_upload": [H, c_int, PD, c_int],
+    "mgic_field_download": [H, c_int, PD, c_int],
+    "mgic_field_set_val": [H, c_double],
+    "mgic_field_set_zero": [H],
+    "mgic_field_exchange": [H],
+    "mgic_field_copy_to": [H, H, c_int],
+    "mgic_field_binary_bh": [H, H, PD],
+    "mgic_factory_define": [H, POINTER(OpParams), H, H, PH],
+    "mgic_factory_destroy": [H],
+    "mgic_factory_mg_new_op": [H, c_int, PH],
+    "mgic_factory_amr_new_op": [H, PH],
+    "mgic_factory_ref_to_finer": [H, PI],
+    "mgic_op_destroy": [H],
+    "mgic_op_grid": [H, PH],
+    "mgic_op_coef": [H, c_int, PH],
+    "mgic_op_residual": [H, H, H, H, c_int],
+    "mgic_op_apply_op": [H, H, H, c_int],
+    "mgic_op_apply_op_no_boundary": [H, H, H],
+    "mgic_op_precond": [H, H, H],
+    "mgic_op_relax": [H, H, H, c_int],
+    "mgic_op_level_gsrb": [H, H, H],
+    "mgic_op_level_jacobi": [H, H, H],
+    "mgic_op_restrict_residual": [H, H, H, H],
+    "mgic_op_prolong_increment": [H, H, H],
+    "mgic_op_set_alpha_beta": [H, c_double, c_double],
+    "mgic_op_set_coefs": [H, H, H, c_double, c_double],
+    "mgic_op_reset_lambda": [H],
+    "mgic_op_set_time": [H, c_double],
+    "mgic_op_fill_bc": [H, H, c_int],
+    "mgic_op_set_to_zero": [H, H],
+    "mgic_op_assign": [H, H, H],
+    "mgic_op_incr": [H, H, H, c_double],
+    "mgic_op_axby": [H, H, H, H, c_double, c_double],
+    "mgic_op_scale": [H, H, c_double],
+    "mgic_op_dot": [H, H, H, PD],
+    "mgic_op_norm": [H, H, c_int, PD],
+    "mgic_op_bicgstab": [H, H, H, c_int, POINTER(MGParams), PI],
+    "mgic_mg_create": [H, POINTER(MGParams), PH],
+    "mgic_mg_destroy": [H],
+    "mgic_mg_num_depths": [H, PI],
+    "mgic_mg_op": [H, c_int, PH],
+    "mgic_mg_level_field": [H, c_int, c_int, PH],
+    "mgic_mg_one_cycle": [H, H, H],
+    "mgic_mg_iteration": [H, H, H, H, c_int, c_int, PD],
+    "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
+    "mgic_prof_smoother": [c_int, c_long],
+    "mgic_prof_smoother_read": [PI, PD],
+    # ChomboFortran drop-ins (include/mgic_chf.h); argtypes left open
+    "gsrbhelmholtzvc3d_": None,
+    "vccomputeop3d_": None,
+    "vccomputeres3d_": None,
+    "restrictresvc3d_": None,
+}
+
+_RESTYPE = {
+    "mgic_version": c_char_p,
+    "mgic_last_error": c_char_p,
+    "mgic_op_params_default": None,
+    "mgic_mg_params_default": None,
+    "gsrbhelmholtzvc3d_": None,
+    "vccomputeop3d_": None,
+    "vccomputeres3d_": None,
+    "restrictresvc3d_": None,
+}
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError = missing export: fail loudly
+        if argtypes is not None:
+            fn.argtypes = argtypes
+        fn.restype = _RESTYPE.get(name, c_int)
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    msg = lib.mgic_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(func: str, status: int) -> int:
+    """Raise MgicError on a negative status; pass through 0 / 1."""
+    if status < 0:
+        raise MgicError(func, status, last_error())
+    return status
+
+
+def call(name: str, *args) -> int:
+    return check(name, getattr(lib, name)(*args))

@@ -1,0 +1,658 @@
+// capi.cpp -- extern "C" boundary (include/mgic.h) over the C++ layer.
+#include <cstring>
+#include <string>
+
+#include "../../include/mgic.h"
+#include "op.hpp"
+
+using namespace mgic;
+
+struct mgic_comm_s {
+  std::shared_ptr<Comm> c;
+};
+struct mgic_grid_s {
+  std::shared_ptr<Grid> g;
+};
+struct mgic_field_s {
+  std::shared_ptr<LevelData> f;
+};
+struct mgic_factory_s {
+  VariableCoeffPoissonOperatorFactory f;
+};
+struct mgic_op_s {
+  std::unique_ptr<VariableCoeffPoissonOperator> owned;
+  VariableCoeffPoissonOperator *op = nullptr;
+};
+struct mgic_mg_s {
+  AMRMultiGrid amg;
+};
+
+namespace {
+thread_local std::string g_err;
+
+template <class F>
+int guard(F &&f) {
+  try {
+    f();
+    return MGIC_OK;
+  } catch (const Error &e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::exception &e) {
+    g_err = e.what();
+    return MGIC_EUNKNOWN;
+  } catch (...) {
+    g_err = "unknown exception";
+    return MGIC_EUNKNOWN;
+  }
+}
+
+#define NEED(p) MGIC_CHECK((p) != nullptr, "null argument: " #p)
+
+OpParams to_op(const mgic_op_params *p) {
+  OpParams o;
+  if (!p) return o;
+  o.alpha = p->alpha;
+  o.beta = p->beta;
+  for (int d = 0; d < 3; ++d) {
+    o.bc_lo[d] = p->bc_lo[d];
+    o.bc_hi[d] = p->bc_hi[d];
+  }
+  o.bc_value = p->bc_value;
+  o.coefficient_average_type = p->coefficient_average_type;
+  o.prolong_type = p->prolong_type;
+  o.relax_mode = p->relax_mode;
+  o.fused_smoother = p->fused_smoother;
+  return o;
+}
+
+MGParams to_mg(const mgic_mg_params *p) {
+  MGParams m;
+  if (!p) return m;
+  m.max_depth = p->max_depth;
+  m.n_pre = p->n_pre;
+  m.n_post = p->n_post;
+  m.n_bottom = p->n_bottom;
+  m.bottom_solver = p->bottom_solver;
+  m.cycles = p->cycles;
+  m.agglomerate_below = p->agglomerate_below;
+  m.bicg.imax = p->bicg_imax;
+  m.bicg.eps = p->bicg_eps;
+  m.bicg.reps = p->bicg_reps;
+  m.bicg.small = p->bicg_small;
+  m.bicg.numRestarts = p->bicg_restarts;
+  m.bicg.normType = p->bicg_norm_type;
+  return m;
+}
+
+// host contiguous <-> fab region copy through a device staging buffer
+void box_transfer(LevelData &f, int n, double *host, bool upload, bool with_ghosts) {
+  MGIC_CHECK(n >= 0 && n < f.grid->nlocal(), "bad local box index");
+  const FabGeom &g = f.grid->geom[n];
+  Box R = g.valid;
+  if (with_ghosts)
+    for (int d = 0; d < 3; ++d) {
+      R.lo[d] -= 1;
+      R.hi[d] += 1;
+    }
+  const long nc = R.ncells();
+  const hipStream_t st = f.grid->comm->stream();
+  double *dbuf = nullptr;
+  CopyItem *ditem = nullptr;
+  MGIC_HIP(hipMalloc(&dbuf, sizeof(double) * (size_t)nc));
+  MGIC_HIP(hipMalloc(&ditem, sizeof(CopyItem)));
+  CopyItem it{};
+  it.nx = R.size(0);
+  it.ny = R.size(1);
+  it.nz = R.size(2);
+  const long off = g.offset(R.lo[0], R.lo[1], R.lo[2]);
+  if (upload) {
+    it.src = -1;
+    it.soff = 0;
+    it.ssy = it.nx;
+    it.ssz = (long)it.nx * it.ny;
+    it.dst = n;
+    it.doff = off;
+    it.dsy = g.sy;
+    it.dsz = g.sz;
+  } else {
+    it.dst = -1;
+    it.doff = 0;
+    it.dsy = it.nx;
+    it.dsz = (long)it.nx * it.ny;
+    it.src = n;
+    it.soff = off;
+    it.ssy = g.sy;
+    it.ssz = g.sz;
+  }
+  try {
+    MGIC_HIP(hipStreamSynchronize(st));
+    MGIC_HIP(hipMemcpy(ditem, &it, sizeof(CopyItem), hipMemcpyHostToDevice));
+    if (upload) {
+      MGIC_HIP(hipMemcpy(dbuf, host, sizeof(double) * (size_t)nc, hipMemcpyHostToDevice));
+      kern::copy_items(ditem, 1, nc, nullptr, dbuf, f.d_tab, nullptr, st);
+      MGIC_HIP(hipStreamSynchronize(st));
+    } else {
+      kern::copy_items(ditem, 1, nc, f.d_tab, nullptr, nullptr, dbuf, st);
+      MGIC_HIP(hipStreamSynchronize(st));
+      MGIC_HIP(hipMemcpy(host, dbuf, sizeof(double) * (size_t)nc, hipMemcpyDeviceToHost));
+    }
+  } catch (...) {
+    (void)hipFree(dbuf);
+    (void)hipFree(ditem);
+    throw;
+  }
+  MGIC_HIP(hipFree(dbuf));
+  MGIC_HIP(hipFree(ditem));
+}
+
+mgic_field borrowed_field(LevelData *ld) {
+  auto *h = new mgic_field_s;
+  h->f = std::shared_ptr<LevelData>(ld, [](LevelData *) {});
+  return h;
+}
+}  // namespace
+
+extern "C" {
+
+MGIC_API const char *mgic_version(void) { return "mgic 0.1.0 (gfx950, fp64)"; }
+MGIC_API const char *mgic_last_error(void) { return g_err.c_str(); }
+
+MGIC_API int mgic_set_device(int device) {
+  return guard([&] { MGIC_HIP(hipSetDevice(device)); });
+}
+MGIC_API int mgic_get_device_count(int *count) {
+  return guard([&] {
+    NEED(count);
+    MGIC_HIP(hipGetDeviceCount(count));
+  });
+}
+MGIC_API int mgic_device_synchronize(void) {
+  return guard([&] { MGIC_HIP(hipDeviceSynchronize()); });
+}
+
+MGIC_API void mgic_op_params_default(mgic_op_params *p) {
+  if (!p) return;
+  OpParams o;
+  p->alpha = o.alpha;
+  p->beta = o.beta;
+  for (int d = 0; d < 3; ++d) {
+    p->bc_lo[d] = o.bc_lo[d];
+    p->bc_hi[d] = o.bc_hi[d];
+  }
+  p->bc_value = o.bc_value;
+  p->coefficient_average_type = o.coefficient_average_type;
+  p->prolong_type = o.prolong_type;
+  p->relax_mode = o.relax_mode;
+  p->fused_smoother = o.fused_smoother;
+}
+
+MGIC_API void mgic_mg_params_default(mgic_mg_params *p) {
+  if (!p) return;
+  MGParams m;
+  p->max_depth = m.max_depth;
+  p->n_pre = m.n_pre;
+  p->n_post = m.n_post;
+  p->n_bottom = m.n_bottom;
+  p->bottom_solver = m.bottom_solver;
+  p->cycles = m.cycles;
+  p->agglomerate_below = m.agglomerate_below;
+  p->bicg_imax = m.bicg.imax;
+  p->bicg_eps = m.bicg.eps;
+  p->bicg_reps = m.bicg.reps;
+  p->bicg_small = m.bicg.small;
+  p->bicg_restarts = m.bicg.numRestarts;
+  p->bicg_norm_type = m.bicg.normType;
+}
+
+// ---------------------------------------------------------------- comm
+MGIC_API int mgic_comm_unique_id(unsigned char id[MGIC_UNIQUE_ID_BYTES]) {
+  return guard([&] {
+    NEED(id);
+    static_assert(sizeof(ncclUniqueId) == MGIC_UNIQUE_ID_BYTES, "unique id size");
+    ncclUniqueId uid;
+    MGIC_NCCL(ncclGetUniqueId(&uid));
+    std::memcpy(id, &uid, sizeof(uid));
+  });
+}
+
+MGIC_API int mgic_comm_create(int rank, int size, const unsigned char *id, int force_rccl,
+                              mgic_comm *out) {
+  return guard([&] {
+    NEED(out);
+    ncclUniqueId uid;
+    const ncclUniqueId *pid = nullptr;
+    if (id) {
+      std::memcpy(&uid, id, sizeof(uid));
+      pid = &uid;
+    }
+    auto *h = new mgic_comm_s;
+    try {
+      h->c = std::make_shared<Comm>(rank, size, pid, force_rccl != 0);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+MGIC_API int mgic_comm_destroy(mgic_comm c) {
+  return guard([&] { delete c; });
+}
+MGIC_API int mgic_comm_set_stream(mgic_comm c, void *s) {
+  return guard([&] {
+    NEED(c);
+    c->c->set_stream((hipStream_t)s);
+  });
+}
+MGIC_API int mgic_comm_get_stream(mgic_comm c, void **s) {
+  return guard([&] {
+    NEED(c);
+    NEED(s);
+    *s = (void *)c->c->stream();
+  });
+}
+MGIC_API int mgic_comm_set_self_messages(mgic_comm c, int on) {
+  return guard([&] {
+    NEED(c);
+    c->c->set_self_messages(on != 0);
+  });
+}
+MGIC_API int mgic_comm_synchronize(mgic_comm c) {
+  return guard([&] {
+    NEED(c);
+    MGIC_HIP(hipStreamSynchronize(c->c->stream()));
+  });
+}
+MGIC_API int mgic_comm_rank(mgic_comm c, int *rank, int *size, int *uses_rccl) {
+  return guard([&] {
+    NEED(c);
+    if (rank) *rank = c->c->rank();
+    if (size) *size = c->c->size();
+    if (uses_rccl) *uses_rccl = c->c->uses_rccl();
+  });
+}
+
+// ---------------------------------------------------------------- grid
+MGIC_API int mgic_grid_create(mgic_comm c, const int domain[6], const int periodic[3], double dx,
+                              int nbox, const int *boxes, const int *owners, mgic_grid *out) {
+  return guard([&] {
+    NEED(c);
+    NEED(domain);
+    NEED(boxes);
+    NEED(out);
+    MGIC_CHECK(nbox >= 1, "nbox must be >= 1");
+    MGIC_CHECK(dx > 0.0, "dx must be positive");
+    bool per[3] = {false, false, false};
+    if (periodic)
+      for (int d = 0; d < 3; ++d) per[d] = periodic[d] != 0;
+    std::vector<Box> bx;
+    std::vector<int> own;
+    for (int b = 0; b < nbox; ++b) {
+      bx.push_back(Box::make(boxes + 6 * b));
+      own.push_back(owners ? owners[b] : 0);
+    }
+    auto g = std::make_shared<Grid>(c->c, Box::make(domain), per, dx, bx, own);
+    MGIC_CHECK(g->tiles_domain(), "boxes must be disjoint and tile the domain");
+    *out = new mgic_grid_s{g};
+  });
+}
+MGIC_API int mgic_grid_destroy(mgic_grid g) {
+  return guard([&] { delete g; });
+}
+MGIC_API int mgic_grid_num_local(mgic_grid g, int *n) {
+  return guard([&] {
+    NEED(g);
+    NEED(n);
+    *n = g->g->nlocal();
+  });
+}
+MGIC_API int mgic_grid_local_box(mgic_grid g, int n, int lohi[6], int *gi) {
+  return guard([&] {
+    NEED(g);
+    NEED(lohi);
+    MGIC_CHECK(n >= 0 && n < g->g->nlocal(), "bad local box index");
+    const Box &b = g->g->geom[n].valid;
+    for (int d = 0; d < 3; ++d) {
+      lohi[d] = b.lo[d];
+      lohi[3 + d] = b.hi[d];
+    }
+    if (gi) *gi = g->g->local[n];
+  });
+}
+MGIC_API int mgic_grid_coarsen(mgic_grid g, int ratio, mgic_grid *out) {
+  return guard([&] {
+    NEED(g);
+    NEED(out);
+    MGIC_CHECK(ratio >= 1 && g->g->coarsenable(ratio), "grid not coarsenable by ratio");
+    *out = new mgic_grid_s{g->g->coarsened(ratio)};
+  });
+}
+
+// ---------------------------------------------------------------- field
+MGIC_API int mgic_field_create(mgic_grid g, mgic_field *out) {
+  return guard([&] {
+    NEED(g);
+    NEED(out);
+    *out = new mgic_field_s{std::make_shared<LevelData>(g->g)};
+  });
+}
+MGIC_API int mgic_field_destroy(mgic_field f) {
+  return guard([&] { delete f; });
+}
+MGIC_API int mgic_field_device_ptr(mgic_field f, int n, double **p, long strides[3]) {
+  return guard([&] {
+    NEED(f);
+    MGIC_CHECK(n >= 0 && n < f->f->grid->nlocal(), "bad local box index");
+    if (p) *p = f->f->p[n];
+    if (strides) {
+      strides[0] = 1;
+      strides[1] = f->f->grid->geom[n].sy;
+      strides[2] = f->f->grid->geom[n].sz;
+    }
+  });
+}
+MGIC_API int mgic_field_upload(mgic_field f, int n, const double *host, int with_ghosts) {
+  return guard([&] {
+    NEED(f);
+    NEED(host);
+    box_transfer(*f->f, n, const_cast<double *>(host), true, with_ghosts != 0);
+  });
+}
+MGIC_API int mgic_field_download(mgic_field f, int n, double *host, int with_ghosts) {
+  return guard([&] {
+    NEED(f);
+    NEED(host);
+    box_transfer(*f->f, n, host, false, with_ghosts != 0);
+  });
+}
+MGIC_API int mgic_field_set_val(mgic_field f, double v) {
+  return guard([&] {
+    NEED(f);
+    LevelData &x = *f->f;
+    for (int n = 0; n < x.grid->nlocal(); ++n)
+      kern::blas(5, x.p[n], nullptr, nullptr, v, 0.0, x.grid->box_args_plain(n), x.grid->comm->stream());
+  });
+}
+MGIC_API int mgic_field_set_zero(mgic_field f) {
+  return guard([&] {
+    NEED(f);
+    f->f->set_zero_all(f->f->grid->comm->stream());
+  });
+}
+MGIC_API int mgic_field_exchange(mgic_field f) {
+  return guard([&] {
+    NEED(f);
+    f->f->exchange(f->f->grid->comm->stream());
+  });
+}
+MGIC_API int mgic_field_copy_to(mgic_field src, mgic_field dst, int with_faces) {
+  return guard([&] {
+    NEED(src);
+    NEED(dst);
+    auto plan = build_copy_plan(*src->f->grid, *dst->f->grid, true, with_faces != 0);
+    plan->execute(*dst->f->grid->comm, src->f->d_tab, dst->f->d_tab, dst->f->grid->comm->stream());
+    MGIC_HIP(hipStreamSynchronize(dst->f->grid->comm->stream()));
+  });
+}
+MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]) {
+  return guard([&] {
+    NEED(acoef);
+    NEED(rhs);
+    NEED(bh);
+    const Grid &g = *acoef->f->grid;
+    kern::BhParams p;
+    for (int d = 0; d < 3; ++d) p.domlen[d] = bh[0];
+    p.G_Newton = bh[1];
+    p.phi_amplitude = bh[2];
+    p.phi_wavelength = bh[3];
+    p.m1 = bh[4];
+    p.m2 = bh[5];
+    p.spin1 = bh[6];
+    p.spin2 = bh[7];
+    p.off1 = bh[8];
+    p.off2 = bh[9];
+    p.mom1 = bh[10];
+    p.mom2 = bh[11];
+    p.constant_K = bh[12];
+    for (int n = 0; n < g.nlocal(); ++n)
+      kern::binary_bh_coefs(acoef->f->p[n], rhs->f->p[n], g.box_args_plain(n), g.dx, p,
+                            g.comm->stream());
+  });
+}
+
+// ---------------------------------------------------------------- factory / op
+MGIC_API int mgic_factory_define(mgic_grid g, const mgic_op_params *p, mgic_field a,
+                                 mgic_field b, mgic_factory *out) {
+  return guard([&] {
+    NEED(g);
+    NEED(a);
+    NEED(b);
+    NEED(out);
+    auto *h = new mgic_factory_s;
+    h->f.define(g->g, to_op(p), a->f, b->f);
+    *out = h;
+  });
+}
+MGIC_API int mgic_factory_destroy(mgic_factory f) {
+  return guard([&] { delete f; });
+}
+MGIC_API int mgic_factory_mg_new_op(mgic_factory f, int depth, mgic_op *out) {
+  int rc = 0;
+  int st = guard([&] {
+    NEED(f);
+    NEED(out);
+    MGIC_CHECK(depth >= 0, "depth must be >= 0");
+    auto op = f->f.MGnewOp(depth);
+    if (!op) {
+      *out = nullptr;
+      rc = 1;
+      return;
+    }
+    auto *h = new mgic_op_s;
+    h->op = op.get();
+    h->owned = std::move(op);
+    *out = h;
+  });
+  return st ? st : rc;
+}
+MGIC_API int mgic_factory_amr_new_op(mgic_factory f, mgic_op *out) {
+  return guard([&] {
+    NEED(f);
+    NEED(out);
+    auto *h = new mgic_op_s;
+    h->owned = f->f.AMRnewOp();
+    h->op = h->owned.get();
+    *out = h;
+  });
+}
+MGIC_API int mgic_factory_ref_to_finer(mgic_factory f, int *r) {
+  return guard([&] {
+    NEED(f);
+    NEED(r);
+    *r = f->f.refToFiner();
+  });
+}
+
+#define OPGUARD(body)        \
+  return guard([&] {         \
+    NEED(op);                \
+    VariableCoeffPoissonOperator &o = *op->op; \
+    (void)o;                 \
+    body;                    \
+  })
+
+MGIC_API int mgic_op_destroy(mgic_op op) {
+  return guard([&] { delete op; });
+}
+MGIC_API int mgic_op_grid(mgic_op op, mgic_grid *out) {
+  OPGUARD(NEED(out); *out = new mgic_grid_s{o.grid});
+}
+MGIC_API int mgic_op_coef(mgic_op op, int which, mgic_field *out) {
+  OPGUARD({
+    NEED(out);
+    if (which == 0) *out = new mgic_field_s{o.m_aCoef};
+    else if (which == 1) *out = new mgic_field_s{o.m_bCoef};
+    else {
+      o.resetLambda();
+      MGIC_CHECK(o.m_lambda != nullptr, "lambda not defined");
+      *out = borrowed_field(o.m_lambda.get());
+    }
+  });
+}
+MGIC_API int mgic_op_residual(mgic_op op, mgic_field lhs, mgic_field dpsi, mgic_field rhs, int h) {
+  OPGUARD(NEED(lhs); NEED(dpsi); NEED(rhs); o.residualI(*lhs->f, *dpsi->f, *rhs->f, h != 0));
+}
+MGIC_API int mgic_op_apply_op(mgic_op op, mgic_field lhs, mgic_field dpsi, int h) {
+  OPGUARD(NEED(lhs); NEED(dpsi); o.applyOpI(*lhs->f, *dpsi->f, h != 0));
+}
+MGIC_API int mgic_op_apply_op_no_boundary(mgic_op op, mgic_field lhs, mgic_field dpsi) {
+  OPGUARD(NEED(lhs); NEED(dpsi); o.applyOpNoBoundary(*lhs->f, *dpsi->f));
+}
+MGIC_API int mgic_op_precond(mgic_op op, mgic_field cor, mgic_field res) {
+  OPGUARD(NEED(cor); NEED(res); o.preCond(*cor->f, *res->f));
+}
+MGIC_API int mgic_op_relax(mgic_op op, mgic_field e, mgic_field r, int it) {
+  OPGUARD(NEED(e); NEED(r); o.relax(*e->f, *r->f, it));
+}
+MGIC_API int mgic_op_level_gsrb(mgic_op op, mgic_field e, mgic_field r) {
+  OPGUARD(NEED(e); NEED(r); o.levelGSRB(*e->f, *r->f));
+}
+MGIC_API int mgic_op_level_jacobi(mgic_op op, mgic_field e, mgic_field r) {
+  OPGUARD(NEED(e); NEED(r); o.levelJacobi(*e->f, *r->f));
+}
+MGIC_API int mgic_op_restrict_residual(mgic_op op, mgic_field rc, mgic_field df, mgic_field rf) {
+  OPGUARD(NEED(rc); NEED(df); NEED(rf); o.restrictResidual(*rc->f, *df->f, *rf->f));
+}
+MGIC_API int mgic_op_prolong_increment(mgic_op op, mgic_field phi, mgic_field cor) {
+  OPGUARD(NEED(phi); NEED(cor); o.prolongIncrement(*phi->f, *cor->f));
+}
+MGIC_API int mgic_op_set_alpha_beta(mgic_op op, double a, double b) {
+  OPGUARD(o.setAlphaAndBeta(a, b));
+}
+MGIC_API int mgic_op_set_coefs(mgic_op op, mgic_field a, mgic_field b, double alpha, double beta) {
+  OPGUARD(NEED(a); NEED(b); o.setCoefs(a->f, b->f, alpha, beta));
+}
+MGIC_API int mgic_op_reset_lambda(mgic_op op) { OPGUARD(o.resetLambda()); }
+MGIC_API int mgic_op_set_time(mgic_op op, double t) { OPGUARD(o.setTime(t)); }
+MGIC_API int mgic_op_fill_bc(mgic_op op, mgic_field u, int h) {
+  OPGUARD(NEED(u); o.fillBC(*u->f, h != 0));
+}
+MGIC_API int mgic_op_set_to_zero(mgic_op op, mgic_field x) { OPGUARD(NEED(x); o.setToZero(*x->f)); }
+MGIC_API int mgic_op_assign(mgic_op op, mgic_field l, mgic_field r) {
+  OPGUARD(NEED(l); NEED(r); o.assignLocal(*l->f, *r->f));
+}
+MGIC_API int mgic_op_incr(mgic_op op, mgic_field l, mgic_field x, double s) {
+  OPGUARD(NEED(l); NEED(x); o.incr(*l->f, *x->f, s));
+}
+MGIC_API int mgic_op_axby(mgic_op op, mgic_field l, mgic_field x, mgic_field y, double a, double b) {
+  OPGUARD(NEED(l); NEED(x); NEED(y); o.axby(*l->f, *x->f, *y->f, a, b));
+}
+MGIC_API int mgic_op_scale(mgic_op op, mgic_field l, double s) { OPGUARD(NEED(l); o.scale(*l->f, s)); }
+MGIC_API int mgic_op_dot(mgic_op op, mgic_field x, mgic_field y, double *out) {
+  OPGUARD(NEED(x); NEED(y); NEED(out); *out = o.dotProduct(*x->f, *y->f));
+}
+MGIC_API int mgic_op_norm(mgic_op op, mgic_field x, int ord, double *out) {
+  OPGUARD(NEED(x); NEED(out); *out = o.norm(*x->f, ord));
+}
+MGIC_API int mgic_op_bicgstab(mgic_op op, mgic_field phi, mgic_field rhs, int h,
+                              const mgic_mg_params *p, int *iters) {
+  OPGUARD({
+    NEED(phi);
+    NEED(rhs);
+    BiCGStabSolver s;
+    s.prm = to_mg(p).bicg;
+    const int it = s.solve(o, *phi->f, *rhs->f, h != 0);
+    if (iters) *iters = it;
+  });
+}
+
+// ---------------------------------------------------------------- multigrid
+MGIC_API int mgic_mg_create(mgic_factory f, const mgic_mg_params *p, mgic_mg *out) {
+  return guard([&] {
+    NEED(f);
+    NEED(out);
+    auto *h = new mgic_mg_s;
+    try {
+      h->amg.define(f->f, to_mg(p));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+MGIC_API int mgic_mg_destroy(mgic_mg mg) {
+  return guard([&] { delete mg; });
+}
+MGIC_API int mgic_mg_num_depths(mgic_mg mg, int *n) {
+  return guard([&] {
+    NEED(mg);
+    NEED(n);
+    *n = mg->amg.mg.depths();
+  });
+}
+MGIC_API int mgic_mg_op(mgic_mg mg, int depth, mgic_op *out) {
+  return guard([&] {
+    NEED(mg);
+    NEED(out);
+    MGIC_CHECK(depth >= 0 && depth < mg->amg.mg.depths(), "bad depth");
+    auto *h = new mgic_op_s;
+    h->op = &mg->amg.mg.op(depth);
+    *out = h;
+  });
+}
+MGIC_API int mgic_mg_level_field(mgic_mg mg, int depth, int which, mgic_field *out) {
+  return guard([&] {
+    NEED(mg);
+    NEED(out);
+    MGIC_CHECK(depth >= 1 && depth < mg->amg.mg.depths(), "bad depth (internal fields exist for depth >= 1)");
+    LevelData *ld = which == 0 ? mg->amg.mg.corr(depth) : mg->amg.mg.resid(depth);
+    MGIC_CHECK(ld != nullptr, "field not allocated");
+    *out = borrowed_field(ld);
+  });
+}
+MGIC_API int mgic_mg_one_cycle(mgic_mg mg, mgic_field e, mgic_field r) {
+  return guard([&] {
+    NEED(mg);
+    NEED(e);
+    NEED(r);
+    mg->amg.mg.oneCycle(*e->f, *r->f);
+  });
+}
+MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
+                               int norm_type, int h, double *norm) {
+  return guard([&] {
+    NEED(mg);
+    NEED(phi);
+    NEED(rhs);
+    NEED(resid);
+    const double v = mg->amg.iteration(*phi->f, *rhs->f, *resid->f, norm_type, h != 0);
+    if (norm) *norm = v;
+  });
+}
+MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
+                                   int norm_type, int h, double *norm) {
+  return guard([&] {
+    NEED(mg);
+    NEED(phi);
+    NEED(rhs);
+    NEED(resid);
+    const double v = mg->amg.initResidual(*phi->f, *rhs->f, *resid->f, norm_type, h != 0);
+    if (norm) *norm = v;
+  });
+}
+
+MGIC_API int mgic_prof_smoother(int enable, long min_cells) {
+  return guard([&] { prof_enable(enable != 0, min_cells); });
+}
+MGIC_API int mgic_prof_smoother_read(int *launches, double *total_ms) {
+  return guard([&] {
+    double t = 0.0;
+    const int n = prof_read(&t);
+    if (launches) *launches = n;
+    if (total_ms) *total_ms = t;
+  });
+}
+
+}  // extern "C"

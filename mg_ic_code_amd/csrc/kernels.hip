@@ -1,0 +1,531 @@
+// kernels.hip -- gfx950 (CDNA4) kernels of the multigrid V-cycle hot path.
+//
+// Arithmetic restates Source/VariableCoeffPoissonOperatorF.ChF statement by
+// statement (cited per kernel); the library is built with
+// -ffp-contract=off so every result is bit-identical to the CPU oracle.
+// These are HBM-streaming stencils (~0.3 flop/byte): no MFMA, 64-wide
+// wavefronts along x so every wave touches whole 128-byte lines.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+namespace mgic {
+namespace kern {
+
+namespace {
+
+constexpr int TX = 64;  // one wavefront along x
+constexpr int TY = 4;   // 4 waves per block
+
+__device__ __forceinline__ double ghost_of(int mode, double c, double near) {
+  // DiriBC order 1: 2*value - near (c = 2*value); NeumBC: near (+ isign*dx*value)
+  return mode == kBcDirichlet ? (c - near) : (mode == kBcNeumannHom ? near : near + c);
+}
+
+// 7-point Laplacian (.ChF:111-120) with the domain BC folded in: a ghost on
+// a domain face is the BC image of the adjacent valid cell, which is the
+// centre cell itself -- exactly what ParseBC would have written there
+// before this pass (SetBCs.cpp:49-131).
+__device__ __forceinline__ double lap7(const double *__restrict__ u, long idx, double c, int i,
+                                       int j, int k, const BoxArgs &g) {
+  double xm = u[idx - 1], xp = u[idx + 1];
+  double ym = u[idx - g.sy], yp = u[idx + g.sy];
+  double zm = u[idx - g.sz], zp = u[idx + g.sz];
+  if (i == 0 && g.bcm[0]) xm = ghost_of(g.bcm[0], g.bcc[0], c);
+  if (i == g.nx - 1 && g.bcm[1]) xp = ghost_of(g.bcm[1], g.bcc[1], c);
+  if (j == 0 && g.bcm[2]) ym = ghost_of(g.bcm[2], g.bcc[2], c);
+  if (j == g.ny - 1 && g.bcm[3]) yp = ghost_of(g.bcm[3], g.bcc[3], c);
+  if (k == 0 && g.bcm[4]) zm = ghost_of(g.bcm[4], g.bcc[4], c);
+  if (k == g.nz - 1 && g.bcm[5]) zp = ghost_of(g.bcm[5], g.bcc[5], c);
+  const double tx = (xp + xm) - 2.0 * c;
+  const double ty = (yp + ym) - 2.0 * c;
+  const double tz = (zp + zm) - 2.0 * c;
+  return (tx + ty) + tz;
+}
+
+template <bool LAM_MEM>
+__global__ __launch_bounds__(256) void k_gsrb(double *__restrict__ u,
+                                              const double *__restrict__ rhs,
+                                              const double *__restrict__ a,
+                                              const double *__restrict__ b,
+                                              const double *__restrict__ lam, const BoxArgs g,
+                                              const StencilCoefs s, int colour) {
+  const int p = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (j >= g.ny) return;
+  // cells with (i+j+k) % 2 == redBlack in global indices (.ChF:98-106)
+  const int i = 2 * p + ((g.glo[0] + g.glo[1] + j + g.glo[2] + k + colour) & 1);
+  if (i >= g.nx) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  const double uc = u[idx];
+  const double av = a[idx];
+  double lofdpsi = s.alpha * av * uc;           // .ChF:107-108
+  double ldpsi = lap7(u, idx, uc, i, j, k, g);  // .ChF:111-120
+  ldpsi = ldpsi * s.dxinv * b[idx];             // .ChF:122
+  lofdpsi = lofdpsi - s.beta * ldpsi;           // .ChF:124
+  double l;
+  if (LAM_MEM) l = lam[idx];
+  else l = 1.0 / (av * s.alpha + s.lamshift);   // .cpp:234-243
+  u[idx] = uc - l * (lofdpsi - rhs[idx]);       // .ChF:127-128
+}
+
+__global__ __launch_bounds__(256) void k_apply_op(double *__restrict__ lu,
+                                                  const double *__restrict__ u,
+                                                  const double *__restrict__ a,
+                                                  const double *__restrict__ b, const BoxArgs g,
+                                                  const StencilCoefs s) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  const double uc = u[idx];
+  const double lof = s.alpha * a[idx] * uc;                     // .ChF:211-212
+  double ldpsi = lap7(u, idx, uc, i, j, k, g);                   // .ChF:216-225
+  ldpsi = ldpsi * s.dxinv * s.beta * b[idx];                     // .ChF:227
+  lu[idx] = lof - ldpsi;                                         // .ChF:229
+}
+
+__global__ __launch_bounds__(256) void k_residual(double *__restrict__ r,
+                                                  const double *__restrict__ u,
+                                                  const double *__restrict__ rhs,
+                                                  const double *__restrict__ a,
+                                                  const double *__restrict__ b, const BoxArgs g,
+                                                  const StencilCoefs s) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  const double uc = u[idx];
+  const double res = rhs[idx] - s.alpha * a[idx] * uc;           // .ChF:314-316
+  double ldpsi = lap7(u, idx, uc, i, j, k, g);                   // .ChF:320-329
+  ldpsi = ldpsi * s.dxinv * s.beta * b[idx];                     // .ChF:331
+  r[idx] = res + ldpsi;                                          // .ChF:333
+}
+
+// One thread per coarse cell; the 8 fine children are visited in the
+// Fortran k,j,i order so the accumulation res = 0 + t1 + ... + t8
+// (.cpp:177 + .ChF:431-432) rounds exactly like the reference.
+__global__ __launch_bounds__(256) void k_restrict(double *__restrict__ rc, const BoxArgs cg,
+                                                  const double *__restrict__ u,
+                                                  const double *__restrict__ rhs,
+                                                  const double *__restrict__ a,
+                                                  const double *__restrict__ b, const BoxArgs fg,
+                                                  const StencilCoefs s, int accumulate) {
+  const int ci = blockIdx.x * TX + threadIdx.x;
+  const int cj = blockIdx.y * TY + threadIdx.y;
+  const int ck = blockIdx.z;
+  if (ci >= cg.nx || cj >= cg.ny) return;
+  const double denom = 2 * 2 * 2;  // .ChF:402
+  const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
+  double sum = accumulate ? rc[cidx] : 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * ci + ii, j = 2 * cj + jj, k = 2 * ck + kk;
+        const long idx = (long)i + (long)j * fg.sy + (long)k * fg.sz;
+        const double uc = u[idx];
+        double lofdpsi = s.alpha * a[idx] * uc;               // .ChF:411-412
+        double ldpsi = lap7(u, idx, uc, i, j, k, fg);          // .ChF:416-425
+        ldpsi = ldpsi * s.dxinv * s.beta * b[idx];             // .ChF:427
+        lofdpsi = lofdpsi - ldpsi;                             // .ChF:429
+        sum = sum + (rhs[idx] - lofdpsi) / denom;              // .ChF:431-432
+      }
+  rc[cidx] = sum;
+}
+
+struct ProlongArgs {
+  int avail_lo[3], avail_hi[3];
+};
+
+__global__ __launch_bounds__(256) void k_prolong(double *__restrict__ uf, const BoxArgs fg,
+                                                 const double *__restrict__ ec, const BoxArgs cg,
+                                                 const ProlongArgs pa, int type) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= fg.nx || j >= fg.ny) return;
+  const int f[3] = {i, j, k};
+  const int ic[3] = {i >> 1, j >> 1, k >> 1};  // fine boxes start on even cells
+  const long cidx = (long)ic[0] + (long)ic[1] * cg.sy + (long)ic[2] * cg.sz;
+  const double c0 = ec[cidx];
+  double e = c0;
+  if (type == 1) {
+    const long cs[3] = {1, cg.sy, cg.sz};
+    const int cn[3] = {cg.nx, cg.ny, cg.nz};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const bool has_lo = (ic[d] > 0) || pa.avail_lo[d];
+      const bool has_hi = (ic[d] < cn[d] - 1) || pa.avail_hi[d];
+      const bool upper = (f[d] & 1) != 0;
+      const double fac = upper ? 0.25 : -0.25;
+      const bool use_hi = upper ? has_hi : !has_lo;
+      const bool ok = has_lo || has_hi;
+      const double delta = use_hi ? (ec[cidx + cs[d]] - c0) : (c0 - ec[cidx - cs[d]]);
+      if (ok) e = e + delta * fac;
+    }
+  }
+  const long idx = (long)i + (long)j * fg.sy + (long)k * fg.sz;
+  uf[idx] = uf[idx] + e;
+}
+
+__global__ __launch_bounds__(256) void k_lambda(double *__restrict__ lam,
+                                                const double *__restrict__ a, const BoxArgs g,
+                                                const StencilCoefs s) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  double v = a[idx];   // copy   (.cpp:234)
+  v = v * s.alpha;     // mult   (.cpp:235)
+  v = v + s.lamshift;  // plus   (.cpp:240)
+  lam[idx] = 1.0 / v;  // invert (.cpp:243)
+}
+
+// [Chombo] AverageF.ChF AVERAGE / AVERAGEHARMONIC: the ratio^3 children of a
+// coarse cell summed in the k,j,i order of the refinement box, times
+// refScale = 1/ratio^3 (harmonic: reciprocals summed, result inverted).
+__global__ __launch_bounds__(256) void k_average(double *__restrict__ c, const BoxArgs cg,
+                                                 const double *__restrict__ f, const BoxArgs fg,
+                                                 int ratio, int harmonic) {
+  const int I = blockIdx.x * TX + threadIdx.x;
+  const int J = blockIdx.y * TY + threadIdx.y;
+  const int K = blockIdx.z;
+  if (I >= cg.nx || J >= cg.ny) return;
+  const double refScale = 1.0 / (ratio * ratio * ratio);
+  double sum = 0.0;
+  for (int kk = 0; kk < ratio; ++kk)
+    for (int jj = 0; jj < ratio; ++jj)
+      for (int ii = 0; ii < ratio; ++ii) {
+        const double v = f[(long)(ratio * I + ii) + (long)(ratio * J + jj) * fg.sy +
+                           (long)(ratio * K + kk) * fg.sz];
+        sum = sum + (harmonic ? 1.0 / v : v);
+      }
+  c[(long)I + (long)J * cg.sy + (long)K * cg.sz] =
+      harmonic ? 1.0 / (sum * refScale) : sum * refScale;
+}
+
+__global__ void k_fill_bc_face(double *__restrict__ u, const BoxArgs g, int face) {
+  const int dir = face >> 1, side = face & 1;
+  const int n[3] = {g.nx, g.ny, g.nz};
+  const int d1 = dir == 0 ? 1 : 0, d2 = dir == 2 ? 1 : 2;
+  const int a = blockIdx.x * blockDim.x + threadIdx.x;
+  const int bb = blockIdx.y;
+  if (a >= n[d1] || bb >= n[d2]) return;
+  int c[3];
+  c[dir] = side == 0 ? 0 : n[dir] - 1;
+  c[d1] = a;
+  c[d2] = bb;
+  const long s[3] = {1, g.sy, g.sz};
+  const long near = (long)c[0] + (long)c[1] * g.sy + (long)c[2] * g.sz;
+  const long gh = near + (side == 0 ? -s[dir] : s[dir]);
+  u[gh] = ghost_of(g.bcm[face], g.bcc[face], u[near]);
+}
+
+__global__ __launch_bounds__(256) void k_blas(int kind, double *__restrict__ x,
+                                              const double *__restrict__ y,
+                                              const double *__restrict__ z, double s, double t,
+                                              const BoxArgs g) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  switch (kind) {
+    case 0: x[idx] = y[idx]; break;                    // assign / copy
+    case 1: x[idx] = x[idx] + s * y[idx]; break;       // incr  (FArrayBox::plus(src, scale))
+    case 2: x[idx] = x[idx] * s; break;                // scale (FArrayBox::mult(scale))
+    case 3: x[idx] = x[idx] * y[idx]; break;           // mult  (FArrayBox::mult(src))
+    case 4: x[idx] = s * y[idx] + t * z[idx]; break;   // axby
+    default: x[idx] = s; break;                        // setVal
+  }
+}
+
+constexpr int RB = 256;
+
+__device__ __forceinline__ double red_op(int kind, double a, double b) {
+  return kind == 3 ? (a > b ? a : b) : a + b;
+}
+
+__global__ __launch_bounds__(RB) void k_reduce_partial(int kind, const double *__restrict__ x,
+                                                       const double *__restrict__ y,
+                                                       const BoxArgs g,
+                                                       double *__restrict__ partials) {
+  __shared__ double sm[RB];
+  const long ncell = (long)g.nx * g.ny * g.nz;
+  double acc = 0.0;
+  for (long t = (long)blockIdx.x * RB + threadIdx.x; t < ncell; t += (long)gridDim.x * RB) {
+    const int i = (int)(t % g.nx);
+    const long r = t / g.nx;
+    const int j = (int)(r % g.ny);
+    const int k = (int)(r / g.ny);
+    const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+    const double v = x[idx];
+    double term;
+    switch (kind) {
+      case 0: term = v * y[idx]; break;
+      case 1: term = fabs(v); break;
+      case 2: term = v * v; break;
+      default: term = fabs(v); break;
+    }
+    acc = red_op(kind, acc, term);
+  }
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = RB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sm[threadIdx.x] = red_op(kind, sm[threadIdx.x], sm[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = sm[0];
+}
+
+__global__ __launch_bounds__(RB) void k_reduce_final(int kind, const double *__restrict__ p,
+                                                     int n, double *__restrict__ out) {
+  __shared__ double sm[RB];
+  double acc = 0.0;
+  for (int t = threadIdx.x; t < n; t += RB) acc = red_op(kind, acc, p[t]);
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = RB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sm[threadIdx.x] = red_op(kind, sm[threadIdx.x], sm[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = sm[0];
+}
+
+__global__ __launch_bounds__(256) void k_copy_items(const CopyItem *__restrict__ items,
+                                                    double *const *__restrict__ src_tab,
+                                                    const double *__restrict__ src_buf,
+                                                    double *const *__restrict__ dst_tab,
+                                                    double *__restrict__ dst_buf) {
+  const CopyItem it = items[blockIdx.y];
+  const long n = (long)it.nx * it.ny * it.nz;
+  const double *src = it.src >= 0 ? src_tab[it.src] : src_buf;
+  double *dst = it.dst >= 0 ? dst_tab[it.dst] : dst_buf;
+  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (long)gridDim.x * blockDim.x) {
+    const int i = (int)(t % it.nx);
+    const long r = t / it.nx;
+    const int j = (int)(r % it.ny);
+    const int k = (int)(r / it.ny);
+    dst[it.doff + i + j * it.dsy + k * it.dsz] = src[it.soff + i + j * it.ssy + k * it.ssz];
+  }
+}
+
+// ---- input generator: SetLevelData.cpp / SetBinaryBH.H / MyPhiFunction.H
+__device__ double bh_phi(const BhParams &p, double x, double y, double z) {
+  const double r2 = x * x + y * y + z * z;  // MyPhiFunction.H:15
+  return p.phi_amplitude * exp(-r2 / p.phi_wavelength);
+}
+__device__ double bh_loc(int iv, double dx, double domlen) { return ((double)iv + 0.5) * dx - domlen / 2.0; }
+__device__ double bh_Aij(int i, int j, double r1, double r2, const double *n1, const double *n2,
+                         const double *J1, const double *J2, const double *P1, const double *P2) {
+  // SetBinaryBH.H:24-53
+  auto eps = [](int a, int b, int c) -> double {
+    if (a == 0 && b == 1 && c == 2) return 1.0;
+    if (a == 1 && b == 2 && c == 0) return 1.0;
+    if (a == 2 && b == 0 && c == 1) return 1.0;
+    if (a == 0 && b == 2 && c == 1) return -1.0;
+    if (a == 2 && b == 1 && c == 0) return -1.0;
+    if (a == 1 && b == 0 && c == 2) return -1.0;
+    return 0.0;
+  };
+  double Aij = 1.5 / r1 / r1 * (n1[i] * P1[j] + n1[j] * P1[i]) +
+               1.5 / r2 / r2 * (n2[i] * P2[j] + n2[j] * P2[i]);
+  for (int k = 0; k < 3; k++) {
+    Aij += 1.5 / r1 / r1 * (n1[i] * n1[j] - (double)(i == j)) * P1[k] * n1[k] +
+           1.5 / r2 / r2 * (n2[i] * n2[j] - (double)(i == j)) * P2[k] * n2[k];
+    for (int l = 0; l < 3; l++) {
+      Aij += -3.0 / r1 / r1 / r1 * (eps(i, l, k) * n1[j] + eps(j, l, k) * n1[i]) * n1[l] * J1[k] -
+             3.0 / r2 / r2 / r2 * (eps(i, l, k) * n2[j] + eps(j, l, k) * n2[i]) * n2[l] * J2[k];
+    }
+  }
+  return Aij;
+}
+
+__global__ __launch_bounds__(256) void k_binary_bh(double *__restrict__ acoef,
+                                                   double *__restrict__ rhs, const BoxArgs g,
+                                                   double dx, const BhParams p) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const int iv[3] = {g.glo[0] + i, g.glo[1] + j, g.glo[2] + k};
+  double loc[3];
+  for (int d = 0; d < 3; ++d) loc[d] = bh_loc(iv[d], dx, p.domlen[d]);
+  double rho_grad = 0.0;  // GETRHOGRADPHIF, SetLevelDataF.ChF:65-103
+  for (int d0 = 0; d0 < 3; ++d0) {
+    double lp[3], lm[3];
+    for (int d = 0; d < 3; ++d) {
+      lp[d] = bh_loc(iv[d] + (d == d0), dx, p.domlen[d]);
+      lm[d] = bh_loc(iv[d] - (d == d0), dx, p.domlen[d]);
+    }
+    const double dphidx = 0.5 / dx * (+bh_phi(p, lp[0], lp[1], lp[2]) - bh_phi(p, lm[0], lm[1], lm[2]));
+    rho_grad = rho_grad + 0.5 * dphidx * dphidx;
+  }
+  double l1[3] = {loc[0] - p.off1, loc[1], loc[2]}, l2[3] = {loc[0] - p.off2, loc[1], loc[2]};
+  const double r1 = sqrt(l1[0] * l1[0] + l1[1] * l1[1] + l1[2] * l1[2]);
+  const double r2 = sqrt(l2[0] * l2[0] + l2[1] * l2[1] + l2[2] * l2[2]);
+  const double n1[3] = {l1[0] / r1, l1[1] / r1, l1[2] / r1};
+  const double n2[3] = {l2[0] / r2, l2[1] / r2, l2[2] / r2};
+  const double J1[3] = {0.0, 0.0, p.spin1}, J2[3] = {0.0, 0.0, p.spin2};
+  const double P1[3] = {0.0, p.mom1, 0.0}, P2[3] = {0.0, p.mom2, 0.0};
+  const double A11 = bh_Aij(0, 0, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A22 = bh_Aij(1, 1, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A33 = bh_Aij(2, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A12 = bh_Aij(0, 1, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A13 = bh_Aij(0, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A23 = bh_Aij(1, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A2 = pow(A11, 2.0) + pow(A22, 2.0) + pow(A33, 2.0) + 2 * pow(A12, 2.0) +
+                    2 * pow(A13, 2.0) + 2 * pow(A23, 2.0);  // SetLevelData.cpp:312-317
+  const double rho = 0.5 * 0.0 * 0.0 + 0.0;
+  const double m = (2.0 / 3.0) * (p.constant_K * p.constant_K) - 16.0 * M_PI * p.G_Newton * rho;
+  const double psi_bh = p.m1 / r1 + p.m2 / r2;  // SetBinaryBH.H:85-99
+  const double psi_0 = 1.0 + psi_bh;
+  double lap = 0.0;  // GETLAPLACIANPSIF of psi == 1
+  for (int d0 = 0; d0 < 3; ++d0) lap = lap + 1.0 / dx / dx * (+1.0 * 1.0 - 2.0 * 1.0 + 1.0 * 1.0);
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  acoef[idx] = -0.625 * m * pow(psi_0, 4.0) - A2 * pow(psi_0, -8.0) +
+               2.0 * M_PI * p.G_Newton * rho_grad;  // SetLevelData.cpp:321-322
+  rhs[idx] = 0.125 * m * pow(psi_0, 5.0) - 0.125 * A2 * pow(psi_0, -7.0) -
+             2.0 * M_PI * p.G_Newton * rho_grad * psi_0 - lap;  // SetLevelData.cpp:121-124
+}
+
+inline dim3 grid_cells(int nx, int ny, int nz) {
+  return dim3((unsigned)((nx + TX - 1) / TX), (unsigned)((ny + TY - 1) / TY), (unsigned)nz);
+}
+const dim3 kBlock(TX, TY, 1);
+
+inline void check_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(kHipErr, std::string("kernel launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace
+
+void gsrb_pass(double *u, const double *rhs, const double *a, const double *b, const double *lam,
+               const BoxArgs &g, const StencilCoefs &s, int colour, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  const int npairs = (g.nx + 1) / 2;
+  const dim3 grid((unsigned)((npairs + TX - 1) / TX), (unsigned)((g.ny + TY - 1) / TY),
+                  (unsigned)g.nz);
+  if (lam) k_gsrb<true><<<grid, kBlock, 0, st>>>(u, rhs, a, b, lam, g, s, colour);
+  else k_gsrb<false><<<grid, kBlock, 0, st>>>(u, rhs, a, b, nullptr, g, s, colour);
+  check_launch();
+}
+
+bool gsrb_sweep_fused_supported(const BoxArgs &) { return false; }
+void gsrb_sweep_fused(double *, const double *, const double *, const double *, const BoxArgs &,
+                      const StencilCoefs &, hipStream_t) {
+  throw Error(kState, "fused sweep not available");
+}
+
+void apply_op(double *lu, const double *u, const double *a, const double *b, const BoxArgs &g,
+              const StencilCoefs &s, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_apply_op<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(lu, u, a, b, g, s);
+  check_launch();
+}
+
+void residual(double *r, const double *u, const double *rhs, const double *a, const double *b,
+              const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_residual<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
+  check_launch();
+}
+
+void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const double *rhs,
+                       const double *a, const double *b, const BoxArgs &fg, const StencilCoefs &s,
+                       hipStream_t st, bool accumulate) {
+  if (cg.nx <= 0 || cg.ny <= 0 || cg.nz <= 0) return;
+  k_restrict<<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s,
+                                                                  accumulate ? 1 : 0);
+  check_launch();
+}
+
+void prolong(double *uf, const BoxArgs &fg, const double *ec, const BoxArgs &cg,
+             const int avail_lo[3], const int avail_hi[3], int type, hipStream_t st) {
+  if (fg.nx <= 0 || fg.ny <= 0 || fg.nz <= 0) return;
+  ProlongArgs pa;
+  for (int d = 0; d < 3; ++d) {
+    pa.avail_lo[d] = avail_lo[d];
+    pa.avail_hi[d] = avail_hi[d];
+  }
+  k_prolong<<<grid_cells(fg.nx, fg.ny, fg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa, type);
+  check_launch();
+}
+
+void lambda(double *lam, const double *a, const BoxArgs &g, const StencilCoefs &s,
+            hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_lambda<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(lam, a, g, s);
+  check_launch();
+}
+
+void average(double *c, const BoxArgs &cg, const double *f, const BoxArgs &fg, int ratio,
+             int harmonic, hipStream_t st) {
+  if (cg.nx <= 0 || cg.ny <= 0 || cg.nz <= 0) return;
+  k_average<<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(c, cg, f, fg, ratio, harmonic);
+  check_launch();
+}
+
+void fill_bc(double *u, const BoxArgs &g, hipStream_t st) {
+  const int n[3] = {g.nx, g.ny, g.nz};
+  for (int face = 0; face < 6; ++face) {
+    if (!g.bcm[face]) continue;
+    const int dir = face >> 1;
+    const int d1 = dir == 0 ? 1 : 0, d2 = dir == 2 ? 1 : 2;
+    const dim3 grid((unsigned)((n[d1] + 255) / 256), (unsigned)n[d2], 1);
+    k_fill_bc_face<<<grid, dim3(256, 1, 1), 0, st>>>(u, g, face);
+    check_launch();
+  }
+}
+
+void blas(int kind, double *x, const double *y, const double *z, double s, double t,
+          const BoxArgs &g, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_blas<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(kind, x, y, z, s, t, g);
+  check_launch();
+}
+
+int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
+                   double *partials, hipStream_t st) {
+  const long ncell = (long)g.nx * g.ny * g.nz;
+  if (ncell <= 0) return 0;
+  long nb = (ncell + RB - 1) / RB;
+  if (nb > kMaxPartsPerBox) nb = kMaxPartsPerBox;
+  k_reduce_partial<<<dim3((unsigned)nb), dim3(RB), 0, st>>>(kind, x, y, g, partials);
+  check_launch();
+  return (int)nb;
+}
+
+void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st) {
+  k_reduce_final<<<dim3(1), dim3(RB), 0, st>>>(kind, partials, n, out);
+  check_launch();
+}
+
+void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *const *src_tab,
+                const double *src_buf, double *const *dst_tab, double *dst_buf, hipStream_t st) {
+  if (nitems <= 0 || max_cells <= 0) return;
+  long bx = (max_cells + 255) / 256;
+  if (bx > 1024) bx = 1024;
+  k_copy_items<<<dim3((unsigned)bx, (unsigned)nitems), dim3(256), 0, st>>>(d_items, src_tab, src_buf,
+                                                                            dst_tab, dst_buf);
+  check_launch();
+}
+
+void binary_bh_coefs(double *acoef, double *rhs, const BoxArgs &g, double dx, const BhParams &p,
+                     hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_binary_bh<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(acoef, rhs, g, dx, p);
+  check_launch();
+}
+
+}  // namespace kern
+}  // namespace mgic

@@ -1,0 +1,77 @@
+// kernels.hpp -- host-side launchers for the gfx950 kernels in kernels.hip.
+//
+// Every stencil launcher works on ONE box: all arrays share the box's
+// FabGeom (strides sy, sz; pointers point at the valid-lo cell) and the
+// domain boundary is folded in through BoxArgs::bcm/bcc (see mgic_core.hpp).
+#pragma once
+
+#include "mgic_core.hpp"
+
+namespace mgic {
+namespace kern {
+
+// GSRBHELMHOLTZVC3D (.ChF:56-139): one colour pass over the valid region.
+// lam == nullptr: lambda = 1/(alpha*a + 2*3*beta/dx^2) is recomputed in
+// registers (bit-identical to resetLambda, .cpp:234-243) instead of read.
+void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
+               const double *lam, const BoxArgs &g, const StencilCoefs &s, int colour,
+               hipStream_t st);
+// Fused red+black sweep (both passes of one levelGSRB, .cpp:290-331) in one
+// launch, staged through LDS; bit-identical to two gsrb_pass calls.  Only
+// valid when every face is either a domain face (bc folded) or has its
+// ghost already exchanged and the neighbour will not change during the
+// sweep -- i.e. a single box per level (checked by the caller).
+bool gsrb_sweep_fused_supported(const BoxArgs &g);
+void gsrb_sweep_fused(double *u, const double *rhs, const double *a, const double *b,
+                      const BoxArgs &g, const StencilCoefs &s, hipStream_t st);
+// VCCOMPUTEOP3D (.ChF:181-237)
+void apply_op(double *lu, const double *u, const double *a, const double *b,
+              const BoxArgs &g, const StencilCoefs &s, hipStream_t st);
+// VCCOMPUTERES3D (.ChF:283-339)
+void residual(double *r, const double *u, const double *rhs, const double *a,
+              const double *b, const BoxArgs &g, const StencilCoefs &s, hipStream_t st);
+// RESTRICTRESVC3D (.ChF:379-437) incl. setVal(0) on the coarse valid box
+// accumulate=true adds into rc like the bare Fortran kernel (whose caller
+// zeroes rc first); false writes 0 + sum, i.e. setVal(0) + kernel.
+void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const double *rhs,
+                       const double *a, const double *b, const BoxArgs &fg,
+                       const StencilCoefs &s, hipStream_t st, bool accumulate = false);
+// prolongIncrement: uf += P(ec); type 0 constant, 1 linear
+void prolong(double *uf, const BoxArgs &fg, const double *ec, const BoxArgs &cg,
+             const int avail_lo[3], const int avail_hi[3], int type, hipStream_t st);
+// resetLambda (.cpp:220-249)
+void lambda(double *lam, const double *a, const BoxArgs &g, const StencilCoefs &s,
+            hipStream_t st);
+// CoarseAverage arithmetic / harmonic with refinement ratio `ratio`
+void average(double *c, const BoxArgs &cg, const double *f, const BoxArgs &fg, int ratio,
+             int harmonic, hipStream_t st);
+// ParseBC: write the domain-face ghost layers (modes from g.bcm)
+void fill_bc(double *u, const BoxArgs &g, hipStream_t st);
+
+// BLAS-1 over the valid region: kind 0 x=y, 1 x=x+s*y, 2 x=x*s, 3 x=x*y,
+// 4 x = s*y + t*z, 5 x = s (setVal)
+void blas(int kind, double *x, const double *y, const double *z, double s, double t,
+          const BoxArgs &g, hipStream_t st);
+// Deterministic reductions: kind 0 dot(x,y), 1 sum|x|, 2 sum x^2, 3 max|x|.
+// Writes nparts partials at partials[0..nparts); returns nparts.
+int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
+                   double *partials, hipStream_t st);
+constexpr int kMaxPartsPerBox = 256;
+void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st);
+
+// batched rectangular copies (exchange / copyTo / pack / unpack)
+void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *const *src_tab,
+                const double *src_buf, double *const *dst_tab, double *dst_buf,
+                hipStream_t st);
+
+// SetLevelData.cpp set_a_coef/set_rhs at psi = 1 (input generator)
+struct BhParams {
+  double domlen[3];
+  double G_Newton, phi_amplitude, phi_wavelength;
+  double m1, m2, spin1, spin2, off1, off2, mom1, mom2, constant_K;
+};
+void binary_bh_coefs(double *acoef, double *rhs, const BoxArgs &g, double dx,
+                     const BhParams &p, hipStream_t st);
+
+}  // namespace kern
+}  // namespace mgic

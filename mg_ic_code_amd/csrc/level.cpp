@@ -1,0 +1,322 @@
+// level.cpp -- Comm, Grid, CopyPlan, LevelData (see level.hpp).
+#include "level.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace mgic {
+
+// ------------------------------------------------------------------ Comm
+Comm::Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl)
+    : rank_(rank), size_(size) {
+  MGIC_CHECK(size >= 1 && rank >= 0 && rank < size, "bad rank/size");
+  MGIC_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  own_stream_ = true;
+  if (size > 1 || force_rccl) {
+    MGIC_CHECK(id != nullptr, "RCCL unique id required for size > 1");
+    MGIC_NCCL(ncclCommInitRank(&nccl_, size, *id, rank));
+  }
+  MGIC_HIP(hipMalloc(&d_result_, 2 * sizeof(double)));
+  MGIC_HIP(hipHostMalloc(&h_result_, 2 * sizeof(double), hipHostMallocDefault));
+}
+
+Comm::~Comm() {
+  if (nccl_) ncclCommDestroy(nccl_);
+  if (d_partials_) (void)hipFree(d_partials_);
+  if (d_result_) (void)hipFree(d_result_);
+  if (h_result_) (void)hipHostFree(h_result_);
+  if (own_stream_ && stream_) (void)hipStreamDestroy(stream_);
+}
+
+double *Comm::d_partials(int n) {
+  if (n > n_partials_) {
+    if (d_partials_) MGIC_HIP(hipFree(d_partials_));
+    n_partials_ = std::max(n, 4096);
+    MGIC_HIP(hipMalloc(&d_partials_, sizeof(double) * (size_t)n_partials_));
+  }
+  return d_partials_;
+}
+
+void Comm::allreduce(double *d_val, int op) {
+  if (!nccl_ || size_ == 1) return;
+  MGIC_NCCL(ncclAllReduce(d_val, d_val, 1, ncclDouble, op == 1 ? ncclMax : ncclSum, nccl_, stream_));
+}
+
+// ------------------------------------------------------------------ Grid
+Grid::Grid(std::shared_ptr<Comm> c, const Box &dom, const bool per[3], double dx_,
+           const std::vector<Box> &bx, const std::vector<int> &own)
+    : comm(std::move(c)), domain(dom), dx(dx_), boxes(bx), owners(own) {
+  MGIC_CHECK(boxes.size() == owners.size(), "boxes/owners size mismatch");
+  for (int d = 0; d < 3; ++d) periodic[d] = per[d];
+  for (size_t b = 0; b < boxes.size(); ++b) {
+    MGIC_CHECK(!boxes[b].empty(), "empty box");
+    MGIC_CHECK(domain.contains(boxes[b]), "box outside domain");
+    MGIC_CHECK(owners[b] >= 0 && owners[b] < comm->size(), "bad owner rank");
+    if (owners[b] == comm->rank()) {
+      local.push_back((int)b);
+      geom.push_back(FabGeom::make(boxes[b]));
+    }
+  }
+}
+
+long Grid::max_cells_local() const {
+  long m = 0;
+  for (auto &g : geom) m = std::max(m, g.valid.ncells());
+  return m;
+}
+
+bool Grid::tiles_domain() const {
+  long tot = 0;
+  for (auto &b : boxes) tot += b.ncells();
+  if (tot != domain.ncells()) return false;
+  for (size_t a = 0; a < boxes.size(); ++a)
+    for (size_t b = a + 1; b < boxes.size(); ++b)
+      if (!boxes[a].intersect(boxes[b]).empty()) return false;
+  return true;
+}
+
+bool Grid::coarsenable(int r) const {
+  for (auto &b : boxes)
+    if (!b.coarsenable(r)) return false;
+  return true;
+}
+
+std::shared_ptr<Grid> Grid::coarsened(int r) const {
+  std::vector<Box> cb;
+  for (auto &b : boxes) cb.push_back(b.coarsened(r));
+  return std::make_shared<Grid>(comm, domain.coarsened(r), periodic, dx * (double)r, cb, owners);
+}
+
+CopyPlan &Grid::exchange_plan() {
+  if (!exchange_) exchange_ = build_copy_plan(*this, *this, false, true);
+  return *exchange_;
+}
+
+BoxArgs Grid::box_args_plain(int n) const {
+  BoxArgs a{};
+  const FabGeom &g = geom[n];
+  a.nx = g.nx;
+  a.ny = g.ny;
+  a.nz = g.nz;
+  a.sy = g.sy;
+  a.sz = g.sz;
+  for (int d = 0; d < 3; ++d) a.glo[d] = g.valid.lo[d];
+  for (int f = 0; f < 6; ++f) {
+    a.bcm[f] = kBcMemory;
+    a.bcc[f] = 0.0;
+  }
+  return a;
+}
+
+BoxArgs Grid::box_args(int n, const int bc_lo[3], const int bc_hi[3], double bc_value,
+                       bool homogeneous) const {
+  BoxArgs a = box_args_plain(n);
+  const Box &v = geom[n].valid;
+  const double val = homogeneous ? 0.0 : bc_value;  // ParseValue (SetBCs.cpp:42-47)
+  for (int dir = 0; dir < 3; ++dir) {
+    if (periodic[dir]) continue;  // SetBCs.cpp:65
+    for (int side = 0; side < 2; ++side) {
+      const bool at_dom = side == 0 ? v.lo[dir] == domain.lo[dir] : v.hi[dir] == domain.hi[dir];
+      if (!at_dom) continue;  // SetBCs.cpp:68, :98
+      const int flag = side == 0 ? bc_lo[dir] : bc_hi[dir];
+      const int f = 2 * dir + side;
+      const int isign = side == 0 ? -1 : 1;
+      if (flag == 0) {  // DiriBC, order 1
+        a.bcm[f] = kBcDirichlet;
+        a.bcc[f] = 2.0 * val;
+      } else if (flag == 1) {  // NeumBC
+        if (homogeneous) {
+          a.bcm[f] = kBcNeumannHom;
+        } else {
+          a.bcm[f] = kBcNeumann;
+          a.bcc[f] = (double)isign * dx * val;
+        }
+      } else if (flag == 2) {  // periodic flag on a non-periodic domain: no fill
+        a.bcm[f] = kBcMemory;
+      } else {
+        throw Error(kBadArg, "bogus bc flag");  // MayDay::Error (SetBCs.cpp:94, :123)
+      }
+    }
+  }
+  return a;
+}
+
+// ------------------------------------------------------------------ CopyPlan
+std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool with_valid,
+                                          bool with_faces) {
+  auto plan = std::make_unique<CopyPlan>();
+  const int me = dst.comm->rank();
+  std::vector<int> sloc(src.boxes.size(), -1), dloc(dst.boxes.size(), -1);
+  for (int n = 0; n < src.nlocal(); ++n) sloc[src.local[n]] = n;
+  for (int n = 0; n < dst.nlocal(); ++n) dloc[dst.local[n]] = n;
+  int len[3];
+  for (int d = 0; d < 3; ++d) len[d] = dst.domain.size(d);
+  const bool self_msg = dst.comm->self_messages() && dst.comm->uses_rccl();
+  for (size_t db = 0; db < dst.boxes.size(); ++db) {
+    const Box &dv = dst.boxes[db];
+    std::vector<Box> regions;
+    if (with_valid) regions.push_back(dv);
+    if (with_faces)
+      for (int dir = 0; dir < 3; ++dir)
+        for (int side = 0; side < 2; ++side) regions.push_back(dv.adj_cell(dir, side));
+    const int od = dst.owners[db];
+    for (const Box &R : regions) {
+      for (size_t sb = 0; sb < src.boxes.size(); ++sb) {
+        const int os = src.owners[sb];
+        if (od != me && os != me) continue;
+        for (int sz = -1; sz <= 1; ++sz)
+          for (int sy = -1; sy <= 1; ++sy)
+            for (int sx = -1; sx <= 1; ++sx) {
+              if ((sx && !dst.periodic[0]) || (sy && !dst.periodic[1]) || (sz && !dst.periodic[2]))
+                continue;
+              const int sh[3] = {sx * len[0], sy * len[1], sz * len[2]};
+              const Box X = R.intersect(src.boxes[sb].shifted(sh));
+              if (X.empty()) continue;
+              CopyItem it{};
+              it.nx = X.size(0);
+              it.ny = X.size(1);
+              it.nz = X.size(2);
+              const long n = X.ncells();
+              if (od == me) {
+                const FabGeom &g = dst.geom[dloc[db]];
+                it.dst = dloc[db];
+                it.doff = g.offset(X.lo[0], X.lo[1], X.lo[2]);
+                it.dsy = g.sy;
+                it.dsz = g.sz;
+              }
+              if (os == me) {
+                const FabGeom &g = src.geom[sloc[sb]];
+                it.src = sloc[sb];
+                it.soff = g.offset(X.lo[0] - sh[0], X.lo[1] - sh[1], X.lo[2] - sh[2]);
+                it.ssy = g.sy;
+                it.ssz = g.sz;
+              }
+              if (od == me && os == me && !self_msg) {
+                plan->local_.push_back(it);
+                continue;
+              }
+              if (os == me) {  // send to od (possibly ourselves through RCCL)
+                CopyItem p = it;
+                p.dst = -1;
+                p.pad = od;
+                p.doff = plan->send_cnt_[od];
+                p.dsy = it.nx;
+                p.dsz = (long)it.nx * it.ny;
+                plan->send_cnt_[od] += n;
+                plan->pack_.push_back(p);
+              }
+              if (od == me) {  // receive from os
+                CopyItem u = it;
+                u.src = -1;
+                u.pad = os;
+                u.soff = plan->recv_cnt_[os];
+                u.ssy = it.nx;
+                u.ssz = (long)it.nx * it.ny;
+                plan->recv_cnt_[os] += n;
+                plan->unpack_.push_back(u);
+              }
+            }
+      }
+    }
+  }
+  plan->finalize();
+  return plan;
+}
+
+CopyPlan::~CopyPlan() {
+  if (d_local_) (void)hipFree(d_local_);
+  if (d_pack_) (void)hipFree(d_pack_);
+  if (d_unpack_) (void)hipFree(d_unpack_);
+  if (sendbuf_) (void)hipFree(sendbuf_);
+  if (recvbuf_) (void)hipFree(recvbuf_);
+}
+
+static CopyItem *upload_items(const std::vector<CopyItem> &v, long &maxc) {
+  maxc = 0;
+  for (auto &it : v) maxc = std::max(maxc, (long)it.nx * it.ny * it.nz);
+  if (v.empty()) return nullptr;
+  CopyItem *d = nullptr;
+  MGIC_HIP(hipMalloc(&d, sizeof(CopyItem) * v.size()));
+  MGIC_HIP(hipMemcpy(d, v.data(), sizeof(CopyItem) * v.size(), hipMemcpyHostToDevice));
+  return d;
+}
+
+void CopyPlan::finalize() {
+  if (final_) return;
+  long off = 0;
+  for (auto &kv : send_cnt_) {
+    send_off_[kv.first] = off;
+    off += kv.second;
+  }
+  send_total_ = off;
+  off = 0;
+  for (auto &kv : recv_cnt_) {
+    recv_off_[kv.first] = off;
+    off += kv.second;
+  }
+  recv_total_ = off;
+  for (auto &it : pack_) it.doff += send_off_[it.pad];
+  for (auto &it : unpack_) it.soff += recv_off_[it.pad];
+  d_local_ = upload_items(local_, max_local_);
+  d_pack_ = upload_items(pack_, max_pack_);
+  d_unpack_ = upload_items(unpack_, max_unpack_);
+  if (send_total_) MGIC_HIP(hipMalloc(&sendbuf_, sizeof(double) * (size_t)send_total_));
+  if (recv_total_) MGIC_HIP(hipMalloc(&recvbuf_, sizeof(double) * (size_t)recv_total_));
+  final_ = true;
+}
+
+void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_tab,
+                       hipStream_t st) {
+  if (!local_.empty())
+    kern::copy_items(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
+  if (send_total_ || recv_total_) {
+    MGIC_CHECK(comm.uses_rccl(), "remote copies need an RCCL communicator");
+    if (!pack_.empty())
+      kern::copy_items(d_pack_, (int)pack_.size(), max_pack_, src_tab, nullptr, nullptr, sendbuf_, st);
+    MGIC_NCCL(ncclGroupStart());
+    for (auto &kv : send_cnt_)
+      MGIC_NCCL(ncclSend(sendbuf_ + send_off_[kv.first], (size_t)kv.second, ncclDouble, kv.first,
+                         comm.nccl(), st));
+    for (auto &kv : recv_cnt_)
+      MGIC_NCCL(ncclRecv(recvbuf_ + recv_off_[kv.first], (size_t)kv.second, ncclDouble, kv.first,
+                         comm.nccl(), st));
+    MGIC_NCCL(ncclGroupEnd());
+    if (!unpack_.empty())
+      kern::copy_items(d_unpack_, (int)unpack_.size(), max_unpack_, nullptr, recvbuf_, dst_tab,
+                       nullptr, st);
+  }
+}
+
+// ------------------------------------------------------------------ LevelData
+LevelData::LevelData(std::shared_ptr<Grid> g) : grid(std::move(g)) {
+  const int n = grid->nlocal();
+  base.resize(n, nullptr);
+  p.resize(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    const FabGeom &fg = grid->geom[i];
+    MGIC_HIP(hipMalloc(&base[i], sizeof(double) * (size_t)fg.total));
+    MGIC_HIP(hipMemset(base[i], 0, sizeof(double) * (size_t)fg.total));
+    p[i] = base[i] + fg.origin;
+  }
+  MGIC_HIP(hipMalloc(&d_tab, sizeof(double *) * (size_t)std::max(n, 1)));
+  if (n) MGIC_HIP(hipMemcpy(d_tab, p.data(), sizeof(double *) * (size_t)n, hipMemcpyHostToDevice));
+}
+
+LevelData::~LevelData() {
+  for (double *b : base)
+    if (b) (void)hipFree(b);
+  if (d_tab) (void)hipFree(d_tab);
+}
+
+void LevelData::set_zero_all(hipStream_t st) {
+  for (int i = 0; i < (int)base.size(); ++i)
+    MGIC_HIP(hipMemsetAsync(base[i], 0, sizeof(double) * (size_t)grid->geom[i].total, st));
+}
+
+void LevelData::exchange(hipStream_t st) {
+  CopyPlan &pl = grid->exchange_plan();
+  if (pl.empty()) return;
+  pl.execute(*grid->comm, d_tab, d_tab, st);
+}
+
+}  // namespace mgic

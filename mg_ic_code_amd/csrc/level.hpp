@@ -1,0 +1,139 @@
+// level.hpp -- layouts, level data and ghost exchange (the Chombo
+// DisjointBoxLayout / LevelData<FArrayBox> / Copier layer the reference
+// operator relies on), MI355X-first:
+//   * one process per GPU; boxes are owned by ranks; a rank may own several
+//     boxes (tests run a multi-box decomposition on one GPU through the same
+//     code path);
+//   * the exchange is a precomputed CopyPlan: one batched kernel for
+//     same-rank copies and packing, one grouped RCCL send/recv per peer over
+//     xGMI, one batched unpack kernel -- no host round trip, capturable.
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <map>
+
+#include "kernels.hpp"
+#include "mgic_core.hpp"
+
+namespace mgic {
+
+#define MGIC_NCCL(x)                                                                  \
+  do {                                                                                \
+    ncclResult_t r_ = (x);                                                            \
+    if (r_ != ncclSuccess)                                                            \
+      throw ::mgic::Error(::mgic::kRcclErr,                                           \
+                          std::string("RCCL error ") + ncclGetErrorString(r_) + " in " #x); \
+  } while (0)
+
+// One process's view of the job: rank, size, RCCL communicator, stream.
+class Comm {
+ public:
+  Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl);
+  ~Comm();
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  bool uses_rccl() const { return nccl_ != nullptr; }
+  // route same-rank copies through RCCL self send/recv (tests the remote
+  // path on one GPU)
+  bool self_messages() const { return self_messages_; }
+  void set_self_messages(bool v) { self_messages_ = v; }
+  ncclComm_t nccl() const { return nccl_; }
+  hipStream_t stream() const { return stream_; }
+  void set_stream(hipStream_t s) { stream_ = s; }
+  // in-place allreduce of one device double (op: 0 sum, 1 max)
+  void allreduce(double *d_val, int op);
+  // scratch for reductions (device partials + result, pinned host result)
+  double *d_partials(int n);
+  double *d_result() const { return d_result_; }
+  double *h_result() const { return h_result_; }
+
+ private:
+  int rank_, size_;
+  bool self_messages_ = false;
+  ncclComm_t nccl_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
+  double *d_partials_ = nullptr;
+  int n_partials_ = 0;
+  double *d_result_ = nullptr;
+  double *h_result_ = nullptr;
+};
+
+// A precomputed set of rectangular copies between two LevelData layouts
+// (possibly the same), split into same-rank copies and per-peer messages.
+class CopyPlan {
+ public:
+  ~CopyPlan();
+  void finalize();  // upload item tables, allocate message buffers
+  // src_tab / dst_tab: device tables of valid-lo pointers per local box
+  void execute(Comm &comm, double *const *src_tab, double *const *dst_tab, hipStream_t st);
+  bool empty() const { return local_.empty() && pack_.empty() && unpack_.empty(); }
+
+  std::vector<CopyItem> local_, pack_, unpack_;
+  std::map<int, long> send_cnt_, recv_cnt_;  // per peer rank, doubles
+  std::map<int, long> send_off_, recv_off_;
+  long send_total_ = 0, recv_total_ = 0;
+
+ private:
+  CopyItem *d_local_ = nullptr, *d_pack_ = nullptr, *d_unpack_ = nullptr;
+  long max_local_ = 0, max_pack_ = 0, max_unpack_ = 0;
+  double *sendbuf_ = nullptr, *recvbuf_ = nullptr;
+  bool final_ = false;
+};
+
+// DisjointBoxLayout + ProblemDomain + dx at one level.
+class Grid {
+ public:
+  Grid(std::shared_ptr<Comm> comm, const Box &domain, const bool periodic[3], double dx,
+       const std::vector<Box> &boxes, const std::vector<int> &owners);
+  std::shared_ptr<Comm> comm;
+  Box domain;
+  bool periodic[3];
+  double dx;
+  std::vector<Box> boxes;    // global list
+  std::vector<int> owners;   // rank per box
+  std::vector<int> local;    // global indices of my boxes
+  std::vector<FabGeom> geom; // per local box
+  int nlocal() const { return (int)local.size(); }
+  long max_cells_local() const;
+  bool tiles_domain() const;  // boxes disjoint and covering the domain
+  bool coarsenable(int r) const;
+  std::shared_ptr<Grid> coarsened(int r) const;
+  // face ghost exchange plan (exchangeDefine(grids, Unit) + trimEdges)
+  CopyPlan &exchange_plan();
+  // BoxArgs of local box n with the face BC modes for (bc flags, value,
+  // homogeneous); faces that are not domain faces (or are periodic) get
+  // kBcMemory.
+  BoxArgs box_args(int n, const int bc_lo[3], const int bc_hi[3], double bc_value,
+                   bool homogeneous) const;
+  BoxArgs box_args_plain(int n) const;  // all faces kBcMemory
+
+ private:
+  std::unique_ptr<CopyPlan> exchange_;
+};
+
+// Build a copy plan from src layout to dst layout.  dst regions: the valid
+// box (with_valid) and/or its six 1-deep face slabs (with_faces); periodic
+// images of src boxes are used in periodic directions.  Both layouts must
+// live on the same domain index space.
+std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool with_valid,
+                                          bool with_faces);
+
+// LevelData<FArrayBox> with one component and one ghost layer.
+class LevelData {
+ public:
+  explicit LevelData(std::shared_ptr<Grid> g);
+  ~LevelData();
+  LevelData(const LevelData &) = delete;
+  LevelData &operator=(const LevelData &) = delete;
+  std::shared_ptr<Grid> grid;
+  std::vector<double *> base;  // allocation per local box
+  std::vector<double *> p;     // valid-lo pointer per local box
+  double **d_tab = nullptr;    // device copy of p
+  double *ptr(int n) const { return p[n]; }
+  void set_zero_all(hipStream_t st);  // valid + ghosts
+  void exchange(hipStream_t st);
+};
+
+}  // namespace mgic

@@ -1,0 +1,618 @@
+// op.cpp -- VariableCoeffPoissonOperator(+Factory), BiCGStabSolver,
+// MultiGrid, AMRMultiGrid (see op.hpp).
+#include "op.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace mgic {
+
+// --------------------------------------------------------------- profiling
+namespace {
+struct SmootherProf {
+  bool on = false;
+  long min_cells = 0;
+  std::vector<hipEvent_t> ev;
+  size_t used = 0;
+  bool open = false;
+} g_prof;
+}  // namespace
+
+void prof_enable(bool on, long min_cells) {
+  g_prof.on = on;
+  g_prof.min_cells = min_cells;
+  g_prof.used = 0;
+  g_prof.open = false;
+}
+
+static void prof_mark(hipStream_t st, long ncells, bool begin) {
+  if (!g_prof.on || ncells < g_prof.min_cells) return;
+  if (begin) {
+    if (g_prof.used + 2 > g_prof.ev.size()) {
+      const size_t add = std::max<size_t>(256, g_prof.ev.size());
+      for (size_t i = 0; i < add; ++i) {
+        hipEvent_t e;
+        MGIC_HIP(hipEventCreate(&e));
+        g_prof.ev.push_back(e);
+      }
+    }
+    MGIC_HIP(hipEventRecord(g_prof.ev[g_prof.used], st));
+    g_prof.open = true;
+  } else if (g_prof.open) {
+    MGIC_HIP(hipEventRecord(g_prof.ev[g_prof.used + 1], st));
+    g_prof.used += 2;
+    g_prof.open = false;
+  }
+}
+
+int prof_read(double *total_ms) {
+  double tot = 0.0;
+  if (g_prof.used) MGIC_HIP(hipEventSynchronize(g_prof.ev[g_prof.used - 1]));
+  for (size_t i = 0; i + 1 < g_prof.used; i += 2) {
+    float ms = 0.f;
+    MGIC_HIP(hipEventElapsedTime(&ms, g_prof.ev[i], g_prof.ev[i + 1]));
+    tot += ms;
+  }
+  *total_ms = tot;
+  return (int)(g_prof.used / 2);
+}
+
+// --------------------------------------------------------------- operator
+int VariableCoeffPoissonOperator::s_maxCoarse = 2;
+
+static void check_same_layout(const Grid &g, const LevelData &x, const char *what) {
+  const Grid &h = *x.grid;
+  bool ok = h.nlocal() == g.nlocal();
+  for (int n = 0; ok && n < g.nlocal(); ++n)
+    ok = h.geom[n].valid == g.geom[n].valid && h.geom[n].sy == g.geom[n].sy &&
+         h.geom[n].sz == g.geom[n].sz;
+  if (!ok) throw Error(kBadArg, std::string("layout mismatch: ") + what);
+}
+
+void VariableCoeffPoissonOperator::define(std::shared_ptr<Grid> g, const OpParams &p) {
+  grid = std::move(g);
+  prm = p;
+  m_dx = grid->dx;
+  m_alpha = p.alpha;
+  m_beta = p.beta;
+  m_lambdaNeedsResetting = true;
+  build_args();
+}
+
+void VariableCoeffPoissonOperator::build_args() {
+  args_hom_.clear();
+  args_inhom_.clear();
+  args_plain_.clear();
+  for (int n = 0; n < grid->nlocal(); ++n) {
+    args_hom_.push_back(grid->box_args(n, prm.bc_lo, prm.bc_hi, prm.bc_value, true));
+    args_inhom_.push_back(grid->box_args(n, prm.bc_lo, prm.bc_hi, prm.bc_value, false));
+    args_plain_.push_back(grid->box_args_plain(n));
+  }
+}
+
+const BoxArgs &VariableCoeffPoissonOperator::args(int n, bool homogeneous) {
+  return homogeneous ? args_hom_[n] : args_inhom_[n];
+}
+
+StencilCoefs VariableCoeffPoissonOperator::coefs() const {
+  StencilCoefs s;
+  s.alpha = m_alpha;
+  s.beta = m_beta;
+  s.dx = m_dx;
+  s.dxinv = 1.0 / (m_dx * m_dx);                    // .ChF:89
+  s.lamshift = 2.0 * 3 * m_beta / (m_dx * m_dx);    // .cpp:240
+  return s;
+}
+
+void VariableCoeffPoissonOperator::residualI(LevelData &lhs, LevelData &dpsi,
+                                             const LevelData &rhs, bool homogeneous) {
+  check_same_layout(*grid, lhs, "residual lhs");
+  check_same_layout(*grid, dpsi, "residual dpsi");
+  check_same_layout(*grid, rhs, "residual rhs");
+  const hipStream_t st = stream();
+  dpsi.exchange(st);  // .cpp:48 (the BC of :43-45 is folded into the kernel)
+  const StencilCoefs s = coefs();
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::residual(lhs.p[n], dpsi.p[n], rhs.p[n], m_aCoef->p[n], m_bCoef->p[n], args(n, homogeneous),
+                   s, st);
+}
+
+void VariableCoeffPoissonOperator::preCond(LevelData &cor, const LevelData &res) {
+  resetLambda();  // .cpp:90
+  const hipStream_t st = stream();
+  for (int n = 0; n < grid->nlocal(); ++n) {
+    kern::blas(0, cor.p[n], res.p[n], nullptr, 0.0, 0.0, args_plain_[n], st);            // :99
+    kern::blas(3, cor.p[n], m_lambda->p[n], nullptr, 0.0, 0.0, args_plain_[n], st);      // :100
+  }
+  relax(cor, res, 2);  // :103
+}
+
+void VariableCoeffPoissonOperator::applyOpI(LevelData &lhs, LevelData &dpsi, bool homogeneous) {
+  check_same_layout(*grid, lhs, "applyOp lhs");
+  check_same_layout(*grid, dpsi, "applyOp dpsi");
+  const hipStream_t st = stream();
+  dpsi.exchange(st);  // .cpp:131 (BC of :115-117 folded)
+  const StencilCoefs s = coefs();
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::apply_op(lhs.p[n], dpsi.p[n], m_aCoef->p[n], m_bCoef->p[n], args(n, homogeneous), s, st);
+}
+
+void VariableCoeffPoissonOperator::applyOpNoBoundary(LevelData &lhs, LevelData &dpsi) {
+  const hipStream_t st = stream();
+  dpsi.exchange(st);
+  const StencilCoefs s = coefs();
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::apply_op(lhs.p[n], dpsi.p[n], m_aCoef->p[n], m_bCoef->p[n], args_plain_[n], s, st);
+}
+
+void VariableCoeffPoissonOperator::restrictResidual(LevelData &resC, LevelData &dpsiF,
+                                                    const LevelData &rhsF) {
+  const Grid &cg = *resC.grid;
+  MGIC_CHECK(cg.nlocal() == grid->nlocal(), "restrictResidual: coarse layout mismatch");
+  for (int n = 0; n < grid->nlocal(); ++n) {
+    MGIC_CHECK(grid->geom[n].valid.coarsenable(2), "restrictResidual: fine box not coarsenable");
+    MGIC_CHECK(cg.geom[n].valid == grid->geom[n].valid.coarsened(2),
+               "restrictResidual: coarse box is not coarsen(fine box, 2)");
+  }
+  const hipStream_t st = stream();
+  dpsiF.exchange(st);  // .cpp:163 (BC of :158-161 folded, homogeneous)
+  const StencilCoefs s = coefs();
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::restrict_residual(resC.p[n], cg.box_args_plain(n), dpsiF.p[n], rhsF.p[n], m_aCoef->p[n],
+                            m_bCoef->p[n], args(n, true), s, st);
+}
+
+void VariableCoeffPoissonOperator::prolongIncrement(LevelData &phi, LevelData &corC) {
+  if (prm.prolong_type == 1) corC.exchange(stream());
+  prolongIncrementFilled(phi, corC);
+}
+
+void VariableCoeffPoissonOperator::prolongIncrementFilled(LevelData &phi, const LevelData &corC) {
+  const Grid &cg = *corC.grid;
+  MGIC_CHECK(cg.nlocal() == grid->nlocal(), "prolongIncrement: coarse layout mismatch");
+  const hipStream_t st = stream();
+  for (int n = 0; n < grid->nlocal(); ++n) {
+    const Box &cb = cg.geom[n].valid;
+    MGIC_CHECK(cb == grid->geom[n].valid.coarsened(2), "prolongIncrement: coarse box mismatch");
+    int alo[3], ahi[3];
+    for (int d = 0; d < 3; ++d) {
+      alo[d] = cg.periodic[d] || cb.lo[d] > cg.domain.lo[d];
+      ahi[d] = cg.periodic[d] || cb.hi[d] < cg.domain.hi[d];
+    }
+    kern::prolong(phi.p[n], args_plain_[n], corC.p[n], cg.box_args_plain(n), alo, ahi,
+                  prm.prolong_type, st);
+  }
+}
+
+void VariableCoeffPoissonOperator::setAlphaAndBeta(double alpha, double beta) {
+  m_alpha = alpha;  // .cpp:196-203
+  m_beta = beta;
+  m_lambdaNeedsResetting = true;
+}
+
+void VariableCoeffPoissonOperator::setCoefs(std::shared_ptr<LevelData> a,
+                                            std::shared_ptr<LevelData> b, double alpha,
+                                            double beta) {
+  check_same_layout(*grid, *a, "aCoef");
+  check_same_layout(*grid, *b, "bCoef");
+  m_alpha = alpha;  // .cpp:205-218
+  m_beta = beta;
+  m_aCoef = std::move(a);
+  m_bCoef = std::move(b);
+  m_lambdaNeedsResetting = true;
+}
+
+void VariableCoeffPoissonOperator::resetLambda() {
+  if (!m_lambdaNeedsResetting) return;  // .cpp:222
+  if (!m_lambda) m_lambda = std::make_unique<LevelData>(grid);
+  const StencilCoefs s = coefs();
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::lambda(m_lambda->p[n], m_aCoef->p[n], args_plain_[n], s, stream());
+  m_lambdaNeedsResetting = false;
+}
+
+void VariableCoeffPoissonOperator::computeLambda() {
+  if (!m_lambda) m_lambda = std::make_unique<LevelData>(grid);  // .cpp:258
+  m_lambdaNeedsResetting = true;
+  resetLambda();
+}
+
+void VariableCoeffPoissonOperator::setTime(double t) {
+  m_time = t;  // .cpp:400-420 (no b-coefficient interpolator is set in this app)
+  m_lambdaNeedsResetting = true;
+}
+
+void VariableCoeffPoissonOperator::relax(LevelData &e, const LevelData &r, int iterations) {
+  for (int it = 0; it < iterations; ++it) {
+    switch (prm.relax_mode) {
+      case 1: levelGSRB(e, r); break;
+      case 4: levelJacobi(e, r); break;
+      case 2: levelMultiColor(e, r);
+      case 3: looseGSRB(e, r);
+      case 5: overlapGSRB(e, r);
+      default: levelGSRBLazy(e, r);
+    }
+  }
+}
+
+void VariableCoeffPoissonOperator::levelGSRB(LevelData &dpsi, const LevelData &rhs) {
+  resetLambda();  // .cpp:283
+  const hipStream_t st = stream();
+  const StencilCoefs s = coefs();
+  // One box covering the whole non-periodic domain: no exchange is needed
+  // between the two colour passes, so both run in one fused launch.
+  if (prm.fused_smoother && grid->boxes.size() == 1 && grid->nlocal() == 1 &&
+      !grid->periodic[0] && !grid->periodic[1] && !grid->periodic[2] &&
+      kern::gsrb_sweep_fused_supported(args_hom_[0])) {
+    const long nc = grid->geom[0].valid.ncells();
+    prof_mark(st, nc, true);
+    kern::gsrb_sweep_fused(dpsi.p[0], rhs.p[0], m_aCoef->p[0], m_bCoef->p[0], args_hom_[0], s, st);
+    prof_mark(st, nc, false);
+    return;
+  }
+  for (int pass = 0; pass <= 1; ++pass) {  // .cpp:290
+    dpsi.exchange(st);                      // .cpp:301 (BC of :307-310 folded)
+    for (int n = 0; n < grid->nlocal(); ++n) {
+      const long nc = grid->geom[n].valid.ncells();
+      prof_mark(st, nc, true);
+      kern::gsrb_pass(dpsi.p[n], rhs.p[n], m_aCoef->p[n], m_bCoef->p[n], nullptr, args_hom_[n], s,
+                      pass, st);  // .cpp:313-330
+      prof_mark(st, nc, false);
+    }
+  }
+}
+
+void VariableCoeffPoissonOperator::levelJacobi(LevelData &dpsi, const LevelData &rhs) {
+  resetLambda();  // .cpp:366
+  if (!jac_tmp_) jac_tmp_ = create();
+  residualI(*jac_tmp_, dpsi, rhs, true);  // .cpp:372
+  const hipStream_t st = stream();
+  for (int n = 0; n < grid->nlocal(); ++n) {
+    kern::blas(3, jac_tmp_->p[n], m_lambda->p[n], nullptr, 0.0, 0.0, args_plain_[n], st);  // :377
+    kern::blas(1, dpsi.p[n], jac_tmp_->p[n], nullptr, 0.5, 0.0, args_plain_[n], st);       // :381
+  }
+  dpsi.exchange(st);  // :384
+}
+
+void VariableCoeffPoissonOperator::levelMultiColor(LevelData &, const LevelData &) {
+  throw Error(kState, "VariableCoeffPoissonOperator::levelMultiColor - Not implemented");
+}
+void VariableCoeffPoissonOperator::looseGSRB(LevelData &, const LevelData &) {
+  throw Error(kState, "VariableCoeffPoissonOperator::looseGSRB - Not implemented");
+}
+void VariableCoeffPoissonOperator::overlapGSRB(LevelData &, const LevelData &) {
+  throw Error(kState, "VariableCoeffPoissonOperator::overlapGSRB - Not implemented");
+}
+void VariableCoeffPoissonOperator::levelGSRBLazy(LevelData &, const LevelData &) {
+  throw Error(kState, "VariableCoeffPoissonOperator::levelGSRBLazy - Not implemented");
+}
+
+void VariableCoeffPoissonOperator::fillBC(LevelData &u, bool homogeneous) {
+  for (int n = 0; n < grid->nlocal(); ++n) kern::fill_bc(u.p[n], args(n, homogeneous), stream());
+}
+
+void VariableCoeffPoissonOperator::setToZero(LevelData &x) { x.set_zero_all(stream()); }
+
+void VariableCoeffPoissonOperator::assignLocal(LevelData &lhs, const LevelData &rhs) {
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::blas(0, lhs.p[n], rhs.p[n], nullptr, 0.0, 0.0, args_plain_[n], stream());
+}
+void VariableCoeffPoissonOperator::incr(LevelData &lhs, const LevelData &x, double sc) {
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::blas(1, lhs.p[n], x.p[n], nullptr, sc, 0.0, args_plain_[n], stream());
+}
+void VariableCoeffPoissonOperator::axby(LevelData &lhs, const LevelData &x, const LevelData &y,
+                                        double a, double b) {
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::blas(4, lhs.p[n], x.p[n], y.p[n], a, b, args_plain_[n], stream());
+}
+void VariableCoeffPoissonOperator::scale(LevelData &lhs, double sc) {
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::blas(2, lhs.p[n], nullptr, nullptr, sc, 0.0, args_plain_[n], stream());
+}
+void VariableCoeffPoissonOperator::mult(LevelData &lhs, const LevelData &x) {
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::blas(3, lhs.p[n], x.p[n], nullptr, 0.0, 0.0, args_plain_[n], stream());
+}
+void VariableCoeffPoissonOperator::setVal(LevelData &lhs, double v) {
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::blas(5, lhs.p[n], nullptr, nullptr, v, 0.0, args_plain_[n], stream());
+}
+
+double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const LevelData *y) {
+  Comm &c = *grid->comm;
+  const hipStream_t st = stream();
+  double *parts = c.d_partials(std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox);
+  int total = 0;
+  for (int n = 0; n < grid->nlocal(); ++n)
+    total += kern::reduce_partial(kind, x.p[n], y ? y->p[n] : nullptr, args_plain_[n], parts + total, st);
+  if (total == 0) MGIC_HIP(hipMemsetAsync(c.d_result(), 0, sizeof(double), st));
+  else kern::reduce_final(kind, parts, total, c.d_result(), st);
+  c.allreduce(c.d_result(), kind == 3 ? 1 : 0);
+  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
+  MGIC_HIP(hipStreamSynchronize(st));
+  return c.h_result()[0];
+}
+
+double VariableCoeffPoissonOperator::dotProduct(const LevelData &x, const LevelData &y) {
+  return reduce(0, x, &y);
+}
+
+double VariableCoeffPoissonOperator::norm(const LevelData &x, int ord) {
+  if (ord == 0) return reduce(3, x, nullptr);
+  if (ord == 1) return reduce(1, x, nullptr);
+  return std::sqrt(reduce(2, x, nullptr));
+}
+
+// --------------------------------------------------------------- factory
+void VariableCoeffPoissonOperatorFactory::define(std::shared_ptr<Grid> g, const OpParams &p,
+                                                 std::shared_ptr<LevelData> a,
+                                                 std::shared_ptr<LevelData> b) {
+  grid = std::move(g);  // Factory.cpp:59-106 (one AMR level)
+  prm = p;
+  m_aCoef = std::move(a);
+  m_bCoef = std::move(b);
+  m_coefficient_average_type = p.coefficient_average_type;  // Factory.cpp:44-46
+}
+
+std::shared_ptr<LevelData> average_coef(const LevelData &fine, std::shared_ptr<Grid> cgrid,
+                                        int ratio, int harmonic) {
+  auto c = std::make_shared<LevelData>(cgrid);
+  const hipStream_t st = fine.grid->comm->stream();
+  for (int n = 0; n < cgrid->nlocal(); ++n)
+    kern::average(c->p[n], cgrid->box_args_plain(n), fine.p[n], fine.grid->box_args_plain(n), ratio,
+                  harmonic, st);
+  return c;
+}
+
+std::unique_ptr<VariableCoeffPoissonOperator> VariableCoeffPoissonOperatorFactory::MGnewOp(
+    int depth, bool) {
+  const int coarsening = 1 << depth;  // Factory.cpp:161-166
+  if (coarsening > 1 && !grid->coarsenable(coarsening * VariableCoeffPoissonOperator::s_maxCoarse))
+    return nullptr;  // :168-172
+  auto layout = depth == 0 ? grid : grid->coarsened(coarsening);
+  auto op = std::make_unique<VariableCoeffPoissonOperator>();
+  OpParams p = prm;
+  p.coefficient_average_type = m_coefficient_average_type;
+  op->define(layout, p);  // :189
+  op->m_alpha = prm.alpha;
+  op->m_beta = prm.beta;
+  if (depth == 0) {  // :194-197
+    op->m_aCoef = m_aCoef;
+    op->m_bCoef = m_bCoef;
+  } else {  // :198-227: CoarseAverage straight from the AMR level, ratio 2^depth
+    const int harm = m_coefficient_average_type == 1;
+    op->m_aCoef = average_coef(*m_aCoef, layout, coarsening, harm);
+    op->m_bCoef = average_coef(*m_bCoef, layout, coarsening, harm);
+  }
+  op->computeLambda();  // :229
+  return op;
+}
+
+std::unique_ptr<VariableCoeffPoissonOperator> VariableCoeffPoissonOperatorFactory::AMRnewOp() {
+  auto op = std::make_unique<VariableCoeffPoissonOperator>();  // Factory.cpp:236-295
+  op->define(grid, prm);
+  op->m_alpha = prm.alpha;
+  op->m_beta = prm.beta;
+  op->m_aCoef = m_aCoef;
+  op->m_bCoef = m_bCoef;
+  op->computeLambda();
+  return op;
+}
+
+// --------------------------------------------------------------- BiCGStab
+int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
+                          bool hom) {
+  auto &tv = temps_[op.grid.get()];
+  if (tv.empty())
+    for (int i = 0; i < 9; ++i) tv.push_back(op.create());
+  LevelData &R = *tv[0], &RT = *tv[1], &E = *tv[2], &P = *tv[3], &PT = *tv[4], &S = *tv[5],
+            &ST = *tv[6], &T = *tv[7], &V = *tv[8];
+  const int nt = prm.normType;
+  op.residual(R, phi, rhs, hom);
+  op.assignLocal(RT, R);
+  op.setToZero(E);
+  op.setToZero(PT);
+  op.setToZero(ST);
+  op.setToZero(P);
+  op.setToZero(V);
+  double rho1 = 0.0, rho2 = 0.0, alpha = 0.0, beta = 0.0, omega = 0.0;
+  const double init_norm = op.norm(R, nt);
+  double nrm = init_norm;
+  int it = 0, restarts = 0;
+  bool init = true;
+  while (it < prm.imax && nrm > prm.eps * init_norm && nrm > prm.reps) {
+    ++it;
+    rho2 = rho1;
+    rho1 = op.dotProduct(RT, R);
+    if (rho1 == 0.0) break;
+    if (init) {
+      op.assignLocal(P, R);
+      init = false;
+    } else {
+      beta = (rho1 / rho2) * (alpha / omega);
+      op.scale(P, beta);
+      op.incr(P, V, -beta * omega);
+      op.incr(P, R, 1.0);
+    }
+    op.preCond(PT, P);
+    op.setToZero(V);
+    op.applyOp(V, PT, true);
+    const double m = op.dotProduct(RT, V);
+    if (std::fabs(m) > prm.small * std::fabs(rho1)) {
+      alpha = rho1 / m;
+      op.assignLocal(S, R);
+      op.incr(S, V, -alpha);
+      op.incr(E, PT, alpha);
+      nrm = op.norm(S, nt);
+      if (nrm <= prm.eps * init_norm || nrm <= prm.reps) break;
+      op.preCond(ST, S);
+      op.setToZero(T);
+      op.applyOp(T, ST, true);
+      const double ts = op.dotProduct(T, S);
+      const double tt = op.dotProduct(T, T);
+      if (tt == 0.0) break;
+      omega = ts / tt;
+      op.assignLocal(R, S);
+      op.incr(R, T, -omega);
+      op.incr(E, ST, omega);
+      nrm = op.norm(R, nt);
+      if (omega == 0.0) break;
+    } else {
+      if (restarts >= prm.numRestarts) break;
+      ++restarts;
+      op.incr(phi, E, 1.0);
+      op.residual(R, phi, rhs, hom);
+      op.assignLocal(RT, R);
+      op.setToZero(E);
+      nrm = op.norm(R, nt);
+      init = true;
+    }
+  }
+  op.incr(phi, E, 1.0);
+  last_iters = it;
+  return it;
+}
+
+// --------------------------------------------------------------- MultiGrid
+static int min_box_side(const Grid &g) {
+  int m = 1 << 30;
+  for (auto &b : g.boxes)
+    for (int d = 0; d < 3; ++d) m = std::min(m, b.size(d));
+  return m;
+}
+
+void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &p) {
+  prm = p;
+  bottom.prm = p.bicg;
+  levels_.clear();
+  {
+    Level L0;
+    L0.op = factory.MGnewOp(0);
+    levels_.push_back(std::move(L0));
+  }
+  bool agg_chain = false;
+  for (int d = 1;; ++d) {
+    if (prm.max_depth >= 0 && d > prm.max_depth) break;
+    Level L;
+    if (!agg_chain) {
+      auto op = factory.MGnewOp(d);
+      if (!op) break;
+      const bool do_agg = prm.agglomerate_below > 0 && op->grid->boxes.size() > 1 &&
+                          min_box_side(*op->grid) < prm.agglomerate_below;
+      if (!do_agg) {
+        L.e = op->create();
+        L.r = op->create();
+        L.op = std::move(op);
+      } else {
+        // gather this depth onto one box owned by rank 0
+        const Grid &dg = *op->grid;
+        bool per[3] = {dg.periodic[0], dg.periodic[1], dg.periodic[2]};
+        auto ag = std::make_shared<Grid>(dg.comm, dg.domain, per, dg.dx, std::vector<Box>{dg.domain},
+                                         std::vector<int>{0});
+        auto a = std::make_shared<LevelData>(ag);
+        auto b = std::make_shared<LevelData>(ag);
+        auto to_agg = build_copy_plan(dg, *ag, true, false);
+        to_agg->execute(*dg.comm, op->m_aCoef->d_tab, a->d_tab, dg.comm->stream());
+        to_agg->execute(*dg.comm, op->m_bCoef->d_tab, b->d_tab, dg.comm->stream());
+        auto aop = std::make_unique<VariableCoeffPoissonOperator>();
+        aop->define(ag, op->prm);
+        aop->m_aCoef = a;
+        aop->m_bCoef = b;
+        aop->computeLambda();
+        L.r_stage = op->create();
+        L.e_stage = op->create();
+        L.restrict_plan = build_copy_plan(dg, *ag, true, false);
+        L.prolong_plan = build_copy_plan(*ag, dg, true, true);
+        L.e = aop->create();
+        L.r = aop->create();
+        L.op = std::move(aop);
+        L.agg = true;
+        agg_chain = true;
+      }
+    } else {
+      const VariableCoeffPoissonOperator &prev = *levels_.back().op;
+      if (!prev.grid->coarsenable(2 * VariableCoeffPoissonOperator::s_maxCoarse)) break;
+      auto cg = prev.grid->coarsened(2);
+      auto op = std::make_unique<VariableCoeffPoissonOperator>();
+      op->define(cg, prev.prm);
+      const int harm = prev.prm.coefficient_average_type == 1;
+      if (factory.grid->coarsenable(1 << d)) {
+        // same coefficients as MGnewOp(d) would give: average from the AMR
+        // level, then gather
+        auto dgrid = factory.grid->coarsened(1 << d);
+        auto da = average_coef(*factory.m_aCoef, dgrid, 1 << d, harm);
+        auto db = average_coef(*factory.m_bCoef, dgrid, 1 << d, harm);
+        auto a = std::make_shared<LevelData>(cg);
+        auto b = std::make_shared<LevelData>(cg);
+        auto pl = build_copy_plan(*dgrid, *cg, true, false);
+        pl->execute(*cg->comm, da->d_tab, a->d_tab, cg->comm->stream());
+        pl->execute(*cg->comm, db->d_tab, b->d_tab, cg->comm->stream());
+        MGIC_HIP(hipStreamSynchronize(cg->comm->stream()));
+        op->m_aCoef = a;
+        op->m_bCoef = b;
+      } else {
+        op->m_aCoef = average_coef(*prev.m_aCoef, cg, 2, harm);
+        op->m_bCoef = average_coef(*prev.m_bCoef, cg, 2, harm);
+      }
+      op->computeLambda();
+      L.e = op->create();
+      L.r = op->create();
+      L.op = std::move(op);
+    }
+    levels_.push_back(std::move(L));
+  }
+  MGIC_HIP(hipStreamSynchronize(levels_[0].op->stream()));
+}
+
+void MultiGrid::cycle(int d, LevelData &e, LevelData &r) {
+  VariableCoeffPoissonOperator &op = *levels_[d].op;
+  const hipStream_t st = op.stream();
+  if (d == (int)levels_.size() - 1) {  // bottom
+    if (prm.bottom_solver == 1) bottom.solve(op, e, r, true);
+    else op.relax(e, r, prm.n_bottom);
+    return;
+  }
+  op.relax(e, r, prm.n_pre);
+  Level &N = levels_[d + 1];
+  if (!N.agg) {
+    op.restrictResidual(*N.r, e, r);
+  } else {
+    op.restrictResidual(*N.r_stage, e, r);
+    N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
+  }
+  N.op->setToZero(*N.e);
+  for (int c = 0; c < prm.cycles; ++c) cycle(d + 1, *N.e, *N.r);
+  if (!N.agg) {
+    op.prolongIncrement(e, *N.e);
+  } else {
+    N.prolong_plan->execute(*op.grid->comm, N.e->d_tab, N.e_stage->d_tab, st);
+    op.prolongIncrementFilled(e, *N.e_stage);
+  }
+  op.relax(e, r, prm.n_post);
+}
+
+// --------------------------------------------------------------- AMRMultiGrid
+void AMRMultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &p) {
+  mg.define(factory, p);
+  corr_ = mg.op(0).create();
+}
+
+double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &resid,
+                               int normType, bool homogeneous) {
+  VariableCoeffPoissonOperator &op0 = mg.op(0);
+  op0.setToZero(*corr_);
+  mg.oneCycle(*corr_, resid);
+  op0.incr(phi, *corr_, 1.0);
+  op0.residual(resid, phi, rhs, homogeneous);
+  return normType >= 0 ? op0.norm(resid, normType) : -1.0;
+}
+
+double AMRMultiGrid::initResidual(LevelData &phi, const LevelData &rhs, LevelData &resid,
+                                  int normType, bool homogeneous) {
+  VariableCoeffPoissonOperator &op0 = mg.op(0);
+  op0.residual(resid, phi, rhs, homogeneous);
+  return normType >= 0 ? op0.norm(resid, normType) : -1.0;
+}
+
+}  // namespace mgic

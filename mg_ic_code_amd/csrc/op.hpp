@@ -1,0 +1,201 @@
+// op.hpp -- the reference's operator-plugin API, MI355X-native.
+//
+// VariableCoeffPoissonOperator mirrors Source/VariableCoeffPoissonOperator.H
+// (method names, argument meaning, lazy lambda), VariableCoeffPoisson
+// OperatorFactory mirrors Source/VariableCoeffPoissonOperatorFactory.H, and
+// MultiGrid / BiCGStabSolver / AMRMultiGrid re-host the [Chombo] drivers
+// that call them (MultiGrid::oneCycle, BiCGStabSolver::solve,
+// AMRMultiGrid::solve on one AMR level).  Everything runs on the Comm's HIP
+// stream; host code only sequences kernels (and reads back the scalars the
+// Krylov bottom solver branches on).
+#pragma once
+
+#include "level.hpp"
+
+namespace mgic {
+
+// ParseBC state (SetBCs.cpp GlobalBCRS + ParmParse bc_value) and the
+// operator constants/options of params.txt.
+struct OpParams {
+  double alpha = 0.0, beta = -1.0;  // factory defaults (Factory.cpp:317-322)
+  int bc_lo[3] = {0, 0, 0};
+  int bc_hi[3] = {0, 0, 0};
+  double bc_value = 0.0;
+  int coefficient_average_type = 0;  // 0 arithmetic (default), 1 harmonic
+  int prolong_type = 1;              // 0 piecewise constant, 1 linear
+  int relax_mode = 1;                // [Chombo] s_relaxMode: 1 GSRB, 4 Jacobi
+  int fused_smoother = 1;            // allow the fused red+black sweep kernel
+};
+
+class VariableCoeffPoissonOperator {
+ public:
+  static int s_maxCoarse;  // [Chombo] AMRPoissonOp::s_maxCoarse
+
+  // AMRPoissonOp::define(grids, dx, domain, bc, exchangeCopier, cfregion)
+  void define(std::shared_ptr<Grid> grid, const OpParams &prm);
+  hipStream_t stream() const { return grid->comm->stream(); }
+
+  // --- AMRLevelOp / MGLevelOp overrides (VariableCoeffPoissonOperator.H:39-90)
+  void residualI(LevelData &lhs, LevelData &dpsi, const LevelData &rhs, bool homogeneous);
+  void residual(LevelData &lhs, LevelData &dpsi, const LevelData &rhs, bool homogeneous) {
+    residualI(lhs, dpsi, rhs, homogeneous);
+  }
+  void preCond(LevelData &correction, const LevelData &residual);
+  void applyOpI(LevelData &lhs, LevelData &dpsi, bool homogeneous);
+  void applyOp(LevelData &lhs, LevelData &dpsi, bool homogeneous) { applyOpI(lhs, dpsi, homogeneous); }
+  void applyOpNoBoundary(LevelData &lhs, LevelData &dpsi);
+  void restrictResidual(LevelData &resCoarse, LevelData &dpsiFine, const LevelData &rhsFine);
+  // [Chombo] AMRPoissonOp::prolongIncrement (inherited)
+  void prolongIncrement(LevelData &phiThisLevel, LevelData &correctCoarse);
+  // same, with the coarse ghost layer already filled by the caller
+  void prolongIncrementFilled(LevelData &phiThisLevel, const LevelData &correctCoarse);
+  void setAlphaAndBeta(double alpha, double beta);
+  void setCoefs(std::shared_ptr<LevelData> aCoef, std::shared_ptr<LevelData> bCoef, double alpha,
+                double beta);
+  void resetLambda();
+  void computeLambda();
+  void reflux() {}   // not implemented in the reference either (.cpp:264-271)
+  void getFlux() {}  // (.cpp:389-397)
+  void setTime(double t);
+  void relax(LevelData &e, const LevelData &r, int iterations);  // [Chombo] AMRPoissonOp::relax
+  void levelGSRB(LevelData &dpsi, const LevelData &rhs);
+  void levelJacobi(LevelData &dpsi, const LevelData &rhs);
+  [[noreturn]] void levelMultiColor(LevelData &, const LevelData &);
+  [[noreturn]] void looseGSRB(LevelData &, const LevelData &);
+  [[noreturn]] void overlapGSRB(LevelData &, const LevelData &);
+  [[noreturn]] void levelGSRBLazy(LevelData &, const LevelData &);
+  // ParseBC on every box (m_bc): writes the domain-face ghost layers
+  void fillBC(LevelData &u, bool homogeneous);
+
+  // --- LinearOp<LevelData> vector interface ([Chombo] AMRPoissonOp)
+  std::unique_ptr<LevelData> create() const { return std::make_unique<LevelData>(grid); }
+  void setToZero(LevelData &x);
+  void assignLocal(LevelData &lhs, const LevelData &rhs);
+  void assign(LevelData &lhs, const LevelData &rhs) { assignLocal(lhs, rhs); }
+  void incr(LevelData &lhs, const LevelData &x, double scale);
+  void axby(LevelData &lhs, const LevelData &x, const LevelData &y, double a, double b);
+  void scale(LevelData &lhs, double s);
+  void mult(LevelData &lhs, const LevelData &x);  // lhs *= x (FArrayBox::mult)
+  void setVal(LevelData &lhs, double v);
+  double dotProduct(const LevelData &x, const LevelData &y);
+  double norm(const LevelData &x, int ord);
+
+  // state (public as in the reference: m_aCoef, m_bCoef, m_lambda)
+  std::shared_ptr<Grid> grid;
+  OpParams prm;
+  double m_alpha = 0.0, m_beta = -1.0, m_dx = 1.0, m_dxCrse = -1.0, m_time = 0.0;
+  std::shared_ptr<LevelData> m_aCoef, m_bCoef;
+  std::unique_ptr<LevelData> m_lambda;
+  bool m_lambdaNeedsResetting = true;
+
+
+ private:
+  StencilCoefs coefs() const;
+  const BoxArgs &args(int n, bool homogeneous);
+  void build_args();
+  double reduce(int kind, const LevelData &x, const LevelData *y);
+  std::vector<BoxArgs> args_hom_, args_inhom_, args_plain_;
+  std::unique_ptr<LevelData> jac_tmp_;
+};
+
+// CoarseAverage (arithmetic / harmonic) of a fine LevelData onto the layout
+// coarsened by `ratio` (same box order and owners).
+std::shared_ptr<LevelData> average_coef(const LevelData &fine, std::shared_ptr<Grid> cgrid,
+                                        int ratio, int harmonic);
+
+// Smoother instrumentation: when enabled, every smoother launch on a box of
+// at least min_cells cells is bracketed by hipEvents on its stream.
+void prof_enable(bool on, long min_cells);
+int prof_read(double *total_ms);  // returns launches timed, total ms
+
+// VariableCoeffPoissonOperatorFactory (single AMR level; the configs have one)
+class VariableCoeffPoissonOperatorFactory {
+ public:
+  // define(coarseDomain, grids, refRatios, coarsedx, bc, alpha, aCoef, beta, bCoef)
+  void define(std::shared_ptr<Grid> grid, const OpParams &prm, std::shared_ptr<LevelData> aCoef,
+              std::shared_ptr<LevelData> bCoef);
+  // MGnewOp: nullptr once !coarsenable(2^depth * s_maxCoarse) (Factory.cpp:168-172)
+  std::unique_ptr<VariableCoeffPoissonOperator> MGnewOp(int depth, bool homoOnly = true);
+  std::unique_ptr<VariableCoeffPoissonOperator> AMRnewOp();
+  int refToFiner() const { return 2; }  // refRatio forced to 2 (PoissonParameters.cpp:75-79)
+  int m_coefficient_average_type = 0;
+
+  std::shared_ptr<Grid> grid;
+  OpParams prm;
+  std::shared_ptr<LevelData> m_aCoef, m_bCoef;
+};
+
+struct BiCGStabParams {
+  int imax = 80;
+  double eps = 1.0e-6, reps = 1.0e-12, small = 1.0e-30;
+  int numRestarts = 5;
+  int normType = 2;
+};
+
+// [Chombo] BiCGStabSolver<LevelData<FArrayBox>>::solve restated (the same
+// control flow as oracle/mgic_oracle.c orc_mg_bicgstab)
+class BiCGStabSolver {
+ public:
+  BiCGStabParams prm;
+  int last_iters = 0;
+  int solve(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
+            bool homogeneous);
+
+ private:
+  std::map<const Grid *, std::vector<std::unique_ptr<LevelData>>> temps_;
+};
+
+struct MGParams {
+  int max_depth = -1;  // deepest MG depth (-1: as deep as coarsenable)
+  int n_pre = 4, n_post = 4, n_bottom = 4;
+  int bottom_solver = 1;       // 0: relax(n_bottom), 1: BiCGStab
+  int cycles = 1;              // 1 = V-cycle
+  int agglomerate_below = 0;   // gather to rank 0 when a box side < this (0 off)
+  BiCGStabParams bicg;
+};
+
+// [Chombo] MultiGrid hierarchy built from the factory's MGnewOp; oneCycle is
+// MultiGrid::oneCycle (pre-relax, restrictResidual, recurse, prolongIncrement,
+// post-relax; bottom solver at the coarsest depth).
+class MultiGrid {
+ public:
+  void define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &prm);
+  void oneCycle(LevelData &e, const LevelData &r) { cycle(0, e, const_cast<LevelData &>(r)); }
+  int depths() const { return (int)levels_.size(); }
+  VariableCoeffPoissonOperator &op(int d) { return *levels_[d].op; }
+  LevelData *corr(int d) { return levels_[d].e.get(); }
+  LevelData *resid(int d) { return levels_[d].r.get(); }
+  bool agglomerated(int d) const { return levels_[d].agg; }
+  MGParams prm;
+  BiCGStabSolver bottom;
+
+ private:
+  struct Level {
+    std::unique_ptr<VariableCoeffPoissonOperator> op;
+    std::unique_ptr<LevelData> e, r;
+    bool agg = false;  // this level lives on rank 0 (gathered)
+    std::unique_ptr<LevelData> r_stage, e_stage;  // previous layout coarsened
+    std::unique_ptr<CopyPlan> restrict_plan, prolong_plan;
+  };
+  void cycle(int d, LevelData &e, LevelData &r);
+  std::vector<Level> levels_;
+};
+
+// [Chombo] AMRMultiGrid on a single AMR level: iterations of
+//   e = 0; oneCycle(e, r); phi += e; r = rhs - L(phi)
+class AMRMultiGrid {
+ public:
+  void define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &prm);
+  // one iteration; returns norm(r, normType) if normType >= 0 (host sync),
+  // else -1 without synchronising
+  double iteration(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
+                   bool homogeneous);
+  double initResidual(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
+                      bool homogeneous);
+  MultiGrid mg;
+
+ private:
+  std::unique_ptr<LevelData> corr_;
+};
+
+}  // namespace mgic
