@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--nsmooth", type=int, default=4)
     ap.add_argument("--no-fused", action="store_true", help="per-colour smoother launches")
-    ap.add_argument("--cpu-baseline-iters", type=int, default=1)
+    ap.add_argument("--cpu-baseline-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_smoother.json"))
@@ -214,7 +214,7 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
     o.init_residual(0)
     t0 = time.perf_counter()
     for _ in range(args.cpu_baseline_iters):
-        o.iteration(-1 if False else 0)
+        o.iteration(0)
     dt = time.perf_counter() - t0
     return {
         "value": round(args.cpu_baseline_iters / dt, 6),

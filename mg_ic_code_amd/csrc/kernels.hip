@@ -228,8 +228,10 @@ __global__ void k_fill_bc_face(double *__restrict__ u, const BoxArgs g, int face
   u[gh] = ghost_of(g.bcm[face], g.bcc[face], u[near]);
 }
 
-__global__ __launch_bounds__(256) void k_blas(int kind, double *__restrict__ x,
-                                              const double *__restrict__ y,
+// BLAS-1 kinds are template parameters: every launch compiles to one
+// straight-line body (no runtime switch inside the cell loop).
+template <int KIND>
+__global__ __launch_bounds__(256) void k_blas(double *__restrict__ x, const double *__restrict__ y,
                                               const double *__restrict__ z, double s, double t,
                                               const BoxArgs g) {
   const int i = blockIdx.x * TX + threadIdx.x;
@@ -237,63 +239,63 @@ __global__ __launch_bounds__(256) void k_blas(int kind, double *__restrict__ x,
   const int k = blockIdx.z;
   if (i >= g.nx || j >= g.ny) return;
   const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
-  switch (kind) {
-    case 0: x[idx] = y[idx]; break;                    // assign / copy
-    case 1: x[idx] = x[idx] + s * y[idx]; break;       // incr  (FArrayBox::plus(src, scale))
-    case 2: x[idx] = x[idx] * s; break;                // scale (FArrayBox::mult(scale))
-    case 3: x[idx] = x[idx] * y[idx]; break;           // mult  (FArrayBox::mult(src))
-    case 4: x[idx] = s * y[idx] + t * z[idx]; break;   // axby
-    default: x[idx] = s; break;                        // setVal
-  }
+  if constexpr (KIND == 0) x[idx] = y[idx];                    // assign / copy
+  else if constexpr (KIND == 1) x[idx] = x[idx] + s * y[idx];  // incr (FArrayBox::plus(src, scale))
+  else if constexpr (KIND == 2) x[idx] = x[idx] * s;           // scale (FArrayBox::mult(scale))
+  else if constexpr (KIND == 3) x[idx] = x[idx] * y[idx];      // mult (FArrayBox::mult(src))
+  else if constexpr (KIND == 4) x[idx] = s * y[idx] + t * z[idx];  // axby
+  else x[idx] = s;                                             // setVal
 }
 
 constexpr int RB = 256;
 
-__device__ __forceinline__ double red_op(int kind, double a, double b) {
-  return kind == 3 ? (a > b ? a : b) : a + b;
+template <int KIND>
+__device__ __forceinline__ double red_op(double a, double b) {
+  if constexpr (KIND == 3) return a > b ? a : b;
+  else return a + b;
 }
 
-__global__ __launch_bounds__(RB) void k_reduce_partial(int kind, const double *__restrict__ x,
+template <int KIND>
+__global__ __launch_bounds__(RB) void k_reduce_partial(const double *__restrict__ x,
                                                        const double *__restrict__ y,
                                                        const BoxArgs g,
                                                        double *__restrict__ partials) {
   __shared__ double sm[RB];
   const long ncell = (long)g.nx * g.ny * g.nz;
+  const long plane = (long)g.nx * g.ny;
   double acc = 0.0;
   for (long t = (long)blockIdx.x * RB + threadIdx.x; t < ncell; t += (long)gridDim.x * RB) {
-    const int i = (int)(t % g.nx);
-    const long r = t / g.nx;
-    const int j = (int)(r % g.ny);
-    const int k = (int)(r / g.ny);
+    const int k = (int)(t / plane);
+    const int rem = (int)(t - (long)k * plane);
+    const int j = rem / g.nx;
+    const int i = rem - j * g.nx;
     const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
     const double v = x[idx];
     double term;
-    switch (kind) {
-      case 0: term = v * y[idx]; break;
-      case 1: term = fabs(v); break;
-      case 2: term = v * v; break;
-      default: term = fabs(v); break;
-    }
-    acc = red_op(kind, acc, term);
+    if constexpr (KIND == 0) term = v * y[idx];
+    else if constexpr (KIND == 2) term = v * v;
+    else term = fabs(v);
+    acc = red_op<KIND>(acc, term);
   }
   sm[threadIdx.x] = acc;
   __syncthreads();
   for (int w = RB / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) sm[threadIdx.x] = red_op(kind, sm[threadIdx.x], sm[threadIdx.x + w]);
+    if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
     __syncthreads();
   }
   if (threadIdx.x == 0) partials[blockIdx.x] = sm[0];
 }
 
-__global__ __launch_bounds__(RB) void k_reduce_final(int kind, const double *__restrict__ p,
-                                                     int n, double *__restrict__ out) {
+template <int KIND>
+__global__ __launch_bounds__(RB) void k_reduce_final(const double *__restrict__ p, int n,
+                                                     double *__restrict__ out) {
   __shared__ double sm[RB];
   double acc = 0.0;
-  for (int t = threadIdx.x; t < n; t += RB) acc = red_op(kind, acc, p[t]);
+  for (int t = threadIdx.x; t < n; t += RB) acc = red_op<KIND>(acc, p[t]);
   sm[threadIdx.x] = acc;
   __syncthreads();
   for (int w = RB / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) sm[threadIdx.x] = red_op(kind, sm[threadIdx.x], sm[threadIdx.x + w]);
+    if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
     __syncthreads();
   }
   if (threadIdx.x == 0) out[0] = sm[0];
@@ -490,7 +492,16 @@ void fill_bc(double *u, const BoxArgs &g, hipStream_t st) {
 void blas(int kind, double *x, const double *y, const double *z, double s, double t,
           const BoxArgs &g, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  k_blas<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(kind, x, y, z, s, t, g);
+  const dim3 grid = grid_cells(g.nx, g.ny, g.nz);
+  switch (kind) {
+    case 0: k_blas<0><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
+    case 1: k_blas<1><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
+    case 2: k_blas<2><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
+    case 3: k_blas<3><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
+    case 4: k_blas<4><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
+    case 5: k_blas<5><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
+    default: throw Error(kBadArg, "blas: bad kind");
+  }
   check_launch();
 }
 
@@ -500,13 +511,26 @@ int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
   if (ncell <= 0) return 0;
   long nb = (ncell + RB - 1) / RB;
   if (nb > kMaxPartsPerBox) nb = kMaxPartsPerBox;
-  k_reduce_partial<<<dim3((unsigned)nb), dim3(RB), 0, st>>>(kind, x, y, g, partials);
+  const dim3 grid((unsigned)nb), block(RB);
+  switch (kind) {
+    case 0: k_reduce_partial<0><<<grid, block, 0, st>>>(x, y, g, partials); break;
+    case 1: k_reduce_partial<1><<<grid, block, 0, st>>>(x, y, g, partials); break;
+    case 2: k_reduce_partial<2><<<grid, block, 0, st>>>(x, y, g, partials); break;
+    case 3: k_reduce_partial<3><<<grid, block, 0, st>>>(x, y, g, partials); break;
+    default: throw Error(kBadArg, "reduce: bad kind");
+  }
   check_launch();
   return (int)nb;
 }
 
 void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st) {
-  k_reduce_final<<<dim3(1), dim3(RB), 0, st>>>(kind, partials, n, out);
+  switch (kind) {
+    case 0: k_reduce_final<0><<<1, RB, 0, st>>>(partials, n, out); break;
+    case 1: k_reduce_final<1><<<1, RB, 0, st>>>(partials, n, out); break;
+    case 2: k_reduce_final<2><<<1, RB, 0, st>>>(partials, n, out); break;
+    case 3: k_reduce_final<3><<<1, RB, 0, st>>>(partials, n, out); break;
+    default: throw Error(kBadArg, "reduce: bad kind");
+  }
   check_launch();
 }
 
