@@ -422,12 +422,6 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b, c
   check_launch();
 }
 
-bool gsrb_sweep_fused_supported(const BoxArgs &) { return false; }
-void gsrb_sweep_fused(double *, const double *, const double *, const double *, const BoxArgs &,
-                      const StencilCoefs &, hipStream_t) {
-  throw Error(kState, "fused sweep not available");
-}
-
 void apply_op(double *lu, const double *u, const double *a, const double *b, const BoxArgs &g,
               const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;

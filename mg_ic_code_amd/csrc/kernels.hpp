@@ -17,13 +17,12 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
                const double *lam, const BoxArgs &g, const StencilCoefs &s, int colour,
                hipStream_t st);
 // Fused red+black sweep (both passes of one levelGSRB, .cpp:290-331) in one
-// launch, staged through LDS; bit-identical to two gsrb_pass calls.  Only
-// valid when every face is either a domain face (bc folded) or has its
-// ghost already exchanged and the neighbour will not change during the
-// sweep -- i.e. a single box per level (checked by the caller).
+// launch, staged through LDS, OUT OF PLACE: u_out = sweep(u_in); bit-
+// identical to two in-place gsrb_pass calls.  Needs every face of the box
+// to be a BC-folded domain face (one box per level, smoother.hip).
 bool gsrb_sweep_fused_supported(const BoxArgs &g);
-void gsrb_sweep_fused(double *u, const double *rhs, const double *a, const double *b,
-                      const BoxArgs &g, const StencilCoefs &s, hipStream_t st);
+void gsrb_sweep_fused(double *u_out, const double *u_in, const double *rhs, const double *a,
+                      const double *b, const BoxArgs &g, const StencilCoefs &s, hipStream_t st);
 // VCCOMPUTEOP3D (.ChF:181-237)
 void apply_op(double *lu, const double *u, const double *a, const double *b,
               const BoxArgs &g, const StencilCoefs &s, hipStream_t st);

@@ -222,7 +222,39 @@ void VariableCoeffPoissonOperator::setTime(double t) {
   m_lambdaNeedsResetting = true;
 }
 
+bool VariableCoeffPoissonOperator::fusedSmootherApplies() const {
+  // One box covering a non-periodic domain: every face is a BC-folded
+  // domain face, so no exchange is needed inside a sweep and both colour
+  // passes can run in one launch.
+  return prm.fused_smoother && grid->boxes.size() == 1 && grid->nlocal() == 1 &&
+         !grid->periodic[0] && !grid->periodic[1] && !grid->periodic[2] &&
+         kern::gsrb_sweep_fused_supported(args_hom_[0]);
+}
+
+void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n) {
+  resetLambda();  // .cpp:283
+  const hipStream_t st = stream();
+  const StencilCoefs s = coefs();
+  if (!sweep_tmp_) sweep_tmp_ = create();
+  LevelData *src = &dpsi, *dst = sweep_tmp_.get();
+  const long nc = grid->geom[0].valid.ncells();
+  for (int it = 0; it < n; ++it) {
+    prof_mark(st, nc, true);
+    kern::gsrb_sweep_fused(dst->p[0], src->p[0], rhs.p[0], m_aCoef->p[0], m_bCoef->p[0],
+                           args_hom_[0], s, st);
+    prof_mark(st, nc, false);
+    std::swap(src, dst);
+  }
+  if (src != &dpsi)  // odd sweep count: the result sits in the scratch buffer
+    kern::blas(0, dpsi.p[0], src->p[0], nullptr, 0.0, 0.0, args_plain_[0], st);
+}
+
 void VariableCoeffPoissonOperator::relax(LevelData &e, const LevelData &r, int iterations) {
+  if (iterations <= 0) return;
+  if (prm.relax_mode == 1 && fusedSmootherApplies()) {
+    fusedRelax(e, r, iterations);
+    return;
+  }
   for (int it = 0; it < iterations; ++it) {
     switch (prm.relax_mode) {
       case 1: levelGSRB(e, r); break;
@@ -236,20 +268,13 @@ void VariableCoeffPoissonOperator::relax(LevelData &e, const LevelData &r, int i
 }
 
 void VariableCoeffPoissonOperator::levelGSRB(LevelData &dpsi, const LevelData &rhs) {
+  if (fusedSmootherApplies()) {
+    fusedRelax(dpsi, rhs, 1);
+    return;
+  }
   resetLambda();  // .cpp:283
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
-  // One box covering the whole non-periodic domain: no exchange is needed
-  // between the two colour passes, so both run in one fused launch.
-  if (prm.fused_smoother && grid->boxes.size() == 1 && grid->nlocal() == 1 &&
-      !grid->periodic[0] && !grid->periodic[1] && !grid->periodic[2] &&
-      kern::gsrb_sweep_fused_supported(args_hom_[0])) {
-    const long nc = grid->geom[0].valid.ncells();
-    prof_mark(st, nc, true);
-    kern::gsrb_sweep_fused(dpsi.p[0], rhs.p[0], m_aCoef->p[0], m_bCoef->p[0], args_hom_[0], s, st);
-    prof_mark(st, nc, false);
-    return;
-  }
   for (int pass = 0; pass <= 1; ++pass) {  // .cpp:290
     dpsi.exchange(st);                      // .cpp:301 (BC of :307-310 folded)
     for (int n = 0; n < grid->nlocal(); ++n) {

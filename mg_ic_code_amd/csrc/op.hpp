@@ -96,6 +96,13 @@ class VariableCoeffPoissonOperator {
   double reduce(int kind, const LevelData &x, const LevelData *y);
   std::vector<BoxArgs> args_hom_, args_inhom_, args_plain_;
   std::unique_ptr<LevelData> jac_tmp_;
+  std::unique_ptr<LevelData> sweep_tmp_;  // out-of-place buffer of the fused sweep
+
+ public:
+  bool fusedSmootherApplies() const;
+  // `n` levelGSRB sweeps with the fused out-of-place kernel (alternating
+  // dpsi and the scratch buffer; the result always ends in dpsi)
+  void fusedRelax(LevelData &dpsi, const LevelData &rhs, int n);
 };
 
 // CoarseAverage (arithmetic / harmonic) of a fine LevelData onto the layout
