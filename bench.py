@@ -132,6 +132,9 @@ def main():
     fused = launches > 0 and launches == args.steps * 2 * args.nsmooth
     passes_per_launch = 2 if fused else 1
     bytes_per_launch = 48.0 * fine_cells * passes_per_launch  # 48 B/cell/pass
+    # compulsory traffic of one launch: u, rhs, a, b read once + u written
+    # once (40 B/cell) whether one or both colours are updated
+    compulsory = 40.0 * fine_cells
     avg_launch_ms = smooth_ms / launches if launches else float("nan")
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if launches else None
     traffic = None
@@ -182,6 +185,12 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
+                "traffic_GBps": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and launches else None,
+                "compulsory_bytes_per_launch": compulsory,
+                "compulsory_GBps": round(compulsory / (avg_launch_ms * 1e-3) / 1e9, 1) if launches else None,
+                "note": "achieved/frac use SURVEY 8(d)'s 48 B/cell/colour-pass credit (an effective "
+                        "bandwidth: the fused launch does two passes reading each array once, so frac "
+                        "can exceed 1); traffic = PMC HBM bytes per launch (profiles/traffic_smoother.json)",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": round(avg_launch_ms, 5),
                 "launches_timed": launches,

@@ -241,7 +241,7 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   for (int it = 0; it < n; ++it) {
     prof_mark(st, nc, true);
     kern::gsrb_sweep_fused(dst->p[0], src->p[0], rhs.p[0], m_aCoef->p[0], m_bCoef->p[0],
-                           args_hom_[0], s, st);
+                           m_lambda->p[0], args_hom_[0], s, st);
     prof_mark(st, nc, false);
     std::swap(src, dst);
   }
@@ -259,9 +259,9 @@ void VariableCoeffPoissonOperator::relax(LevelData &e, const LevelData &r, int i
     switch (prm.relax_mode) {
       case 1: levelGSRB(e, r); break;
       case 4: levelJacobi(e, r); break;
-      case 2: levelMultiColor(e, r);
-      case 3: looseGSRB(e, r);
-      case 5: overlapGSRB(e, r);
+      case 2: levelMultiColor(e, r); break;
+      case 3: looseGSRB(e, r); break;
+      case 5: overlapGSRB(e, r); break;
       default: levelGSRBLazy(e, r);
     }
   }
