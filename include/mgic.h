@@ -46,6 +46,7 @@ typedef struct mgic_field_s *mgic_field;     /* LevelData<FArrayBox> (1 comp, 1 
 typedef struct mgic_factory_s *mgic_factory; /* VariableCoeffPoissonOperatorFactory */
 typedef struct mgic_op_s *mgic_op;           /* VariableCoeffPoissonOperator */
 typedef struct mgic_mg_s *mgic_mg;           /* AMRMultiGrid on one AMR level */
+typedef struct mgic_plan_s *mgic_plan;       /* host-side view of a Copier plan */
 
 /* Operator constants and ParseBC state (params.txt keys alpha, beta, bc_lo,
  * bc_hi, bc_value, coefficient_average_type; [Chombo] statics). */
@@ -99,6 +100,31 @@ MGIC_API int mgic_grid_destroy(mgic_grid g);
 MGIC_API int mgic_grid_num_local(mgic_grid g, int *n);
 MGIC_API int mgic_grid_local_box(mgic_grid g, int n, int lohi[6], int *global_index);
 MGIC_API int mgic_grid_coarsen(mgic_grid g, int ratio, mgic_grid *out);
+
+/* ---- copy plans, host side (Copier / exchangeDefine + trimEdges,
+ *      Source/VariableCoeffPoissonOperatorFactory.cpp:82-99,179-185).
+ *      The exact plan rank `rank` of `size` executes for a layout pair
+ *      (exchange: src = dst layout, with_faces = 1; gather/scatter for the
+ *      coarse levels: with_valid = 1), computed WITHOUT a GPU so the
+ *      multi-rank path can be checked on CPU.  Items are 12 int64 each:
+ *      {src, dst, soff, doff, ssy, ssz, dsy, dsz, nx, ny, nz, peer}; src/dst
+ *      are local box indices or -1 for the per-peer message buffer, offsets
+ *      are in doubles from the box's valid-lo cell (or from the buffer
+ *      start), strides in doubles.  which: 0 local copies, 1 pack (send),
+ *      2 unpack (receive). */
+MGIC_API int mgic_plan_create(int rank, int size, const int domain[6], const int periodic[3],
+                              int nsrc, const int *src_boxes, const int *src_owners, int ndst,
+                              const int *dst_boxes, const int *dst_owners, int with_valid,
+                              int with_faces, mgic_plan *out);
+MGIC_API int mgic_plan_destroy(mgic_plan p);
+MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpack, int *n_peers);
+MGIC_API int mgic_plan_items(mgic_plan p, int which, long long *items);
+/* per peer (ascending rank): send/recv counts and buffer offsets, doubles */
+MGIC_API int mgic_plan_peers(mgic_plan p, int *peers, long long *send_cnt, long long *send_off,
+                             long long *recv_cnt, long long *recv_off);
+/* FabGeom of local box n of the src (layout = 0) or dst (layout = 1)
+ * layout: {sy, sz, origin, total} in doubles */
+MGIC_API int mgic_plan_geom(mgic_plan p, int layout, int n, long long geom[4]);
 
 /* ---- fields (LevelData<FArrayBox>) */
 MGIC_API int mgic_field_create(mgic_grid g, mgic_field *out);

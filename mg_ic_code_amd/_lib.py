@@ -63,6 +63,7 @@ H = c_void_p  # every opaque handle
 PI = POINTER(c_int)
 PD = POINTER(c_double)
 PH = POINTER(c_void_p)
+PLL = POINTER(ctypes.c_longlong)
 
 # name -> argtypes (all return int status unless listed in _RESTYPE)
 SIGNATURES = {
@@ -86,6 +87,12 @@ SIGNATURES = {
     "mgic_grid_num_local": [H, PI],
     "mgic_grid_local_box": [H, c_int, PI, PI],
     "mgic_grid_coarsen": [H, c_int, PH],
+    "mgic_plan_create": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PI, PI, c_int, c_int, PH],
+    "mgic_plan_destroy": [H],
+    "mgic_plan_sizes": [H, PI, PI, PI, PI],
+    "mgic_plan_items": [H, c_int, PLL],
+    "mgic_plan_peers": [H, PI, PLL, PLL, PLL, PLL],
+    "mgic_plan_geom": [H, c_int, c_int, PLL],
     "mgic_field_create": [H, PH],
     "mgic_field_destroy": [H],
     "mgic_field_device_ptr": [H, c_int, PH, POINTER(c_long)],

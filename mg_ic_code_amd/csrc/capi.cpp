@@ -1,5 +1,6 @@
 // capi.cpp -- extern "C" boundary (include/mgic.h) over the C++ layer.
 #include <cstring>
+#include <map>
 #include <string>
 
 #include "../../include/mgic.h"
@@ -25,6 +26,10 @@ struct mgic_op_s {
 };
 struct mgic_mg_s {
   AMRMultiGrid amg;
+};
+struct mgic_plan_s {
+  std::shared_ptr<Grid> src, dst;
+  std::unique_ptr<CopyPlan> plan;
 };
 
 namespace {
@@ -295,6 +300,104 @@ MGIC_API int mgic_grid_create(mgic_comm c, const int domain[6], const int period
     auto g = std::make_shared<Grid>(c->c, Box::make(domain), per, dx, bx, own);
     MGIC_CHECK(g->tiles_domain(), "boxes must be disjoint and tile the domain");
     *out = new mgic_grid_s{g};
+  });
+}
+MGIC_API int mgic_plan_create(int rank, int size, const int domain[6], const int periodic[3],
+                              int nsrc, const int *src_boxes, const int *src_owners, int ndst,
+                              const int *dst_boxes, const int *dst_owners, int with_valid,
+                              int with_faces, mgic_plan *out) {
+  return guard([&] {
+    NEED(domain);
+    NEED(src_boxes);
+    NEED(src_owners);
+    NEED(dst_boxes);
+    NEED(dst_owners);
+    NEED(out);
+    MGIC_CHECK(nsrc >= 1 && ndst >= 1, "empty layout");
+    bool per[3] = {false, false, false};
+    if (periodic)
+      for (int d = 0; d < 3; ++d) per[d] = periodic[d] != 0;
+    auto comm = Comm::host_only(rank, size);
+    auto layout = [&](int nb, const int *bx, const int *own) {
+      std::vector<Box> b;
+      std::vector<int> o;
+      for (int i = 0; i < nb; ++i) {
+        b.push_back(Box::make(bx + 6 * i));
+        o.push_back(own[i]);
+      }
+      return std::make_shared<Grid>(comm, Box::make(domain), per, 1.0, b, o);
+    };
+    auto p = std::make_unique<mgic_plan_s>();
+    p->src = layout(nsrc, src_boxes, src_owners);
+    p->dst = layout(ndst, dst_boxes, dst_owners);
+    p->plan = build_copy_plan(*p->src, *p->dst, with_valid != 0, with_faces != 0, false);
+    *out = p.release();
+  });
+}
+MGIC_API int mgic_plan_destroy(mgic_plan p) {
+  return guard([&] { delete p; });
+}
+MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpack, int *n_peers) {
+  return guard([&] {
+    NEED(p);
+    std::map<int, int> peers;
+    for (auto &kv : p->plan->send_cnt_) peers[kv.first] = 1;
+    for (auto &kv : p->plan->recv_cnt_) peers[kv.first] = 1;
+    if (n_local) *n_local = (int)p->plan->local_.size();
+    if (n_pack) *n_pack = (int)p->plan->pack_.size();
+    if (n_unpack) *n_unpack = (int)p->plan->unpack_.size();
+    if (n_peers) *n_peers = (int)peers.size();
+  });
+}
+MGIC_API int mgic_plan_items(mgic_plan p, int which, long long *items) {
+  return guard([&] {
+    NEED(p);
+    NEED(items);
+    MGIC_CHECK(which >= 0 && which <= 2, "which must be 0 (local), 1 (pack) or 2 (unpack)");
+    const auto &v = which == 0 ? p->plan->local_ : which == 1 ? p->plan->pack_ : p->plan->unpack_;
+    for (size_t i = 0; i < v.size(); ++i) {
+      const CopyItem &c = v[i];
+      const long long row[12] = {c.src, c.dst, c.soff, c.doff, c.ssy, c.ssz,
+                                 c.dsy, c.dsz, c.nx,   c.ny,   c.nz,  which == 0 ? -1 : c.pad};
+      std::memcpy(items + 12 * i, row, sizeof(row));
+    }
+  });
+}
+MGIC_API int mgic_plan_peers(mgic_plan p, int *peers, long long *send_cnt, long long *send_off,
+                             long long *recv_cnt, long long *recv_off) {
+  return guard([&] {
+    NEED(p);
+    NEED(peers);
+    std::map<int, int> all;
+    for (auto &kv : p->plan->send_cnt_) all[kv.first] = 1;
+    for (auto &kv : p->plan->recv_cnt_) all[kv.first] = 1;
+    int i = 0;
+    for (auto &kv : all) {
+      const int r = kv.first;
+      auto get = [r](const std::map<int, long> &m) {
+        auto it = m.find(r);
+        return it == m.end() ? 0LL : (long long)it->second;
+      };
+      peers[i] = r;
+      if (send_cnt) send_cnt[i] = get(p->plan->send_cnt_);
+      if (send_off) send_off[i] = get(p->plan->send_off_);
+      if (recv_cnt) recv_cnt[i] = get(p->plan->recv_cnt_);
+      if (recv_off) recv_off[i] = get(p->plan->recv_off_);
+      ++i;
+    }
+  });
+}
+MGIC_API int mgic_plan_geom(mgic_plan p, int layout, int n, long long geom[4]) {
+  return guard([&] {
+    NEED(p);
+    NEED(geom);
+    const Grid &g = layout == 0 ? *p->src : *p->dst;
+    MGIC_CHECK(n >= 0 && n < g.nlocal(), "local box index out of range");
+    const FabGeom &f = g.geom[n];
+    geom[0] = f.sy;
+    geom[1] = f.sz;
+    geom[2] = f.origin;
+    geom[3] = f.total;
   });
 }
 MGIC_API int mgic_grid_destroy(mgic_grid g) {

@@ -20,6 +20,14 @@ Comm::Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl)
   MGIC_HIP(hipHostMalloc(&h_result_, 2 * sizeof(double), hipHostMallocDefault));
 }
 
+std::shared_ptr<Comm> Comm::host_only(int rank, int size) {
+  MGIC_CHECK(size >= 1 && rank >= 0 && rank < size, "bad rank/size");
+  std::shared_ptr<Comm> c(new Comm());
+  c->rank_ = rank;
+  c->size_ = size;
+  return c;
+}
+
 Comm::~Comm() {
   if (nccl_) ncclCommDestroy(nccl_);
   if (d_partials_) (void)hipFree(d_partials_);
@@ -143,7 +151,7 @@ BoxArgs Grid::box_args(int n, const int bc_lo[3], const int bc_hi[3], double bc_
 
 // ------------------------------------------------------------------ CopyPlan
 std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool with_valid,
-                                          bool with_faces) {
+                                          bool with_faces, bool upload) {
   auto plan = std::make_unique<CopyPlan>();
   const int me = dst.comm->rank();
   std::vector<int> sloc(src.boxes.size(), -1), dloc(dst.boxes.size(), -1);
@@ -219,7 +227,10 @@ std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool
       }
     }
   }
-  plan->finalize();
+  if (upload)
+    plan->finalize();
+  else
+    plan->finalize_host();
   return plan;
 }
 
@@ -241,8 +252,8 @@ static CopyItem *upload_items(const std::vector<CopyItem> &v, long &maxc) {
   return d;
 }
 
-void CopyPlan::finalize() {
-  if (final_) return;
+void CopyPlan::finalize_host() {
+  if (host_final_) return;
   long off = 0;
   for (auto &kv : send_cnt_) {
     send_off_[kv.first] = off;
@@ -257,6 +268,12 @@ void CopyPlan::finalize() {
   recv_total_ = off;
   for (auto &it : pack_) it.doff += send_off_[it.pad];
   for (auto &it : unpack_) it.soff += recv_off_[it.pad];
+  host_final_ = true;
+}
+
+void CopyPlan::finalize() {
+  if (final_) return;
+  finalize_host();
   d_local_ = upload_items(local_, max_local_);
   d_pack_ = upload_items(pack_, max_pack_);
   d_unpack_ = upload_items(unpack_, max_unpack_);

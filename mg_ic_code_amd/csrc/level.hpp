@@ -30,6 +30,9 @@ namespace mgic {
 class Comm {
  public:
   Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl);
+  // rank/size only, no device resources: host-side planning (the exchange
+  // plans a rank would execute) on machines without a GPU
+  static std::shared_ptr<Comm> host_only(int rank, int size);
   ~Comm();
   int rank() const { return rank_; }
   int size() const { return size_; }
@@ -49,7 +52,8 @@ class Comm {
   double *h_result() const { return h_result_; }
 
  private:
-  int rank_, size_;
+  Comm() = default;
+  int rank_ = 0, size_ = 1;
   bool self_messages_ = false;
   ncclComm_t nccl_ = nullptr;
   hipStream_t stream_ = nullptr;
@@ -65,7 +69,8 @@ class Comm {
 class CopyPlan {
  public:
   ~CopyPlan();
-  void finalize();  // upload item tables, allocate message buffers
+  void finalize_host();  // per-peer buffer offsets (host only)
+  void finalize();       // + upload item tables, allocate message buffers
   // src_tab / dst_tab: device tables of valid-lo pointers per local box
   void execute(Comm &comm, double *const *src_tab, double *const *dst_tab, hipStream_t st);
   bool empty() const { return local_.empty() && pack_.empty() && unpack_.empty(); }
@@ -79,7 +84,7 @@ class CopyPlan {
   CopyItem *d_local_ = nullptr, *d_pack_ = nullptr, *d_unpack_ = nullptr;
   long max_local_ = 0, max_pack_ = 0, max_unpack_ = 0;
   double *sendbuf_ = nullptr, *recvbuf_ = nullptr;
-  bool final_ = false;
+  bool final_ = false, host_final_ = false;
 };
 
 // DisjointBoxLayout + ProblemDomain + dx at one level.
@@ -117,8 +122,9 @@ class Grid {
 // box (with_valid) and/or its six 1-deep face slabs (with_faces); periodic
 // images of src boxes are used in periodic directions.  Both layouts must
 // live on the same domain index space.
+// upload = false: host-side plan only (no device tables / buffers).
 std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool with_valid,
-                                          bool with_faces);
+                                          bool with_faces, bool upload = true);
 
 // LevelData<FArrayBox> with one component and one ghost layer.
 class LevelData {
