@@ -107,7 +107,15 @@ __global__ __launch_bounds__(256) void k_residual(double *__restrict__ r,
 
 // One thread per coarse cell; the 8 fine children are visited in the
 // Fortran k,j,i order so the accumulation res = 0 + t1 + ... + t8
-// (.cpp:177 + .ChF:431-432) rounds exactly like the reference.
+// (.cpp:177 + .ChF:431-432) rounds exactly like the reference.  The two
+// children of a fine row are one 16-B load per array (fine boxes start on
+// even cells and the valid-lo is 128-B aligned); all loads are issued
+// unconditionally (ghost addresses are always allocated) and the domain BC
+// is folded afterwards, as in lap7.
+__device__ __forceinline__ double2 ld2(const double *__restrict__ p) {
+  return *reinterpret_cast<const double2 *>(p);
+}
+
 __global__ __launch_bounds__(256) void k_restrict(double *__restrict__ rc, const BoxArgs cg,
                                                   const double *__restrict__ u,
                                                   const double *__restrict__ rhs,
@@ -121,21 +129,41 @@ __global__ __launch_bounds__(256) void k_restrict(double *__restrict__ rc, const
   const double denom = 2 * 2 * 2;  // .ChF:402
   const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
   double sum = accumulate ? rc[cidx] : 0.0;
+  const int i0 = 2 * ci;
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj)
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * cj + jj, k = 2 * ck + kk;
+      const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
+      const double2 c = ld2(u + row);
+      const double2 ym = ld2(u + row - fg.sy), yp = ld2(u + row + fg.sy);
+      const double2 zm = ld2(u + row - fg.sz), zp = ld2(u + row + fg.sz);
+      const double xl = u[row - 1], xr = u[row + 2];
+      const double2 rv = ld2(rhs + row), av = ld2(a + row), bv = ld2(b + row);
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
-        const int i = 2 * ci + ii, j = 2 * cj + jj, k = 2 * ck + kk;
-        const long idx = (long)i + (long)j * fg.sy + (long)k * fg.sz;
-        const double uc = u[idx];
-        double lofdpsi = s.alpha * a[idx] * uc;               // .ChF:411-412
-        double ldpsi = lap7(u, idx, uc, i, j, k, fg);          // .ChF:416-425
-        ldpsi = ldpsi * s.dxinv * s.beta * b[idx];             // .ChF:427
-        lofdpsi = lofdpsi - ldpsi;                             // .ChF:429
-        sum = sum + (rhs[idx] - lofdpsi) / denom;              // .ChF:431-432
+        const int i = i0 + ii;
+        const double uc = ii ? c.y : c.x;
+        double vxm = ii ? c.x : xl, vxp = ii ? xr : c.y;
+        double vym = ii ? ym.y : ym.x, vyp = ii ? yp.y : yp.x;
+        double vzm = ii ? zm.y : zm.x, vzp = ii ? zp.y : zp.x;
+        if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], fg.bcc[0], uc);
+        if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], fg.bcc[1], uc);
+        if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], fg.bcc[2], uc);
+        if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], fg.bcc[3], uc);
+        if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], fg.bcc[4], uc);
+        if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], fg.bcc[5], uc);
+        const double tx = (vxp + vxm) - 2.0 * uc;
+        const double ty = (vyp + vym) - 2.0 * uc;
+        const double tz = (vzp + vzm) - 2.0 * uc;
+        double ldpsi = (tx + ty) + tz;                                  // .ChF:416-425
+        double lofdpsi = s.alpha * (ii ? av.y : av.x) * uc;            // .ChF:411-412
+        ldpsi = ldpsi * s.dxinv * s.beta * (ii ? bv.y : bv.x);         // .ChF:427
+        lofdpsi = lofdpsi - ldpsi;                                      // .ChF:429
+        sum = sum + ((ii ? rv.y : rv.x) - lofdpsi) / denom;             // .ChF:431-432
       }
+    }
   rc[cidx] = sum;
 }
 
@@ -143,35 +171,66 @@ struct ProlongArgs {
   int avail_lo[3], avail_hi[3];
 };
 
+// One thread per coarse cell, updating its 2x2x2 fine children with two
+// 16-B read-modify-writes per fine row.  Linear (type 1): per direction the
+// slope is taken on the child's side when that coarse neighbour exists
+// (interior, or an exchanged ghost across a box / periodic face), else on the
+// other side; e = c0 + dx-term + dy-term + dz-term in that order.  The six
+// neighbour loads are unconditional (coarse ghosts are always allocated).
+template <int TYPE>
 __global__ __launch_bounds__(256) void k_prolong(double *__restrict__ uf, const BoxArgs fg,
                                                  const double *__restrict__ ec, const BoxArgs cg,
-                                                 const ProlongArgs pa, int type) {
-  const int i = blockIdx.x * TX + threadIdx.x;
-  const int j = blockIdx.y * TY + threadIdx.y;
-  const int k = blockIdx.z;
-  if (i >= fg.nx || j >= fg.ny) return;
-  const int f[3] = {i, j, k};
-  const int ic[3] = {i >> 1, j >> 1, k >> 1};  // fine boxes start on even cells
-  const long cidx = (long)ic[0] + (long)ic[1] * cg.sy + (long)ic[2] * cg.sz;
+                                                 const ProlongArgs pa) {
+  const int ci = blockIdx.x * TX + threadIdx.x;
+  const int cj = blockIdx.y * TY + threadIdx.y;
+  const int ck = blockIdx.z;
+  if (ci >= cg.nx || cj >= cg.ny) return;
+  const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
   const double c0 = ec[cidx];
-  double e = c0;
-  if (type == 1) {
+  double dlo[3] = {0.0, 0.0, 0.0}, dhi[3] = {0.0, 0.0, 0.0};  // slope for lower / upper child
+  bool ok[3] = {false, false, false};
+  if (TYPE == 1) {
     const long cs[3] = {1, cg.sy, cg.sz};
+    const int ic[3] = {ci, cj, ck};
     const int cn[3] = {cg.nx, cg.ny, cg.nz};
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
+      const double lo = ec[cidx - cs[d]], hi = ec[cidx + cs[d]];
       const bool has_lo = (ic[d] > 0) || pa.avail_lo[d];
       const bool has_hi = (ic[d] < cn[d] - 1) || pa.avail_hi[d];
-      const bool upper = (f[d] & 1) != 0;
-      const double fac = upper ? 0.25 : -0.25;
-      const bool use_hi = upper ? has_hi : !has_lo;
-      const bool ok = has_lo || has_hi;
-      const double delta = use_hi ? (ec[cidx + cs[d]] - c0) : (c0 - ec[cidx - cs[d]]);
-      if (ok) e = e + delta * fac;
+      ok[d] = has_lo || has_hi;
+      const double sl_hi = hi - c0, sl_lo = c0 - lo;
+      dhi[d] = (has_hi ? sl_hi : sl_lo) * 0.25;    // upper child: +0.25 * slope
+      dlo[d] = (!has_lo ? sl_hi : sl_lo) * -0.25;  // lower child: -0.25 * slope
     }
   }
-  const long idx = (long)i + (long)j * fg.sy + (long)k * fg.sz;
-  uf[idx] = uf[idx] + e;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const long row = (long)(2 * ci) + (long)(2 * cj + jj) * fg.sy + (long)(2 * ck + kk) * fg.sz;
+      double2 v = ld2(uf + row);
+      double e0 = c0, e1 = c0;
+      if (TYPE == 1) {
+        if (ok[0]) {
+          e0 = e0 + dlo[0];
+          e1 = e1 + dhi[0];
+        }
+        if (ok[1]) {
+          const double t = jj ? dhi[1] : dlo[1];
+          e0 = e0 + t;
+          e1 = e1 + t;
+        }
+        if (ok[2]) {
+          const double t = kk ? dhi[2] : dlo[2];
+          e0 = e0 + t;
+          e1 = e1 + t;
+        }
+      }
+      v.x = v.x + e0;
+      v.y = v.y + e1;
+      *reinterpret_cast<double2 *>(uf + row) = v;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_lambda(double *__restrict__ lam,
@@ -453,7 +512,12 @@ void prolong(double *uf, const BoxArgs &fg, const double *ec, const BoxArgs &cg,
     pa.avail_lo[d] = avail_lo[d];
     pa.avail_hi[d] = avail_hi[d];
   }
-  k_prolong<<<grid_cells(fg.nx, fg.ny, fg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa, type);
+  MGIC_CHECK(fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz,
+             "prolong: fine box must be the coarse box refined by 2");
+  if (type == 1)
+    k_prolong<1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
+  else
+    k_prolong<0><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
   check_launch();
 }
 

@@ -21,10 +21,11 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
 // identical to two in-place gsrb_pass calls.  Needs every face of the box
 // to be a BC-folded domain face (one box per level, smoother.hip).
 bool gsrb_sweep_fused_supported(const BoxArgs &g);
-// lam: the operator's stored lambda (read by variants that do not
-// recompute it; bit-identical either way)
+// one red+black sweep u_in -> u_out (smoother.hip); writes the BC images
+// into u_in's ghost faces first.  zero_in: u_in is identically +0 and is
+// not read (first sweep on a freshly zeroed correction).
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
-                      const double *b, const double *lam, const BoxArgs &g, const StencilCoefs &s,
+                      const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       hipStream_t st);
 // VCCOMPUTEOP3D (.ChF:181-237)
 void apply_op(double *lu, const double *u, const double *a, const double *b,

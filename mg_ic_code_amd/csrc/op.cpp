@@ -231,7 +231,8 @@ bool VariableCoeffPoissonOperator::fusedSmootherApplies() const {
          kern::gsrb_sweep_fused_supported(args_hom_[0]);
 }
 
-void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n) {
+void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
+                                              bool zero_in) {
   resetLambda();  // .cpp:283
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
@@ -241,12 +242,21 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   for (int it = 0; it < n; ++it) {
     prof_mark(st, nc, true);
     kern::gsrb_sweep_fused(dst->p[0], src->p[0], rhs.p[0], m_aCoef->p[0], m_bCoef->p[0],
-                           m_lambda->p[0], args_hom_[0], s, st);
+                           args_hom_[0], s, zero_in && it == 0, st);
     prof_mark(st, nc, false);
     std::swap(src, dst);
   }
   if (src != &dpsi)  // odd sweep count: the result sits in the scratch buffer
     kern::blas(0, dpsi.p[0], src->p[0], nullptr, 0.0, 0.0, args_plain_[0], st);
+}
+
+void VariableCoeffPoissonOperator::relaxFromZero(LevelData &e, const LevelData &r, int n) {
+  if (n > 0 && prm.relax_mode == 1 && fusedSmootherApplies()) {
+    fusedRelax(e, r, n, true);
+    return;
+  }
+  setToZero(e);
+  relax(e, r, n);
 }
 
 void VariableCoeffPoissonOperator::relax(LevelData &e, const LevelData &r, int iterations) {
@@ -590,15 +600,24 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
   MGIC_HIP(hipStreamSynchronize(levels_[0].op->stream()));
 }
 
-void MultiGrid::cycle(int d, LevelData &e, LevelData &r) {
+void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero) {
   VariableCoeffPoissonOperator &op = *levels_[d].op;
   const hipStream_t st = op.stream();
   if (d == (int)levels_.size() - 1) {  // bottom
-    if (prm.bottom_solver == 1) bottom.solve(op, e, r, true);
-    else op.relax(e, r, prm.n_bottom);
+    if (prm.bottom_solver == 1) {
+      if (e_zero) op.setToZero(e);
+      bottom.solve(op, e, r, true);
+    } else if (e_zero) {
+      op.relaxFromZero(e, r, prm.n_bottom);
+    } else {
+      op.relax(e, r, prm.n_bottom);
+    }
     return;
   }
-  op.relax(e, r, prm.n_pre);
+  if (e_zero)
+    op.relaxFromZero(e, r, prm.n_pre);
+  else
+    op.relax(e, r, prm.n_pre);
   Level &N = levels_[d + 1];
   if (!N.agg) {
     op.restrictResidual(*N.r, e, r);
@@ -606,8 +625,8 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r) {
     op.restrictResidual(*N.r_stage, e, r);
     N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
   }
-  N.op->setToZero(*N.e);
-  for (int c = 0; c < prm.cycles; ++c) cycle(d + 1, *N.e, *N.r);
+  // coarse correction e_c = 0 (folded into its first sweep when possible)
+  for (int c = 0; c < prm.cycles; ++c) cycle(d + 1, *N.e, *N.r, c == 0);
   if (!N.agg) {
     op.prolongIncrement(e, *N.e);
   } else {
@@ -626,8 +645,7 @@ void AMRMultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MG
 double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &resid,
                                int normType, bool homogeneous) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
-  op0.setToZero(*corr_);
-  mg.oneCycle(*corr_, resid);
+  mg.oneCycleFromZero(*corr_, resid);  // e = 0; oneCycle(e, r)
   op0.incr(phi, *corr_, 1.0);
   op0.residual(resid, phi, rhs, homogeneous);
   return normType >= 0 ? op0.norm(resid, normType) : -1.0;

@@ -101,8 +101,13 @@ class VariableCoeffPoissonOperator {
  public:
   bool fusedSmootherApplies() const;
   // `n` levelGSRB sweeps with the fused out-of-place kernel (alternating
-  // dpsi and the scratch buffer; the result always ends in dpsi)
-  void fusedRelax(LevelData &dpsi, const LevelData &rhs, int n);
+  // dpsi and the scratch buffer; the result always ends in dpsi).
+  // zero_in: dpsi is taken as identically zero and not read (its memory
+  // need not be zeroed).
+  void fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false);
+  // e = 0; relax(e, r, n) -- without zeroing e in memory when the fused
+  // smoother applies (the first sweep does not read its input)
+  void relaxFromZero(LevelData &e, const LevelData &r, int n);
 };
 
 // CoarseAverage (arithmetic / harmonic) of a fine LevelData onto the layout
@@ -167,7 +172,13 @@ struct MGParams {
 class MultiGrid {
  public:
   void define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &prm);
-  void oneCycle(LevelData &e, const LevelData &r) { cycle(0, e, const_cast<LevelData &>(r)); }
+  void oneCycle(LevelData &e, const LevelData &r) {
+    cycle(0, e, const_cast<LevelData &>(r), false);
+  }
+  // e = 0; oneCycle(e, r)
+  void oneCycleFromZero(LevelData &e, const LevelData &r) {
+    cycle(0, e, const_cast<LevelData &>(r), true);
+  }
   int depths() const { return (int)levels_.size(); }
   VariableCoeffPoissonOperator &op(int d) { return *levels_[d].op; }
   LevelData *corr(int d) { return levels_[d].e.get(); }
@@ -184,7 +195,8 @@ class MultiGrid {
     std::unique_ptr<LevelData> r_stage, e_stage;  // previous layout coarsened
     std::unique_ptr<CopyPlan> restrict_plan, prolong_plan;
   };
-  void cycle(int d, LevelData &e, LevelData &r);
+  // e_zero: treat e as zero on entry (it is zeroed or never read)
+  void cycle(int d, LevelData &e, LevelData &r, bool e_zero);
   std::vector<Level> levels_;
 };
 
