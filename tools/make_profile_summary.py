@@ -62,11 +62,12 @@ def main():
 
     fetch = counters(os.path.join(d, "pmc_fetch", f"{args.tag}_counter_collection.csv"))
     write = counters(os.path.join(d, "pmc_write", f"{args.tag}_counter_collection.csv"))
-    # finest level = the largest grid of the smoother kernel
+    # finest level = the largest grid of the smoother kernel; among its
+    # instantiations the one launched most (the steady-state sweep)
     keys = [k for k in fetch if k[0].startswith(args.kernel)]
     if not keys:
         raise SystemExit("no smoother dispatches in the PMC passes")
-    k = max(keys, key=lambda kk: kk[1])
+    k = max(keys, key=lambda kk: (kk[1], len(fetch[kk]["FETCH_SIZE"])))
     fb = sum(fetch[k]["FETCH_SIZE"]) / len(fetch[k]["FETCH_SIZE"]) * 1024 * 2
     wb = sum(write[k]["WRITE_SIZE"]) / len(write[k]["WRITE_SIZE"]) * 1024
     fused = "fused" in k[0]
