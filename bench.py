@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--nsmooth", type=int, default=4)
     ap.add_argument("--no-fused", action="store_true", help="per-colour smoother launches")
+    ap.add_argument("--boxes-per-rank", default="1,1,1",
+                    help="split each rank's share into this many boxes (x,y,z) -- the multi-box "
+                         "(exchange) path on one GPU")
     ap.add_argument("--cpu-baseline-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -82,7 +85,8 @@ def main():
     dx = prm.L / n
     bh = prm.bh()
     bh["domain_length"] = dx * n
-    dom, boxes, owners = decompose((n, n, n), world)
+    bpr = tuple(int(v) for v in args.boxes_per_rank.split(","))
+    dom, boxes, owners = decompose((n, n, n), world, boxes_per_rank=bpr)
     grid = mg.Grid(comm, dom, boxes, dx, owners=owners)
     fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
     mg.set_binary_bh_coefs(fa, frhs, bh)
@@ -118,7 +122,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    launches, smooth_ms = mg.prof_smoother_read()
+    launches, passes, smooth_ms = mg.prof_smoother_read()
     mg.prof_smoother(False)
     r_final = amg.init_residual(fphi, frhs, fres, norm_type=0)
     if dist is not None:
@@ -127,13 +131,13 @@ def main():
         dist_.all_reduce(t, op=dist_.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # dominant kernel: the fine-level smoother
-    op0 = amg.op(0)
-    fused = launches > 0 and launches == args.steps * 2 * args.nsmooth
-    passes_per_launch = 2 if fused else 1
+    # dominant kernel: the fine-level smoother; passes_per_launch = 1 (one
+    # colour pass), 2 (fused sweep) or 4 (two fused sweeps per launch)
+    passes_per_launch = passes / launches if launches else 0.0
+    fused = passes_per_launch >= 2
     bytes_per_launch = 48.0 * fine_cells * passes_per_launch  # 48 B/cell/pass
     # compulsory traffic of one launch: u, rhs, a, b read once + u written
-    # once (40 B/cell) whether one or both colours are updated
+    # once (40 B/cell), however many colour passes the launch performs
     compulsory = 40.0 * fine_cells
     avg_launch_ms = smooth_ms / launches if launches else float("nan")
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if launches else None
@@ -143,7 +147,7 @@ def main():
         try:
             with open(tj) as f:
                 tinfo = json.load(f)
-            key = f"n{n}_w{world}_{'fused' if fused else 'pass'}"
+            key = f"n{n}_w{world}_{ {1: 'pass', 2: 'fused', 4: 'fused2x'}.get(round(passes_per_launch), 'mixed')}"
             if key in tinfo:
                 traffic = tinfo[key]["hbm_bytes_per_launch"]
         except Exception:
@@ -179,7 +183,9 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "fused red-black GSRB sweep" if fused else "GSRB colour pass",
+                "kernel": {4: "two fused red-black GSRB sweeps per launch", 2: "fused red-black GSRB sweep",
+                           1: "GSRB colour pass"}.get(round(passes_per_launch), "mixed smoother launches"),
+                "colour_passes_per_launch": round(passes_per_launch, 3),
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -208,9 +208,10 @@ MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
                                    double *norm);
 
 /* ---- instrumentation: hipEvents around every smoother launch on boxes of
- * at least min_cells cells */
+ * at least min_cells cells; passes = colour passes those launches performed
+ * (1 per-colour launch, 2 one fused sweep, 4 two fused sweeps) */
 MGIC_API int mgic_prof_smoother(int enable, long min_cells);
-MGIC_API int mgic_prof_smoother_read(int *launches, double *total_ms);
+MGIC_API int mgic_prof_smoother_read(int *launches, long *passes, double *total_ms);
 
 #ifdef __cplusplus
 }

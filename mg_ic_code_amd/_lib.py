@@ -142,7 +142,7 @@ SIGNATURES = {
     "mgic_mg_iteration": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
     "mgic_prof_smoother": [c_int, c_long],
-    "mgic_prof_smoother_read": [PI, PD],
+    "mgic_prof_smoother_read": [PI, POINTER(c_long), PD],
     # ChomboFortran drop-ins (include/mgic_chf.h); argtypes left open
     "gsrbhelmholtzvc3d_": None,
     "vccomputeop3d_": None,

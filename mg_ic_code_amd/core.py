@@ -558,8 +558,10 @@ def prof_smoother(enable: bool, min_cells: int = 0) -> None:
     call("mgic_prof_smoother", int(bool(enable)), int(min_cells))
 
 
-def prof_smoother_read() -> Tuple[int, float]:
+def prof_smoother_read() -> Tuple[int, int, float]:
+    """(launches, colour passes, total ms) since prof_smoother(True)."""
     n = ctypes.c_int()
+    np_ = ctypes.c_long()
     t = ctypes.c_double()
-    call("mgic_prof_smoother_read", ctypes.byref(n), ctypes.byref(t))
-    return n.value, t.value
+    call("mgic_prof_smoother_read", ctypes.byref(n), ctypes.byref(np_), ctypes.byref(t))
+    return n.value, np_.value, t.value

@@ -749,11 +749,13 @@ MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs, m
 MGIC_API int mgic_prof_smoother(int enable, long min_cells) {
   return guard([&] { prof_enable(enable != 0, min_cells); });
 }
-MGIC_API int mgic_prof_smoother_read(int *launches, double *total_ms) {
+MGIC_API int mgic_prof_smoother_read(int *launches, long *passes, double *total_ms) {
   return guard([&] {
     double t = 0.0;
-    const int n = prof_read(&t);
+    long np = 0;
+    const int n = prof_read(&t, &np);
     if (launches) *launches = n;
+    if (passes) *passes = np;
     if (total_ms) *total_ms = t;
   });
 }

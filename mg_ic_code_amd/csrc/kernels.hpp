@@ -18,15 +18,19 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
                hipStream_t st);
 // Fused red+black sweep (both passes of one levelGSRB, .cpp:290-331) in one
 // launch, staged through LDS, OUT OF PLACE: u_out = sweep(u_in); bit-
-// identical to two in-place gsrb_pass calls.  Needs every face of the box
-// to be a BC-folded domain face (one box per level, smoother.hip).
-bool gsrb_sweep_fused_supported(const BoxArgs &g);
-// one red+black sweep u_in -> u_out (smoother.hip); writes the BC images
-// into u_in's ghost faces first.  zero_in: u_in is identically +0 and is
+// identical to two in-place gsrb_pass calls with an exchange before each.
+// Domain faces (bcm != 0): the BC images are written into u_in's ghost
+// layer first.  Exchanged faces (bcm == 0): u_in must hold the 2-deep ghost
+// shell and rhs/a/b ghost layer 1.  zero_in: u_in is identically +0 and is
 // not read (first sweep on a freshly zeroed correction).
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       hipStream_t st);
+// two red+black sweeps u_in -> u_out in one launch (temporal blocking);
+// BC folded in-kernel, u_in is not modified (zero_in: not read either)
+void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,
+                        const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                        hipStream_t st);
 // VCCOMPUTEOP3D (.ChF:181-237)
 void apply_op(double *lu, const double *u, const double *a, const double *b,
               const BoxArgs &g, const StencilCoefs &s, hipStream_t st);

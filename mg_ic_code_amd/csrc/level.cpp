@@ -100,6 +100,20 @@ CopyPlan &Grid::exchange_plan() {
   return *exchange_;
 }
 
+CopyPlan &Grid::shell_plan() {
+  if (!shell_) shell_ = build_copy_plan(*this, *this, false, false, true, 2);
+  return *shell_;
+}
+
+bool Grid::has_memory_faces() const {
+  for (int n = 0; n < nlocal(); ++n) {
+    const Box &v = geom[n].valid;
+    for (int d = 0; d < 3; ++d)
+      if (periodic[d] || v.lo[d] != domain.lo[d] || v.hi[d] != domain.hi[d]) return true;
+  }
+  return false;
+}
+
 BoxArgs Grid::box_args_plain(int n) const {
   BoxArgs a{};
   const FabGeom &g = geom[n];
@@ -151,7 +165,7 @@ BoxArgs Grid::box_args(int n, const int bc_lo[3], const int bc_hi[3], double bc_
 
 // ------------------------------------------------------------------ CopyPlan
 std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool with_valid,
-                                          bool with_faces, bool upload) {
+                                          bool with_faces, bool upload, int shell) {
   auto plan = std::make_unique<CopyPlan>();
   const int me = dst.comm->rank();
   std::vector<int> sloc(src.boxes.size(), -1), dloc(dst.boxes.size(), -1);
@@ -167,6 +181,27 @@ std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool
     if (with_faces)
       for (int dir = 0; dir < 3; ++dir)
         for (int side = 0; side < 2; ++side) regions.push_back(dv.adj_cell(dir, side));
+    if (shell > 0) {  // grow(dv, shell) \ dv as six disjoint slabs: the x slabs span
+      // the grown y and z ranges, the y slabs the valid x and grown z, the z
+      // slabs the valid x and y
+      for (int dir = 0; dir < 3; ++dir)
+        for (int side = 0; side < 2; ++side) {
+          Box r = dv;
+          for (int d = 0; d < 3; ++d)
+            if (d > dir) {
+              r.lo[d] -= shell;
+              r.hi[d] += shell;
+            }
+          if (side == 0) {
+            r.hi[dir] = dv.lo[dir] - 1;
+            r.lo[dir] = dv.lo[dir] - shell;
+          } else {
+            r.lo[dir] = dv.hi[dir] + 1;
+            r.hi[dir] = dv.hi[dir] + shell;
+          }
+          regions.push_back(r);
+        }
+    }
     const int od = dst.owners[db];
     for (const Box &R : regions) {
       for (size_t sb = 0; sb < src.boxes.size(); ++sb) {
@@ -332,6 +367,12 @@ void LevelData::set_zero_all(hipStream_t st) {
 
 void LevelData::exchange(hipStream_t st) {
   CopyPlan &pl = grid->exchange_plan();
+  if (pl.empty()) return;
+  pl.execute(*grid->comm, d_tab, d_tab, st);
+}
+
+void LevelData::exchange_shell(hipStream_t st) {
+  CopyPlan &pl = grid->shell_plan();
   if (pl.empty()) return;
   pl.execute(*grid->comm, d_tab, d_tab, st);
 }

@@ -107,6 +107,10 @@ class Grid {
   std::shared_ptr<Grid> coarsened(int r) const;
   // face ghost exchange plan (exchangeDefine(grids, Unit) + trimEdges)
   CopyPlan &exchange_plan();
+  // full 2-deep ghost shell (faces, edges, corners): what a fused sweep
+  // needs to recompute the neighbours' red values on its own ghost layer
+  CopyPlan &shell_plan();
+  bool has_memory_faces() const;  // some local box face is exchanged
   // BoxArgs of local box n with the face BC modes for (bc flags, value,
   // homogeneous); faces that are not domain faces (or are periodic) get
   // kBcMemory.
@@ -115,7 +119,7 @@ class Grid {
   BoxArgs box_args_plain(int n) const;  // all faces kBcMemory
 
  private:
-  std::unique_ptr<CopyPlan> exchange_;
+  std::unique_ptr<CopyPlan> exchange_, shell_;
 };
 
 // Build a copy plan from src layout to dst layout.  dst regions: the valid
@@ -123,8 +127,9 @@ class Grid {
 // images of src boxes are used in periodic directions.  Both layouts must
 // live on the same domain index space.
 // upload = false: host-side plan only (no device tables / buffers).
+// shell > 0: instead of the 1-deep faces, the full ghost shell of that depth.
 std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool with_valid,
-                                          bool with_faces, bool upload = true);
+                                          bool with_faces, bool upload = true, int shell = 0);
 
 // LevelData<FArrayBox> with one component and one ghost layer.
 class LevelData {
@@ -140,6 +145,7 @@ class LevelData {
   double *ptr(int n) const { return p[n]; }
   void set_zero_all(hipStream_t st);  // valid + ghosts
   void exchange(hipStream_t st);
+  void exchange_shell(hipStream_t st);  // 2-deep faces + edges + corners
 };
 
 }  // namespace mgic

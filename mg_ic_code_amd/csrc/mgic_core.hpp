@@ -21,7 +21,8 @@
 
 namespace mgic {
 
-constexpr int kGhost = 1;     // ghost depth (CH_assert(ghostVect >= Unit), .cpp:279)
+constexpr int kGhost = 2;     // ghost depth allocated: 1 for the stencils (CH_assert(ghostVect >=
+                              // Unit), .cpp:279) + 1 for the fused sweep's halo (shell exchange)
 constexpr int kRowAlign = 16; // doubles: 128-byte rows
 
 struct Error : std::runtime_error {

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace mgic {
 
@@ -15,6 +16,7 @@ struct SmootherProf {
   std::vector<hipEvent_t> ev;
   size_t used = 0;
   bool open = false;
+  long passes = 0;  // colour passes covered by the recorded launches
 } g_prof;
 }  // namespace
 
@@ -23,9 +25,10 @@ void prof_enable(bool on, long min_cells) {
   g_prof.min_cells = min_cells;
   g_prof.used = 0;
   g_prof.open = false;
+  g_prof.passes = 0;
 }
 
-static void prof_mark(hipStream_t st, long ncells, bool begin) {
+static void prof_mark(hipStream_t st, long ncells, bool begin, int passes) {
   if (!g_prof.on || ncells < g_prof.min_cells) return;
   if (begin) {
     if (g_prof.used + 2 > g_prof.ev.size()) {
@@ -41,11 +44,12 @@ static void prof_mark(hipStream_t st, long ncells, bool begin) {
   } else if (g_prof.open) {
     MGIC_HIP(hipEventRecord(g_prof.ev[g_prof.used + 1], st));
     g_prof.used += 2;
+    g_prof.passes += passes;
     g_prof.open = false;
   }
 }
 
-int prof_read(double *total_ms) {
+int prof_read(double *total_ms, long *passes) {
   double tot = 0.0;
   if (g_prof.used) MGIC_HIP(hipEventSynchronize(g_prof.ev[g_prof.used - 1]));
   for (size_t i = 0; i + 1 < g_prof.used; i += 2) {
@@ -54,6 +58,7 @@ int prof_read(double *total_ms) {
     tot += ms;
   }
   *total_ms = tot;
+  if (passes) *passes = g_prof.passes;
   return (int)(g_prof.used / 2);
 }
 
@@ -200,6 +205,7 @@ void VariableCoeffPoissonOperator::setCoefs(std::shared_ptr<LevelData> a,
   m_aCoef = std::move(a);
   m_bCoef = std::move(b);
   m_lambdaNeedsResetting = true;
+  coef_ghosts_ = false;
 }
 
 void VariableCoeffPoissonOperator::resetLambda() {
@@ -223,12 +229,20 @@ void VariableCoeffPoissonOperator::setTime(double t) {
 }
 
 bool VariableCoeffPoissonOperator::fusedSmootherApplies() const {
-  // One box covering a non-periodic domain: every face is a BC-folded
-  // domain face, so no exchange is needed inside a sweep and both colour
-  // passes can run in one launch.
-  return prm.fused_smoother && grid->boxes.size() == 1 && grid->nlocal() == 1 &&
-         !grid->periodic[0] && !grid->periodic[1] && !grid->periodic[2] &&
-         kern::gsrb_sweep_fused_supported(args_hom_[0]);
+  // Both colour passes of a sweep in one launch per box.  Faces on the
+  // domain boundary fold the BC; exchanged faces (box or periodic
+  // neighbours) get a 2-deep ghost shell before the sweep, from which the
+  // kernel recomputes the neighbours' red values on its ghost layer -- the
+  // values the reference's second exchange (.cpp:301, black pass) delivers.
+  return prm.fused_smoother != 0;
+}
+
+static int sweeps_per_launch() {
+  static const int v = [] {
+    const char *e = getenv("MGIC_SWEEPS_PER_LAUNCH");
+    return e ? std::max(1, std::min(2, atoi(e))) : 1;
+  }();
+  return v;
 }
 
 void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
@@ -237,17 +251,38 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
   if (!sweep_tmp_) sweep_tmp_ = create();
-  LevelData *src = &dpsi, *dst = sweep_tmp_.get();
-  const long nc = grid->geom[0].valid.ncells();
-  for (int it = 0; it < n; ++it) {
-    prof_mark(st, nc, true);
-    kern::gsrb_sweep_fused(dst->p[0], src->p[0], rhs.p[0], m_aCoef->p[0], m_bCoef->p[0],
-                           args_hom_[0], s, zero_in && it == 0, st);
-    prof_mark(st, nc, false);
-    std::swap(src, dst);
+  const bool halo = grid->has_memory_faces();
+  if (halo) {  // ghost layer 1 of rhs / aCoef / bCoef for the red ring on the halo
+    const_cast<LevelData &>(rhs).exchange(st);
+    if (!coef_ghosts_) {
+      m_aCoef->exchange(st);
+      m_bCoef->exchange(st);
+      coef_ghosts_ = true;
+    }
   }
-  if (src != &dpsi)  // odd sweep count: the result sits in the scratch buffer
-    kern::blas(0, dpsi.p[0], src->p[0], nullptr, 0.0, 0.0, args_plain_[0], st);
+  LevelData *src = &dpsi, *dst = sweep_tmp_.get();
+  const int per = sweeps_per_launch();
+  for (int it = 0; it < n;) {
+    const bool zin = zero_in && it == 0;
+    const int k = (per == 2 && !halo && n - it >= 2) ? 2 : 1;
+    if (halo && !zin) src->exchange_shell(st);
+    for (int b = 0; b < grid->nlocal(); ++b) {
+      const long nc = grid->geom[b].valid.ncells();
+      prof_mark(st, nc, true, 2 * k);
+      if (k == 2)  // two sweeps in one launch (temporal blocking)
+        kern::gsrb_sweep_fused2x(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
+                                 args_hom_[b], s, zin, st);
+      else
+        kern::gsrb_sweep_fused(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
+                               args_hom_[b], s, zin, st);
+      prof_mark(st, nc, false, 2 * k);
+    }
+    std::swap(src, dst);
+    it += k;
+  }
+  if (src != &dpsi)  // the result sits in the scratch buffer
+    for (int b = 0; b < grid->nlocal(); ++b)
+      kern::blas(0, dpsi.p[b], src->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
 }
 
 void VariableCoeffPoissonOperator::relaxFromZero(LevelData &e, const LevelData &r, int n) {
@@ -289,10 +324,10 @@ void VariableCoeffPoissonOperator::levelGSRB(LevelData &dpsi, const LevelData &r
     dpsi.exchange(st);                      // .cpp:301 (BC of :307-310 folded)
     for (int n = 0; n < grid->nlocal(); ++n) {
       const long nc = grid->geom[n].valid.ncells();
-      prof_mark(st, nc, true);
+      prof_mark(st, nc, true, 1);
       kern::gsrb_pass(dpsi.p[n], rhs.p[n], m_aCoef->p[n], m_bCoef->p[n], nullptr, args_hom_[n], s,
                       pass, st);  // .cpp:313-330
-      prof_mark(st, nc, false);
+      prof_mark(st, nc, false, 1);
     }
   }
 }

@@ -87,6 +87,7 @@ class VariableCoeffPoissonOperator {
   std::shared_ptr<LevelData> m_aCoef, m_bCoef;
   std::unique_ptr<LevelData> m_lambda;
   bool m_lambdaNeedsResetting = true;
+  bool coef_ghosts_ = false;  // aCoef/bCoef face ghosts exchanged (fused sweep)
 
 
  private:
@@ -118,7 +119,7 @@ std::shared_ptr<LevelData> average_coef(const LevelData &fine, std::shared_ptr<G
 // Smoother instrumentation: when enabled, every smoother launch on a box of
 // at least min_cells cells is bracketed by hipEvents on its stream.
 void prof_enable(bool on, long min_cells);
-int prof_read(double *total_ms);  // returns launches timed, total ms
+int prof_read(double *total_ms, long *passes);  // returns launches timed, total ms
 
 // VariableCoeffPoissonOperatorFactory (single AMR level; the configs have one)
 class VariableCoeffPoissonOperatorFactory {

@@ -84,7 +84,14 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   const int tid = threadIdx.x;
   const long sy = g.sy, sz = g.sz;
   const int nx = g.nx, ny = g.ny, nz = g.nz;
-  const int xpmax = nx & ~1;  // last pair start that can hold a needed element
+  // last pair start that can hold a needed element (x <= nx + 1); a pair
+  // past the row end reads the next row's padding or the allocation slack
+  const int xpmax = (nx + 1) & ~1;
+  // the red ring extends onto ghost layer 1 across exchanged faces (the
+  // neighbours' red values there are recomputed from the 2-deep shell)
+  const int rxlo = g.bcm[0] ? 0 : -1, rxhi = g.bcm[1] ? nx - 1 : nx;
+  const int rylo = g.bcm[2] ? 0 : -1, ryhi = g.bcm[3] ? ny - 1 : ny;
+  const int rzlo = g.bcm[4] ? 0 : -1, rzhi = g.bcm[5] ? nz - 1 : nz;
   const int q0 = (x0 + g.glo[0] + g.glo[1] + g.glo[2]) & 1;
   auto slot = [](int p) { return ((p % 5) + 5) % 5; };
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
@@ -98,7 +105,7 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
     const int r = c / PW, m = c - r * PW;
     lgy[i] = y0 - 2 + r;
     const int gx = min(x0 - 2 + 2 * m, xpmax);
-    loff[i] = c < CP ? (long)gx + (long)clampi(lgy[i], -1, ny) * sy : 0;
+    loff[i] = c < CP ? (long)gx + (long)clampi(lgy[i], -2, ny + 1) * sy : 0;
   }
   // ring pairs owned by this thread (coefficient loads, red/black updates)
   long roff[NP], rcoff[NP];
@@ -112,10 +119,11 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
     roff[i] = (long)rgx0[i] + (long)rgy[i] * sy;
     rcoff[i] = c < NRP ? (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], -1, ny) * sy : 0;
     rci[i] = (rr + 1) * PW + m;
-    rrow[i] = c < NRP && rgy[i] >= 0 && rgy[i] < ny;
-    rtile[i] = rrow[i] && rr >= 1 && rr <= TY && m >= 1 && m <= TX / 2 && rgx0[i] < nx;
+    rrow[i] = c < NRP && rgy[i] >= rylo && rgy[i] <= ryhi;
+    rtile[i] = c < NRP && rgy[i] >= 0 && rgy[i] < ny && rr >= 1 && rr <= TY && m >= 1 &&
+               m <= TX / 2 && rgx0[i] < nx;
   }
-  const int gxlo = max(x0 - 1, 0), gxhi = min(x0 + TX, nx - 1);  // red ring extent
+  const int gxlo = max(x0 - 1, rxlo), gxhi = min(x0 + TX, rxhi);  // red ring extent
 
   double pu0[NL], pu1[NL];
   double cr0[NP], cr1[NP], ca0[NP], ca1[NP], cb0[NP], cb1[NP];
@@ -123,7 +131,7 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   double kr[NP], ka[NP], kb[NP];
 
   auto fetch_u = [&](int p) {
-    const long pz = (long)clampi(p, -1, nz) * sz;
+    const long pz = (long)clampi(p, -2, nz + 1) * sz;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (ZIN) {  // the input is identically +0 (a freshly zeroed correction)
@@ -148,7 +156,7 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
     }
   };
   auto fetch_c = [&](int p) {
-    const long pz = (long)clampi(p, 0, nz - 1) * sz;
+    const long pz = (long)clampi(p, -1, nz) * sz;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const long off = rcoff[i] + pz;
@@ -190,7 +198,7 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
     fetch_u(p + 2);
     fetch_c(p + 1);
     __syncthreads();
-    if (p >= 0 && p < nz) {  // RED cells of plane p on the ring
+    if (p >= rzlo && p <= rzhi) {  // RED cells of plane p on the ring
       double *Rs = R + slot(p) * CP;
       const double *Bs = B + slot(p) * CP;
       const double *Bm = B + slot(p - 1) * CP;
@@ -272,21 +280,312 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused6(double *__restrict__ uo,
                                   min(z0 + kc, g.nz));
 }
 
-// All six face ghost layers of one box in one launch (faces with a BC only;
-// each face writes its own ghost cells, edges and corners are untouched).
+// ---- two sweeps per launch (temporal blocking) ---------------------------
+// The same streaming scheme carried two sweeps deep: at step p the workgroup
+// updates RED(sweep 1) on plane p, BLACK(1) on p-1, RED(2) on p-2 and
+// BLACK(2) on p-3, on rings of width 3, 2, 1, 0 around its tile, then stores
+// plane p-3.  Each plane lives in one LDS slot from its load until its final
+// store and is updated in place by the four stages (a colour pass reads only
+// the other colour, so in-place order inside a pass does not matter).
+// Compulsory traffic: 40 B/cell per TWO sweeps.  The domain BC is folded into
+// every update (a ghost is the BC image of the cell being updated, before its
+// update -- exactly the value ParseBC writes before each colour pass), so no
+// ghost fill is needed.  rhs/a/b: the pair of plane p+1 is loaded one step
+// ahead for stages 1-2 (kept in registers, as in the single sweep); stages
+// 3-4 reload their element from the cache hierarchy two / three steps later.
+template <int TX, int TY, int NT>
+struct Fused2x {
+  static_assert(TX % 2 == 0, "TX must be even");
+  static constexpr int PW = TX / 2 + 4;      // pairs per region row (x0-4 .. x0+TX+3)
+  static constexpr int LH = TY + 8;          // region rows y0-4 .. y0+TY+3
+  static constexpr int CP = PW * LH;         // pairs per plane
+  static constexpr int NRP = PW * (TY + 6);  // ring pairs (rows y0-3 .. y0+TY+2)
+  static constexpr int NL = (CP + NT - 1) / NT;
+  static constexpr int NP = (NRP + NT - 1) / NT;
+  static constexpr int S = 7;                // LDS ring planes p-5 .. p+1
+};
+
+template <int TX, int TY, int NT, bool ZIN>
+__global__ __launch_bounds__(NT) void k_gsrb_fused2x(double *__restrict__ uo,
+                                                     const double *__restrict__ ui,
+                                                     const double *__restrict__ rhs,
+                                                     const double *__restrict__ a,
+                                                     const double *__restrict__ b,
+                                                     const BoxArgs g, const StencilCoefs s, int kc,
+                                                     int ntx, int nty, int nblocks) {
+  using F = Fused2x<TX, TY, NT>;
+  constexpr int PW = F::PW, CP = F::CP, NRP = F::NRP, NL = F::NL, NP = F::NP, S = F::S;
+  __shared__ double R[S * CP];  // red element of every pair
+  __shared__ double B[S * CP];  // black element
+
+  const int bid = blockIdx.x;  // XCD-aware: consecutive tiles on one XCD
+  const int q8 = nblocks / 8, r8 = nblocks % 8;
+  const int xcd = bid % 8, i8 = bid / 8;
+  const int L = xcd * q8 + min(xcd, r8) + i8;
+  const int tx_ = L % ntx, ty_ = (L / ntx) % nty, tz_ = L / (ntx * nty);
+  const int x0 = tx_ * TX, y0 = ty_ * TY;
+  const int z0 = tz_ * kc, z1 = min(z0 + kc, g.nz);
+  const int tid = threadIdx.x;
+  const long sy = g.sy, sz = g.sz;
+  const int nx = g.nx, ny = g.ny, nz = g.nz;
+  const int xpmax = nx & ~1;
+  const int q0 = (x0 + g.glo[0] + g.glo[1] + g.glo[2]) & 1;
+  auto slot = [](int p) { return ((p % S) + S) % S; };
+  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+
+  long loff[NL];
+  int lgy[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = tid + i * NT;
+    const int r = c / PW, m = c - r * PW;
+    lgy[i] = y0 - 4 + r;
+    loff[i] = c < CP ? (long)min(x0 - 4 + 2 * m, xpmax) + (long)clampi(lgy[i], -1, ny) * sy : 0;
+  }
+  long roff[NP], rcoff[NP];
+  int rgy[NP], rgx0[NP], rci[NP], rok[NP], rtile[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int c = tid + i * NT;
+    const int rr = c / PW, m = c - rr * PW;
+    rgy[i] = y0 - 3 + rr;
+    rgx0[i] = x0 - 4 + 2 * m;
+    roff[i] = (long)rgx0[i] + (long)rgy[i] * sy;
+    rcoff[i] = c < NRP ? (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], -1, ny) * sy : 0;
+    rci[i] = (rr + 1) * PW + m;
+    rok[i] = c < NRP && rgy[i] >= 0 && rgy[i] < ny;
+    rtile[i] = rok[i] && rr >= 3 && rr <= TY + 2 && m >= 2 && m <= TX / 2 + 1 && rgx0[i] < nx;
+  }
+  // no cell this workgroup updates touches an x or y domain face
+  const bool xy_interior = x0 - 4 > 0 && x0 + TX + 3 < nx - 1 && y0 - 4 > 0 && y0 + TY + 3 < ny - 1;
+  // cell (gx, gy) is on the ring of width w around the tile, inside the box
+  auto on_ring = [&](int gx, int gy, int w) {
+    return gx >= max(x0 - w, 0) && gx <= min(x0 + TX - 1 + w, nx - 1) && gy >= max(y0 - w, 0) &&
+           gy <= min(y0 + TY - 1 + w, ny - 1);
+  };
+
+  double pu0[NL], pu1[NL];
+  double c0r0[NP], c0r1[NP], c0a0[NP], c0a1[NP], c0b0[NP], c0b1[NP];  // plane p (pairs)
+  double nr0[NP], nr1[NP], na0[NP], na1[NP], nb0[NP], nb1[NP];        // plane p+1 (loading)
+  double c1r[NP], c1a[NP], c1b[NP];  // black element, plane p-1 (stage 2)
+  double c3r[NP], c3a[NP], c3b[NP];  // red element, plane p-2 (stage 3)
+  double c4r[NP], c4a[NP], c4b[NP];  // black element, plane p-3 (stage 4)
+
+  auto fetch_u = [&](int p) {
+    const long pz = (long)clampi(p, -1, nz) * sz;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      if (ZIN) {  // the input is identically +0 (a freshly zeroed correction)
+        pu0[i] = 0.0;
+        pu1[i] = 0.0;
+      } else {
+        const double2 v = *reinterpret_cast<const double2 *>(ui + loff[i] + pz);
+        pu0[i] = v.x;
+        pu1[i] = v.y;
+      }
+    }
+  };
+  auto put_u = [&](int p) {
+    double *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + i * NT;
+      if (NL * NT > CP && c >= CP) continue;
+      const int q = (q0 + lgy[i] + p) & 1;  // 1: the red element is the second
+      Rs[c] = bsel(q, pu1[i], pu0[i]);
+      Bs[c] = bsel(q, pu0[i], pu1[i]);
+    }
+  };
+  auto fetch_c = [&](int p) {
+    const long pz = (long)clampi(p, 0, nz - 1) * sz;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const long off = rcoff[i] + pz;
+      const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
+      const double2 va = *reinterpret_cast<const double2 *>(a + off);
+      const double2 vb = *reinterpret_cast<const double2 *>(b + off);
+      nr0[i] = vr.x; nr1[i] = vr.y;
+      na0[i] = va.x; na1[i] = va.y;
+      nb0[i] = vb.x; nb1[i] = vb.y;
+    }
+  };
+  // the element of colour `black` (0 red, 1 black) of every ring pair, plane p
+  auto fetch_elem = [&](int p, int black, double *r, double *av, double *bv) {
+    const long pz = (long)clampi(p, 0, nz - 1) * sz;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int e = ((q0 + rgy[i] + p) & 1) ^ black;
+      const long off = rcoff[i] + pz + e;
+      r[i] = rhs[off];
+      av[i] = a[off];
+      bv[i] = b[off];
+    }
+  };
+  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
+                 double rv, double av, double bv, int gx, int gy, int p) -> double {
+    if (!xy_interior) {  // SetBCs.cpp:49-131 folded (workgroup-uniform branch)
+      if (gx == 0) xm = ghost_of(g.bcm[0], g.bcc[0], uc);
+      if (gx == nx - 1) xp = ghost_of(g.bcm[1], g.bcc[1], uc);
+      if (gy == 0) ym = ghost_of(g.bcm[2], g.bcc[2], uc);
+      if (gy == ny - 1) yp = ghost_of(g.bcm[3], g.bcc[3], uc);
+    }
+    if (p == 0) zm = ghost_of(g.bcm[4], g.bcc[4], uc);  // plane-uniform
+    if (p == nz - 1) zp = ghost_of(g.bcm[5], g.bcc[5], uc);
+    const double tx = (xp + xm) - 2.0 * uc;
+    const double ty = (yp + ym) - 2.0 * uc;
+    const double tz = (zp + zm) - 2.0 * uc;
+    const double lap = (tx + ty) + tz;                     // .ChF:111-120
+    double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
+    const double ldpsi = lap * s.dxinv * bv;               // .ChF:122
+    lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
+    const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
+    return uc - lam * (lofdpsi - rv);                      // .ChF:127-128
+  };
+  // one colour pass on plane p over the ring of width w; `red` selects the
+  // updated colour, coef(i, q) returns (rhs, a, b) of the updated element
+  auto pass_red = [&](int p, int w, const double *cr, const double *ca, const double *cb,
+                      bool from_pairs) {
+    double *Rs = R + slot(p) * CP;
+    const double *Bs = B + slot(p) * CP;
+    const double *Bm = B + slot(p - 1) * CP;
+    const double *Bp = B + slot(p + 1) * CP;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int q = (q0 + rgy[i] + p) & 1;
+      const int gx = rgx0[i] + q;
+      if (!rok[i] || !on_ring(gx, rgy[i], w)) continue;
+      const int ci = rci[i];
+      const double xm = q ? Bs[ci] : Bs[ci - 1];
+      const double xp = q ? Bs[ci + 1] : Bs[ci];
+      double rv, av, bv;
+      if (from_pairs) {
+        rv = bsel(q, c0r1[i], c0r0[i]);
+        av = bsel(q, c0a1[i], c0a0[i]);
+        bv = bsel(q, c0b1[i], c0b0[i]);
+      } else {
+        rv = cr[i];
+        av = ca[i];
+        bv = cb[i];
+      }
+      Rs[ci] = upd(Rs[ci], xm, xp, Bs[ci - PW], Bs[ci + PW], Bm[ci], Bp[ci], rv, av, bv, gx,
+                   rgy[i], p);
+    }
+  };
+  auto pass_black = [&](int k, int w, const double *cr, const double *ca, const double *cb) {
+    double *Bs = B + slot(k) * CP;
+    const double *Rs = R + slot(k) * CP;
+    const double *Rm = R + slot(k - 1) * CP;
+    const double *Rp = R + slot(k + 1) * CP;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int qb = 1 - ((q0 + rgy[i] + k) & 1);
+      const int gx = rgx0[i] + qb;
+      if (!rok[i] || !on_ring(gx, rgy[i], w)) continue;
+      const int ci = rci[i];
+      const double xm = qb ? Rs[ci] : Rs[ci - 1];
+      const double xp = qb ? Rs[ci + 1] : Rs[ci];
+      Bs[ci] = upd(Bs[ci], xm, xp, Rs[ci - PW], Rs[ci + PW], Rm[ci], Rp[ci], cr[i], ca[i], cb[i],
+                   gx, rgy[i], k);
+    }
+  };
+
+  fetch_u(z0 - 4);
+  put_u(z0 - 4);
+  fetch_u(z0 - 3);
+  put_u(z0 - 3);
+  fetch_u(z0 - 2);
+  fetch_c(z0 - 3);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    c0r0[i] = nr0[i]; c0r1[i] = nr1[i];
+    c0a0[i] = na0[i]; c0a1[i] = na1[i];
+    c0b0[i] = nb0[i]; c0b1[i] = nb1[i];
+    c1r[i] = c1a[i] = c1b[i] = 0.0;
+  }
+  const int zlo = max(z0 - 3, 0), zhi = min(z1 + 2, nz - 1);  // stage-1 planes
+  for (int p = z0 - 3; p <= z1 + 2; ++p) {
+    put_u(p + 1);
+    fetch_u(p + 2);
+    fetch_c(p + 1);
+    fetch_elem(p - 2, 0, c3r, c3a, c3b);
+    fetch_elem(p - 3, 1, c4r, c4a, c4b);
+    __syncthreads();
+    if (p >= zlo && p <= zhi) pass_red(p, 3, nullptr, nullptr, nullptr, true);  // sweep 1 red
+    __syncthreads();
+    {
+      const int k = p - 1;  // sweep 1 black
+      if (k >= max(z0 - 2, 0) && k <= min(z1 + 1, nz - 1)) pass_black(k, 2, c1r, c1a, c1b);
+    }
+    __syncthreads();
+    {
+      const int k = p - 2;  // sweep 2 red
+      if (k >= max(z0 - 1, 0) && k <= min(z1, nz - 1)) pass_red(k, 1, c3r, c3a, c3b, false);
+    }
+    __syncthreads();
+    const int k = p - 3;  // sweep 2 black on the tile + store
+    if (k >= z0 && k < z1) {
+      double *Bs = B + slot(k) * CP;
+      const double *Rs = R + slot(k) * CP;
+      const double *Rm = R + slot(k - 1) * CP;
+      const double *Rp = R + slot(k + 1) * CP;
+      double *dst = uo + (long)k * sz;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        if (!rtile[i]) continue;
+        const int qb = 1 - ((q0 + rgy[i] + k) & 1);
+        const int gx = rgx0[i] + qb;
+        const int ci = rci[i];
+        const double red = Rs[ci];
+        double blk = Bs[ci];
+        if (gx < nx) {
+          const double xm = qb ? Rs[ci] : Rs[ci - 1];
+          const double xp = qb ? Rs[ci + 1] : Rs[ci];
+          blk = upd(blk, xm, xp, Rs[ci - PW], Rs[ci + PW], Rm[ci], Rp[ci], c4r[i], c4a[i],
+                    c4b[i], gx, rgy[i], k);
+        }
+        if (rgx0[i] + 1 < nx) {
+          double2 w;
+          w.x = bsel(qb, red, blk);
+          w.y = bsel(qb, blk, red);
+          *reinterpret_cast<double2 *>(dst + roff[i]) = w;
+        } else {
+          dst[roff[i]] = bsel(qb, red, blk);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {  // plane p's black coefficients: stage 2, next step
+      const int qb = 1 - ((q0 + rgy[i] + p) & 1);
+      c1r[i] = bsel(qb, c0r1[i], c0r0[i]);
+      c1a[i] = bsel(qb, c0a1[i], c0a0[i]);
+      c1b[i] = bsel(qb, c0b1[i], c0b0[i]);
+      c0r0[i] = nr0[i]; c0r1[i] = nr1[i];
+      c0a0[i] = na0[i]; c0a1[i] = na1[i];
+      c0b0[i] = nb0[i]; c0b1[i] = nb1[i];
+    }
+  }
+}
+
+// The ghost layer of every BC face of one box in one launch.  Along an
+// exchanged face the range extends one cell onto that face's ghost layer:
+// the sweep recomputes the neighbour's red values there, and the neighbour
+// would have seen its own BC image in these cells (ParseBC before each
+// pass).  Run after the shell exchange, which supplies the centre values.
 __global__ void k_fill_bc_faces(double *__restrict__ u, const BoxArgs g) {
   const int face = blockIdx.z;
   if (!g.bcm[face]) return;
   const int dir = face >> 1, side = face & 1;
-  const int n0 = dir == 0 ? g.ny : g.nx;  // fastest in-face direction
-  const int n1 = dir == 2 ? g.ny : g.nz;
-  const int a0 = blockIdx.x * blockDim.x + threadIdx.x;
-  const int a1 = blockIdx.y;
-  if (a0 >= n0 || a1 >= n1) return;
+  const int d0 = dir == 0 ? 1 : 0, d1 = dir == 2 ? 1 : 2;  // in-face directions
+  const int n[3] = {g.nx, g.ny, g.nz};
+  const int lo0 = g.bcm[2 * d0] ? 0 : -1, hi0 = g.bcm[2 * d0 + 1] ? n[d0] - 1 : n[d0];
+  const int lo1 = g.bcm[2 * d1] ? 0 : -1, hi1 = g.bcm[2 * d1 + 1] ? n[d1] - 1 : n[d1];
+  const int a0 = lo0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int a1 = lo1 + (int)blockIdx.y;
+  if (a0 > hi0 || a1 > hi1) return;
   int c[3];
-  c[dir] = side == 0 ? 0 : (dir == 0 ? g.nx : dir == 1 ? g.ny : g.nz) - 1;
-  c[dir == 0 ? 1 : 0] = a0;
-  c[dir == 2 ? 1 : 2] = a1;
+  c[dir] = side == 0 ? 0 : n[dir] - 1;
+  c[d0] = a0;
+  c[d1] = a1;
   const long st = dir == 0 ? 1 : dir == 1 ? g.sy : g.sz;
   const long near = (long)c[0] + (long)c[1] * g.sy + (long)c[2] * g.sz;
   u[near + (side == 0 ? -st : st)] = ghost_of(g.bcm[face], g.bcc[face], u[near]);
@@ -294,19 +593,13 @@ __global__ void k_fill_bc_faces(double *__restrict__ u, const BoxArgs g) {
 
 }  // namespace
 
-bool gsrb_sweep_fused_supported(const BoxArgs &g) {
-  for (int f = 0; f < 6; ++f)
-    if (g.bcm[f] == kBcMemory) return false;  // needs every face BC-filled
-  return g.nx > 0 && g.ny > 0 && g.nz > 0;
-}
-
 template <int TX, int TY, int NT>
 static void launch_fused6(double *u_out, double *u_in, const double *rhs, const double *a,
                           const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                           hipStream_t st) {
   if (!zero_in) {  // BC image of every face into the input's ghost layer
-    const int m = g.nx > g.ny ? g.nx : g.ny;
-    const int m1 = g.ny > g.nz ? g.ny : g.nz;
+    const int m = (g.nx > g.ny ? g.nx : g.ny) + 2;
+    const int m1 = (g.ny > g.nz ? g.ny : g.nz) + 2;
     k_fill_bc_faces<<<dim3((unsigned)((m + 255) / 256), (unsigned)m1, 6), dim3(256), 0, st>>>(u_in,
                                                                                             g);
   }
@@ -323,6 +616,47 @@ static void launch_fused6(double *u_out, double *u_in, const double *rhs, const 
         u_out, u_in, rhs, a, b, g, s, kc, ntx, nty, nblocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw Error(kHipErr, std::string("fused sweep launch: ") + hipGetErrorString(e));
+}
+
+template <int TX, int TY, int NT>
+static void launch_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,
+                           const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                           hipStream_t st) {
+  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
+  int kc = g.nz;
+  while (kc > 32 && (long)ntx * nty * ((g.nz + kc - 1) / kc) < 2048) kc = (kc + 1) / 2;
+  const int ntz = (g.nz + kc - 1) / kc;
+  const int nblocks = ntx * nty * ntz;
+  if (zero_in)
+    k_gsrb_fused2x<TX, TY, NT, true><<<dim3((unsigned)nblocks), dim3(NT), 0, st>>>(
+        u_out, u_in, rhs, a, b, g, s, kc, ntx, nty, nblocks);
+  else
+    k_gsrb_fused2x<TX, TY, NT, false><<<dim3((unsigned)nblocks), dim3(NT), 0, st>>>(
+        u_out, u_in, rhs, a, b, g, s, kc, ntx, nty, nblocks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(kHipErr, std::string("fused sweep launch: ") + hipGetErrorString(e));
+}
+
+static int fused2x_variant() {
+  static int v = [] {
+    const char *e = getenv("MGIC_FUSED2X_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,
+                        const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                        hipStream_t st) {
+  switch (fused2x_variant()) {
+    case 1: launch_fused2x<120, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 2: launch_fused2x<56, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 3: launch_fused2x<56, 6, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 4: launch_fused2x<56, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 5: launch_fused2x<56, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 6: launch_fused2x<120, 4, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    default: launch_fused2x<56, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+  }
 }
 
 // tile shape, for measurement (MGIC_FUSED_VARIANT): 0 = 60x8 / 256 threads

@@ -2,7 +2,8 @@
 """Micro-benchmark of the fine-level smoother: time `relax(nsweeps)` on one
 n^3 box (SetBinaryBH inputs) and print one JSON line with per-sweep time,
 effective GB/s (48 B/cell/pass credited) and a checksum of the result.
-The fused-kernel variant is selected with MGIC_FUSED_VARIANT."""
+Kernel selection: MGIC_SWEEPS_PER_LAUNCH (1 or 2), MGIC_FUSED_VARIANT /
+MGIC_FUSED2X_VARIANT (tile shapes)."""
 import argparse
 import hashlib
 import json
@@ -45,15 +46,16 @@ def main():
         op.relax(fu, fr, args.sweeps)
     comm.synchronize()
     wall = time.perf_counter() - t0
-    launches, ms = mg.prof_smoother_read()
+    launches, passes, ms = mg.prof_smoother_read()
     mg.prof_smoother(False)
     sweeps = args.reps * args.sweeps
     per_sweep = wall / sweeps * 1e3
     h = hashlib.sha1(fu.download(0).tobytes()).hexdigest()[:16]
-    print(json.dumps({"variant": "passes" if args.no_fused else (args.tag or os.environ.get("MGIC_FUSED_VARIANT", "1")),
+    print(json.dumps({"variant": "passes" if args.no_fused else (args.tag or "default"),
                       "n": n, "ms_per_sweep_wall": round(per_sweep, 4),
                       "ms_per_launch_events": round(ms / max(launches, 1), 4),
-                      "launches": launches,
+                      "launches": launches, "passes": passes,
+                      "ms_per_sweep_events": round(ms / max(passes, 1) * 2, 4),
                       "eff_GBps": round(96.0 * n ** 3 / (per_sweep * 1e-3) / 1e9, 1),
                       "checksum": h}), flush=True)
 

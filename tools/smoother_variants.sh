@@ -1,11 +1,13 @@
 #!/bin/bash
-# Time fused-sweep variants: VARIANTS="v[:zs] ..." (zs -> MGIC_FUSED_ZS)
+# Time smoother configurations: each entry of $VARIANTS is a comma-separated
+# list of VAR=value settings, e.g.
+#   VARIANTS="MGIC_SWEEPS_PER_LAUNCH=1 MGIC_SWEEPS_PER_LAUNCH=2,MGIC_FUSED2X_VARIANT=1"
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 N=${N:-512}
-timeout -k 10 300 python tools/bench_smoother.py --n $N --no-fused || exit $?
-for vz in ${VARIANTS:-0 1 2 3 4}; do
-  v=${vz%%:*}; zs=0; [[ $vz == *:* ]] && zs=${vz##*:}
-  MGIC_FUSED_VARIANT=$v MGIC_FUSED_ZS=$zs timeout -k 10 300 python tools/bench_smoother.py --n $N --tag "$vz" || exit $?
+SWEEPS=${SWEEPS:-8}
+timeout -k 10 300 python tools/bench_smoother.py --n $N --sweeps $SWEEPS --no-fused || exit $?
+for v in ${VARIANTS:-MGIC_SWEEPS_PER_LAUNCH=1 MGIC_SWEEPS_PER_LAUNCH=2}; do
+  env ${v//,/ } timeout -k 10 300 python tools/bench_smoother.py --n $N --sweeps $SWEEPS --tag "$v" || exit $?
 done
