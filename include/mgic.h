@@ -206,6 +206,22 @@ MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_
 MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
                                    mgic_field resid, int norm_type, int homogeneous,
                                    double *norm);
+/* MultilevelLinearOp::preCond: e = 0, then `iters` AMRMultiGrid iterations
+ * on (e, r), homogeneous BC (Main_PoissonSolver.cpp:107-117) */
+MGIC_API int mgic_mg_precondition(mgic_mg mg, mgic_field e, mgic_field r, int iters);
+
+/* ---- the linear solve solver.solve(dpsi, rhs) (Main_PoissonSolver.cpp:
+ *      103-126, 169-184): BiCGStab over the level operator, preconditioned
+ *      by mgic_mg_precondition */
+typedef struct {
+  int num_mg_iterations; /* numMGIterations (default 1) */
+  int max_iterations;    /* max_iterations -> BiCGStab m_imax (default 10) */
+  double tolerance;      /* tolerance -> m_eps (default 1e-7) */
+  int norm_type;         /* m_normType (0 = max norm) */
+} mgic_solve_params;
+MGIC_API void mgic_solve_params_default(mgic_solve_params *p);
+MGIC_API int mgic_mg_solve(mgic_mg mg, mgic_field phi, mgic_field rhs, const mgic_solve_params *p,
+                           int *iterations, double *final_norm);
 
 /* ---- instrumentation: hipEvents around every smoother launch on boxes of
  * at least min_cells cells; passes = colour passes those launches performed

@@ -7,10 +7,12 @@ reference's operator / factory / solver interface (see core.py).
 """
 from .core import (  # noqa: F401
     AMRMultiGrid,
+    BiCGStabSolver,
     Comm,
     Grid,
     LevelData,
     MgicError,
+    MultilevelLinearOp,
     OperatorParams,
     SolverParams,
     VariableCoeffPoissonOperator,

@@ -39,6 +39,17 @@ class OpParams(ctypes.Structure):
     ]
 
 
+class SolveParams(ctypes.Structure):
+    """mgic_solve_params (include/mgic.h)."""
+
+    _fields_ = [
+        ("num_mg_iterations", c_int),
+        ("max_iterations", c_int),
+        ("tolerance", c_double),
+        ("norm_type", c_int),
+    ]
+
+
 class MGParams(ctypes.Structure):
     """mgic_mg_params (include/mgic.h)."""
 
@@ -141,6 +152,9 @@ SIGNATURES = {
     "mgic_mg_one_cycle": [H, H, H],
     "mgic_mg_iteration": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
+    "mgic_mg_precondition": [H, H, H, c_int],
+    "mgic_solve_params_default": [POINTER(SolveParams)],
+    "mgic_mg_solve": [H, H, H, POINTER(SolveParams), PI, PD],
     "mgic_prof_smoother": [c_int, c_long],
     "mgic_prof_smoother_read": [PI, POINTER(c_long), PD],
     # ChomboFortran drop-ins (include/mgic_chf.h); argtypes left open
@@ -155,6 +169,7 @@ _RESTYPE = {
     "mgic_last_error": c_char_p,
     "mgic_op_params_default": None,
     "mgic_mg_params_default": None,
+    "mgic_solve_params_default": None,
     "gsrbhelmholtzvc3d_": None,
     "vccomputeop3d_": None,
     "vccomputeres3d_": None,

@@ -28,6 +28,7 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from . import _lib
 from ._lib import MGParams, MgicError, OpParams, call, lib
 
 __all__ = [
@@ -39,6 +40,8 @@ __all__ = [
     "VariableCoeffPoissonOperatorFactory",
     "VariableCoeffPoissonOperator",
     "AMRMultiGrid",
+    "MultilevelLinearOp",
+    "BiCGStabSolver",
     "defineOperatorFactory",
     "bicgstab",
     "set_binary_bh_coefs",
@@ -541,6 +544,49 @@ class AMRMultiGrid:
         if h:
             lib.mgic_mg_destroy(h)
             self._h = None
+
+
+class MultilevelLinearOp:
+    """MultilevelLinearOp<FArrayBox> on one AMR level (Main_PoissonSolver.cpp:103-117,169-170):
+    the level operator plus the MG preconditioner of `num_mg_iterations` AMRMultiGrid
+    iterations (pre = post = bottom = the SolverParams smoothing counts)."""
+
+    def __init__(self, amg: "AMRMultiGrid", num_mg_iterations: int = 1):
+        self.amg = amg
+        self.num_mg_iterations = int(num_mg_iterations)
+
+    def preCond(self, e: LevelData, r: LevelData) -> None:
+        call("mgic_mg_precondition", self.amg.handle, e.handle, r.handle,
+             self.num_mg_iterations)
+
+
+class BiCGStabSolver:
+    """BiCGStabSolver<Vector<LevelData*>> over a MultilevelLinearOp
+    (Main_PoissonSolver.cpp:104,172-184): m_normType, m_eps = tolerance,
+    m_imax = max_iterations, inhomogeneous BC."""
+
+    def __init__(self, mlop: MultilevelLinearOp, tolerance: float = 1.0e-7,
+                 max_iterations: int = 10, norm_type: int = 0):
+        self.mlop = mlop
+        self.m_eps = tolerance
+        self.m_imax = max_iterations
+        self.m_normType = norm_type
+        self.iterations = 0
+        self.final_norm = None
+
+    def solve(self, phi: LevelData, rhs: LevelData) -> int:
+        p = _lib.SolveParams()
+        lib.mgic_solve_params_default(ctypes.byref(p))
+        p.num_mg_iterations = self.mlop.num_mg_iterations
+        p.max_iterations = int(self.m_imax)
+        p.tolerance = float(self.m_eps)
+        p.norm_type = int(self.m_normType)
+        it = ctypes.c_int()
+        nrm = ctypes.c_double()
+        call("mgic_mg_solve", self.mlop.amg.handle, phi.handle, rhs.handle, ctypes.byref(p),
+             ctypes.byref(it), ctypes.byref(nrm))
+        self.iterations, self.final_norm = it.value, nrm.value
+        return it.value
 
 
 BH_KEYS = ("domain_length", "G_Newton", "phi_amplitude", "phi_wavelength", "bh1_bare_mass",

@@ -746,6 +746,43 @@ MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs, m
   });
 }
 
+MGIC_API int mgic_mg_precondition(mgic_mg mg, mgic_field e, mgic_field r, int iters) {
+  return guard([&] {
+    NEED(mg);
+    NEED(e);
+    NEED(r);
+    MGIC_CHECK(iters >= 0, "iters must be >= 0");
+    mg->amg.precondition(*e->f, *r->f, iters);
+  });
+}
+MGIC_API void mgic_solve_params_default(mgic_solve_params *p) {
+  if (!p) return;
+  SolveParams d;
+  p->num_mg_iterations = d.num_mg_iterations;
+  p->max_iterations = d.max_iterations;
+  p->tolerance = d.tolerance;
+  p->norm_type = d.norm_type;
+}
+MGIC_API int mgic_mg_solve(mgic_mg mg, mgic_field phi, mgic_field rhs, const mgic_solve_params *p,
+                           int *iterations, double *final_norm) {
+  return guard([&] {
+    NEED(mg);
+    NEED(phi);
+    NEED(rhs);
+    SolveParams sp;
+    if (p) {
+      sp.num_mg_iterations = p->num_mg_iterations;
+      sp.max_iterations = p->max_iterations;
+      sp.tolerance = p->tolerance;
+      sp.norm_type = p->norm_type;
+    }
+    MGIC_CHECK(sp.max_iterations >= 0 && sp.tolerance >= 0.0, "bad solve parameters");
+    double nrm = 0.0;
+    const int it = mg->amg.solve(*phi->f, *rhs->f, sp, &nrm);
+    if (iterations) *iterations = it;
+    if (final_norm) *final_norm = nrm;
+  });
+}
 MGIC_API int mgic_prof_smoother(int enable, long min_cells) {
   return guard([&] { prof_enable(enable != 0, min_cells); });
 }

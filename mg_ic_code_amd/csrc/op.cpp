@@ -505,7 +505,8 @@ int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, cons
       op.incr(P, V, -beta * omega);
       op.incr(P, R, 1.0);
     }
-    op.preCond(PT, P);
+    if (precond) precond(PT, P);
+    else op.preCond(PT, P);
     op.setToZero(V);
     op.applyOp(V, PT, true);
     const double m = op.dotProduct(RT, V);
@@ -516,7 +517,8 @@ int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, cons
       op.incr(E, PT, alpha);
       nrm = op.norm(S, nt);
       if (nrm <= prm.eps * init_norm || nrm <= prm.reps) break;
-      op.preCond(ST, S);
+      if (precond) precond(ST, S);
+      else op.preCond(ST, S);
       op.setToZero(T);
       op.applyOp(T, ST, true);
       const double ts = op.dotProduct(T, S);
@@ -684,6 +686,31 @@ double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &
   op0.incr(phi, *corr_, 1.0);
   op0.residual(resid, phi, rhs, homogeneous);
   return normType >= 0 ? op0.norm(resid, normType) : -1.0;
+}
+
+void AMRMultiGrid::precondition(LevelData &e, const LevelData &r, int iters) {
+  VariableCoeffPoissonOperator &op0 = mg.op(0);
+  if (!pre_resid_) pre_resid_ = op0.create();
+  op0.setToZero(e);
+  initResidual(e, r, *pre_resid_, -1, true);
+  for (int i = 0; i < iters; ++i) iteration(e, r, *pre_resid_, -1, true);
+}
+
+int AMRMultiGrid::solve(LevelData &phi, const LevelData &rhs, const SolveParams &p,
+                        double *final_norm) {
+  VariableCoeffPoissonOperator &op0 = mg.op(0);
+  outer_.prm = mg.prm.bicg;  // reps, small, restarts: BiCGStabSolver defaults
+  outer_.prm.imax = p.max_iterations;
+  outer_.prm.eps = p.tolerance;
+  outer_.prm.normType = p.norm_type;
+  const int iters = std::max(1, p.num_mg_iterations);
+  outer_.precond = [this, iters](LevelData &e, const LevelData &r) { precondition(e, r, iters); };
+  const int it = outer_.solve(op0, phi, rhs, false);
+  if (!pre_resid_) pre_resid_ = op0.create();
+  op0.residual(*pre_resid_, phi, rhs, false);
+  const double nrm = op0.norm(*pre_resid_, p.norm_type);
+  if (final_norm) *final_norm = nrm;
+  return it;
 }
 
 double AMRMultiGrid::initResidual(LevelData &phi, const LevelData &rhs, LevelData &resid,

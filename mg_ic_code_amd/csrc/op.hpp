@@ -10,6 +10,8 @@
 // Krylov bottom solver branches on).
 #pragma once
 
+#include <functional>
+
 #include "level.hpp"
 
 namespace mgic {
@@ -151,6 +153,8 @@ class BiCGStabSolver {
  public:
   BiCGStabParams prm;
   int last_iters = 0;
+  // preconditioner; empty = op.preCond (the bottom-solver use)
+  std::function<void(LevelData &, const LevelData &)> precond;
   int solve(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
             bool homogeneous);
 
@@ -203,9 +207,23 @@ class MultiGrid {
 
 // [Chombo] AMRMultiGrid on a single AMR level: iterations of
 //   e = 0; oneCycle(e, r); phi += e; r = rhs - L(phi)
+struct SolveParams {  // Main_PoissonSolver.cpp:106-126 defaults (params.txt overrides)
+  int num_mg_iterations = 1;  // numMGIterations (:107-109)
+  int max_iterations = 10;    // max_iterations (:122-123) -> m_imax (:178)
+  double tolerance = 1.0e-7;  // tolerance (:119-120) -> m_eps (:177)
+  int norm_type = 0;          // m_normType (:176)
+};
+
 class AMRMultiGrid {
  public:
   void define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &prm);
+  // MultilevelLinearOp::preCond on this AMR level: e = 0, then `iters`
+  // iterations on (e, r) with homogeneous BC
+  void precondition(LevelData &e, const LevelData &r, int iters);
+  // solver.solve(dpsi, rhs) (Main_PoissonSolver.cpp:174-184): BiCGStab
+  // over the level operator, preconditioned by precondition(); returns
+  // iterations, *final_norm = norm(rhs - L(phi), norm_type)
+  int solve(LevelData &phi, const LevelData &rhs, const SolveParams &p, double *final_norm);
   // one iteration; returns norm(r, normType) if normType >= 0 (host sync),
   // else -1 without synchronising
   double iteration(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
@@ -215,7 +233,8 @@ class AMRMultiGrid {
   MultiGrid mg;
 
  private:
-  std::unique_ptr<LevelData> corr_;
+  std::unique_ptr<LevelData> corr_, pre_resid_;
+  BiCGStabSolver outer_;
 };
 
 }  // namespace mgic

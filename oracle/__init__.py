@@ -90,6 +90,8 @@ _sig = {
     "orc_mg_iteration": [ctypes.c_void_p, c_int],
     "orc_mg_init_residual": [ctypes.c_void_p, c_int],
     "orc_mg_bicgstab": [ctypes.c_void_p, c_int, c_int, c_int, c_int],
+    "orc_mg_amr_precond": [ctypes.c_void_p, c_int, c_int, c_int],
+    "orc_mg_solve": [ctypes.c_void_p, c_int, c_int, c_double, c_int, POINTER(c_double)],
     "orc_mg_norm": [ctypes.c_void_p, c_int, c_int, c_int],
     "orc_mg_dot": [ctypes.c_void_p, c_int, c_int, c_int],
     "orc_mg_last_bicg_iters": [ctypes.c_void_p],
@@ -105,6 +107,7 @@ for _n, _a in _sig.items():
     _f.restype = _res.get(_n, c_int if _n in ("orc_mg_nlevels", "orc_mg_bicgstab",
                                                "orc_mg_last_bicg_iters", "orc_get_threads")
                           else None)
+_lib.orc_mg_solve.restype = c_int
 
 # field ids (mgic_oracle.h)
 PHI, RHS, ACOEF, BCOEF, LAMBDA, RESID, CORR, TMP = range(8)
@@ -284,6 +287,16 @@ class OracleMG:
 
     def bicgstab(self, level, fe, fr, homogeneous=1) -> int:
         return _lib.orc_mg_bicgstab(self._h, level, fe, fr, int(homogeneous))
+
+    def amr_precond(self, fe, fr, iters):
+        _lib.orc_mg_amr_precond(self._h, fe, fr, int(iters))
+
+    def solve(self, mg_iters=1, imax=10, eps=1e-7, norm_type=0):
+        """Outer MG-preconditioned BiCGStab on level-0 PHI/RHS: (iterations, final norm)."""
+        out = c_double()
+        it = _lib.orc_mg_solve(self._h, int(mg_iters), int(imax), float(eps), int(norm_type),
+                               ctypes.byref(out))
+        return it, out.value
 
     def norm(self, level, field, norm_type=2) -> float:
         return _lib.orc_mg_norm(self._h, level, field, int(norm_type))

@@ -661,12 +661,44 @@ void orc_mg_precond(orc_mg *mg, int l, int fe, int fr) {
   orc_mg_relax(mg, l, fe, fr, 2);       /* :103 */
 }
 
+void orc_mg_one_cycle(orc_mg *mg, int l);
+
+typedef struct {
+  int imax;
+  double eps, reps, small;
+  int restarts, norm_type;
+  int mg_iters; /* 0: op->preCond (bottom solver); > 0: MultilevelLinearOp::preCond */
+} bicg_cfg;
+
+static void bicg_precond(orc_mg *mg, int l, int fe, int fr, const bicg_cfg *c) {
+  if (c->mg_iters > 0)
+    orc_mg_amr_precond(mg, fe, fr, c->mg_iters);
+  else
+    orc_mg_precond(mg, l, fe, fr);
+}
+
+/* MultilevelLinearOp::preCond on one AMR level (Main_PoissonSolver.cpp:
+ * 107-117 sets m_num_mg_iterations / m_num_mg_smooth), restated
+ * (unpinned): e = 0, then `iters` AMRMultiGrid iterations on (e, r) with
+ * homogeneous BC: CORR = 0; oneCycle(CORR, RESID); e += CORR;
+ * RESID = r - L(e).  Level-0 CORR / RESID are the MG's own fields. */
+void orc_mg_amr_precond(orc_mg *mg, int fe, int fr, int iters) {
+  lv_zero_all(mg, 0, fe);
+  orc_mg_residual(mg, 0, ORC_RESID, fe, fr, 1);
+  for (int i = 0; i < iters; ++i) {
+    lv_zero_all(mg, 0, ORC_CORR);
+    orc_mg_one_cycle(mg, 0);
+    lv_op(mg, 0, fe, ORC_CORR, 1.0, 1);
+    orc_mg_residual(mg, 0, ORC_RESID, fe, fr, 1);
+  }
+}
+
 /* [Chombo] BiCGStabSolver<T>::solve, restated (unpinned): van der Vorst
- * BiCGStab with op->preCond as the preconditioner, m_eps relative
- * tolerance on norm(r, m_normType), |m| <= m_small*|rho| restarts. */
-int orc_mg_bicgstab(orc_mg *mg, int l, int fe, int fr, int hom) {
-  const orc_mg_params *p = &mg->prm;
-  const int nt = p->bicg_norm_type;
+ * BiCGStab with a right preconditioner, m_eps relative tolerance on
+ * norm(r, m_normType), |m| <= m_small*|rho| restarts. */
+static int bicgstab_core(orc_mg *mg, int l, int fe, int fr, int hom, const bicg_cfg *c) {
+  const bicg_cfg *p = c;
+  const int nt = c->norm_type;
   orc_mg_residual(mg, l, W_R, fe, fr, hom);
   lv_op(mg, l, W_RT, W_R, 0.0, 0);
   lv_zero_all(mg, l, W_E);
@@ -678,7 +710,7 @@ int orc_mg_bicgstab(orc_mg *mg, int l, int fe, int fr, int hom) {
   const double init_norm = orc_mg_norm(mg, l, W_R, nt);
   double nrm = init_norm;
   int it = 0, init = 1, restarts = 0;
-  while (it < p->bicg_imax && nrm > p->bicg_eps * init_norm && nrm > p->bicg_reps) {
+  while (it < p->imax && nrm > p->eps * init_norm && nrm > p->reps) {
     ++it;
     rho2 = rho1;
     rho1 = orc_mg_dot(mg, l, W_RT, W_R);
@@ -692,18 +724,18 @@ int orc_mg_bicgstab(orc_mg *mg, int l, int fe, int fr, int hom) {
       lv_op(mg, l, W_P, W_V, -beta * omega, 1);
       lv_op(mg, l, W_P, W_R, 1.0, 1);
     }
-    orc_mg_precond(mg, l, W_PT, W_P);
+    bicg_precond(mg, l, W_PT, W_P, c);
     lv_zero_all(mg, l, W_V);
     orc_mg_apply_op(mg, l, W_V, W_PT, 1);
     const double m = orc_mg_dot(mg, l, W_RT, W_V);
-    if (fabs(m) > p->bicg_small * fabs(rho1)) {
+    if (fabs(m) > p->small * fabs(rho1)) {
       alpha = rho1 / m;
       lv_op(mg, l, W_S, W_R, 0.0, 0);
       lv_op(mg, l, W_S, W_V, -alpha, 1);
       lv_op(mg, l, W_E, W_PT, alpha, 1);
       nrm = orc_mg_norm(mg, l, W_S, nt);
-      if (nrm <= p->bicg_eps * init_norm || nrm <= p->bicg_reps) break;
-      orc_mg_precond(mg, l, W_ST, W_S);
+      if (nrm <= p->eps * init_norm || nrm <= p->reps) break;
+      bicg_precond(mg, l, W_ST, W_S, c);
       lv_zero_all(mg, l, W_T);
       orc_mg_apply_op(mg, l, W_T, W_ST, 1);
       const double ts = orc_mg_dot(mg, l, W_T, W_S);
@@ -716,7 +748,7 @@ int orc_mg_bicgstab(orc_mg *mg, int l, int fe, int fr, int hom) {
       nrm = orc_mg_norm(mg, l, W_R, nt);
       if (omega == 0.0) break;
     } else {
-      if (restarts >= p->bicg_restarts) break;
+      if (restarts >= p->restarts) break;
       ++restarts;
       lv_op(mg, l, fe, W_E, 1.0, 1);
       orc_mg_residual(mg, l, W_R, fe, fr, hom);
@@ -728,6 +760,29 @@ int orc_mg_bicgstab(orc_mg *mg, int l, int fe, int fr, int hom) {
   }
   lv_op(mg, l, fe, W_E, 1.0, 1);
   mg->last_iters = it;
+  return it;
+}
+
+int orc_mg_bicgstab(orc_mg *mg, int l, int fe, int fr, int hom) {
+  const orc_mg_params *p = &mg->prm;
+  const bicg_cfg c = {p->bicg_imax, p->bicg_eps, p->bicg_reps, p->bicg_small, p->bicg_restarts,
+                      p->bicg_norm_type, 0};
+  return bicgstab_core(mg, l, fe, fr, hom, &c);
+}
+
+/* solver.solve(dpsi, rhs) of Main_PoissonSolver.cpp:174-184 on one AMR
+ * level: BiCGStab (m_normType = 0, m_eps = tolerance, m_imax =
+ * max_iterations, inhomogeneous BC) on PHI / RHS, preconditioned by
+ * MultilevelLinearOp::preCond.  Returns the iteration count; *final_norm =
+ * norm(RHS - L(PHI), norm_type) afterwards (RESID holds it). */
+int orc_mg_solve(orc_mg *mg, int mg_iters, int imax, double eps, int norm_type,
+                 double *final_norm) {
+  const orc_mg_params *p = &mg->prm;
+  const bicg_cfg c = {imax, eps, p->bicg_reps, p->bicg_small, p->bicg_restarts, norm_type,
+                      mg_iters > 0 ? mg_iters : 1};
+  const int it = bicgstab_core(mg, 0, ORC_PHI, ORC_RHS, 0, &c);
+  orc_mg_residual(mg, 0, ORC_RESID, ORC_PHI, ORC_RHS, 0);
+  if (final_norm) *final_norm = orc_mg_norm(mg, 0, ORC_RESID, norm_type);
   return it;
 }
 

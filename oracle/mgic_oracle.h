@@ -143,6 +143,13 @@ double orc_mg_iteration(orc_mg *mg, int norm_type);
 double orc_mg_init_residual(orc_mg *mg, int norm_type);
 /* BiCGStab (homogeneous) on a level: solves L e = r for fields fe, fr */
 int orc_mg_bicgstab(orc_mg *mg, int level, int fe, int fr, int homogeneous);
+/* MultilevelLinearOp::preCond on level 0: fe = 0, then `iters`
+ * AMRMultiGrid iterations on (fe, fr), homogeneous BC */
+void orc_mg_amr_precond(orc_mg *mg, int fe, int fr, int iters);
+/* the outer solve (Main_PoissonSolver.cpp:174-184): MG-preconditioned
+ * BiCGStab on level-0 PHI / RHS; returns iterations, final residual norm */
+int orc_mg_solve(orc_mg *mg, int mg_iters, int imax, double eps, int norm_type,
+                 double *final_norm);
 double orc_mg_norm(orc_mg *mg, int level, int field, int norm_type);
 double orc_mg_dot(orc_mg *mg, int level, int fx, int fy);
 int orc_mg_last_bicg_iters(const orc_mg *mg);

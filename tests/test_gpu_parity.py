@@ -372,3 +372,35 @@ def test_fused_sweep_matches_oracle_and_passes(comm, rng, shape, lo, nsweeps):
     o.setup()
     o.relax(0, oracle.PHI, oracle.RHS, nsweeps)
     assert np.array_equal(outs[0], o.get(0, oracle.PHI, 0))
+
+
+# ------------------------------------------------- outer solve
+@pytest.mark.parametrize("parts", [(1, 1, 1), (2, 1, 2)])
+def test_mg_preconditioner_bitwise(comm, rng, parts):
+    # MultilevelLinearOp::preCond: e = 0 + numMGIterations AMRMultiGrid
+    # iterations (homogeneous BC) -- no reductions, so bit for bit
+    n = 32
+    S = build_pair(comm, rng, n, parts, nlevels=3, bottom=0, bvar=False)
+    e = mg.LevelData(S["grid"])
+    mg.MultilevelLinearOp(S["amg"], 2).preCond(e, S["frhs"])
+    o = S["o"]
+    o.amr_precond(oracle.TMP, oracle.RHS, 2)
+    assert np.array_equal(download_global(e, S["grid"], (n,) * 3), o.get(0, oracle.TMP, 0))
+
+
+@pytest.mark.parametrize("parts", [(1, 1, 1), (2, 2, 2)])
+def test_outer_bicgstab_solve_matches_oracle(comm, rng, parts):
+    # solver.solve(dpsi, rhs) of Main_PoissonSolver.cpp:174-184 with the
+    # params.txt settings; dot products reduce in a different order, so the
+    # bar is rel-L2 <= 1e-10 on phi and the same iteration count
+    n = 32
+    S = build_pair(comm, rng, n, parts, nlevels=3, bottom=0, bvar=False)
+    solver = mg.BiCGStabSolver(mg.MultilevelLinearOp(S["amg"], 2), tolerance=1e-10,
+                               max_iterations=100, norm_type=0)
+    it = solver.solve(S["fphi"], S["frhs"])
+    it_o, fin_o = S["o"].solve(mg_iters=2, imax=100, eps=1e-10, norm_type=0)
+    assert it == it_o
+    g = download_global(S["fphi"], S["grid"], (n,) * 3)
+    c = S["o"].get(0, oracle.PHI, 0)
+    assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
+    assert solver.final_norm <= 1e-9 * np.max(np.abs(S["rhs"]))  # true residual, max norm
