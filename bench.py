@@ -136,9 +136,10 @@ def main():
     passes_per_launch = passes / launches if launches else 0.0
     fused = passes_per_launch >= 2
     bytes_per_launch = 48.0 * fine_cells * passes_per_launch  # 48 B/cell/pass
-    # compulsory traffic of one launch: u, rhs, a, b read once + u written
-    # once (40 B/cell), however many colour passes the launch performs
-    compulsory = 40.0 * fine_cells
+    # compulsory traffic of one launch: u, rhs, a read once (+ b unless it is
+    # one value everywhere -- bCoef = 1 here, which the operator detects and
+    # does not load) + u written once, however many colour passes it performs
+    compulsory = 32.0 * fine_cells
     avg_launch_ms = smooth_ms / launches if launches else float("nan")
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if launches else None
     traffic = None
@@ -195,8 +196,10 @@ def main():
                 "compulsory_bytes_per_launch": compulsory,
                 "compulsory_GBps": round(compulsory / (avg_launch_ms * 1e-3) / 1e9, 1) if launches else None,
                 "note": "achieved/frac use SURVEY 8(d)'s 48 B/cell/colour-pass credit (an effective "
-                        "bandwidth: the fused launch does two passes reading each array once, so frac "
-                        "can exceed 1); traffic = PMC HBM bytes per launch (profiles/traffic_smoother.json)",
+                        "bandwidth: the fused launch does two passes reading each array once and "
+                        "bCoef = 1 is not loaded, so frac can exceed 1); compulsory = 32 B/cell "
+                        "(u, rhs, aCoef in, u out); traffic = PMC HBM bytes per launch "
+                        "(profiles/traffic_smoother.json)",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": round(avg_launch_ms, 5),
                 "launches_timed": launches,

@@ -43,7 +43,7 @@ __device__ __forceinline__ double lap7(const double *__restrict__ u, long idx, d
   return (tx + ty) + tz;
 }
 
-template <bool LAM_MEM>
+template <bool LAM_MEM, bool BC>
 __global__ __launch_bounds__(256) void k_gsrb(double *__restrict__ u,
                                               const double *__restrict__ rhs,
                                               const double *__restrict__ a,
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_gsrb(double *__restrict__ u,
   const double av = a[idx];
   double lofdpsi = s.alpha * av * uc;           // .ChF:107-108
   double ldpsi = lap7(u, idx, uc, i, j, k, g);  // .ChF:111-120
-  ldpsi = ldpsi * s.dxinv * b[idx];             // .ChF:122
+  ldpsi = ldpsi * s.dxinv * (BC ? s.bval : b[idx]);  // .ChF:122
   lofdpsi = lofdpsi - s.beta * ldpsi;           // .ChF:124
   double l;
   if (LAM_MEM) l = lam[idx];
@@ -70,6 +70,7 @@ __global__ __launch_bounds__(256) void k_gsrb(double *__restrict__ u,
   u[idx] = uc - l * (lofdpsi - rhs[idx]);       // .ChF:127-128
 }
 
+template <bool BC>
 __global__ __launch_bounds__(256) void k_apply_op(double *__restrict__ lu,
                                                   const double *__restrict__ u,
                                                   const double *__restrict__ a,
@@ -83,10 +84,11 @@ __global__ __launch_bounds__(256) void k_apply_op(double *__restrict__ lu,
   const double uc = u[idx];
   const double lof = s.alpha * a[idx] * uc;                     // .ChF:211-212
   double ldpsi = lap7(u, idx, uc, i, j, k, g);                   // .ChF:216-225
-  ldpsi = ldpsi * s.dxinv * s.beta * b[idx];                     // .ChF:227
+  ldpsi = ldpsi * s.dxinv * s.beta * (BC ? s.bval : b[idx]);     // .ChF:227
   lu[idx] = lof - ldpsi;                                         // .ChF:229
 }
 
+template <bool BC>
 __global__ __launch_bounds__(256) void k_residual(double *__restrict__ r,
                                                   const double *__restrict__ u,
                                                   const double *__restrict__ rhs,
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void k_residual(double *__restrict__ r,
   const double uc = u[idx];
   const double res = rhs[idx] - s.alpha * a[idx] * uc;           // .ChF:314-316
   double ldpsi = lap7(u, idx, uc, i, j, k, g);                   // .ChF:320-329
-  ldpsi = ldpsi * s.dxinv * s.beta * b[idx];                     // .ChF:331
+  ldpsi = ldpsi * s.dxinv * s.beta * (BC ? s.bval : b[idx]);     // .ChF:331
   r[idx] = res + ldpsi;                                          // .ChF:333
 }
 
@@ -116,6 +118,7 @@ __device__ __forceinline__ double2 ld2(const double *__restrict__ p) {
   return *reinterpret_cast<const double2 *>(p);
 }
 
+template <bool BC>
 __global__ __launch_bounds__(256) void k_restrict(double *__restrict__ rc, const BoxArgs cg,
                                                   const double *__restrict__ u,
                                                   const double *__restrict__ rhs,
@@ -140,7 +143,8 @@ __global__ __launch_bounds__(256) void k_restrict(double *__restrict__ rc, const
       const double2 ym = ld2(u + row - fg.sy), yp = ld2(u + row + fg.sy);
       const double2 zm = ld2(u + row - fg.sz), zp = ld2(u + row + fg.sz);
       const double xl = u[row - 1], xr = u[row + 2];
-      const double2 rv = ld2(rhs + row), av = ld2(a + row), bv = ld2(b + row);
+      const double2 rv = ld2(rhs + row), av = ld2(a + row);
+      const double2 bv = BC ? make_double2(s.bval, s.bval) : ld2(b + row);
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
         const int i = i0 + ii;
@@ -310,8 +314,14 @@ constexpr int RB = 256;
 
 template <int KIND>
 __device__ __forceinline__ double red_op(double a, double b) {
-  if constexpr (KIND == 3) return a > b ? a : b;
+  if constexpr (KIND >= 3) return a > b ? a : b;
   else return a + b;
+}
+// identity of the reduction: 0 for sums and max|x|, -inf for max x / max -x
+template <int KIND>
+__device__ __forceinline__ double red_init() {
+  if constexpr (KIND >= 4) return -__builtin_huge_val();
+  else return 0.0;
 }
 
 template <int KIND>
@@ -322,7 +332,7 @@ __global__ __launch_bounds__(RB) void k_reduce_partial(const double *__restrict_
   __shared__ double sm[RB];
   const long ncell = (long)g.nx * g.ny * g.nz;
   const long plane = (long)g.nx * g.ny;
-  double acc = 0.0;
+  double acc = red_init<KIND>();
   for (long t = (long)blockIdx.x * RB + threadIdx.x; t < ncell; t += (long)gridDim.x * RB) {
     const int k = (int)(t / plane);
     const int rem = (int)(t - (long)k * plane);
@@ -333,6 +343,8 @@ __global__ __launch_bounds__(RB) void k_reduce_partial(const double *__restrict_
     double term;
     if constexpr (KIND == 0) term = v * y[idx];
     else if constexpr (KIND == 2) term = v * v;
+    else if constexpr (KIND == 4) term = v;
+    else if constexpr (KIND == 5) term = -v;
     else term = fabs(v);
     acc = red_op<KIND>(acc, term);
   }
@@ -349,7 +361,7 @@ template <int KIND>
 __global__ __launch_bounds__(RB) void k_reduce_final(const double *__restrict__ p, int n,
                                                      double *__restrict__ out) {
   __shared__ double sm[RB];
-  double acc = 0.0;
+  double acc = red_init<KIND>();
   for (int t = threadIdx.x; t < n; t += RB) acc = red_op<KIND>(acc, p[t]);
   sm[threadIdx.x] = acc;
   __syncthreads();
@@ -476,22 +488,31 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b, c
   const int npairs = (g.nx + 1) / 2;
   const dim3 grid((unsigned)((npairs + TX - 1) / TX), (unsigned)((g.ny + TY - 1) / TY),
                   (unsigned)g.nz);
-  if (lam) k_gsrb<true><<<grid, kBlock, 0, st>>>(u, rhs, a, b, lam, g, s, colour);
-  else k_gsrb<false><<<grid, kBlock, 0, st>>>(u, rhs, a, b, nullptr, g, s, colour);
+  if (lam) {
+    if (s.bconst) k_gsrb<true, true><<<grid, kBlock, 0, st>>>(u, rhs, a, b, lam, g, s, colour);
+    else k_gsrb<true, false><<<grid, kBlock, 0, st>>>(u, rhs, a, b, lam, g, s, colour);
+  } else {
+    if (s.bconst) k_gsrb<false, true><<<grid, kBlock, 0, st>>>(u, rhs, a, b, nullptr, g, s, colour);
+    else k_gsrb<false, false><<<grid, kBlock, 0, st>>>(u, rhs, a, b, nullptr, g, s, colour);
+  }
   check_launch();
 }
 
 void apply_op(double *lu, const double *u, const double *a, const double *b, const BoxArgs &g,
               const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  k_apply_op<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(lu, u, a, b, g, s);
+  if (s.bconst) k_apply_op<true><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(lu, u, a, b, g, s);
+  else k_apply_op<false><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(lu, u, a, b, g, s);
   check_launch();
 }
 
 void residual(double *r, const double *u, const double *rhs, const double *a, const double *b,
               const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  k_residual<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
+  if (s.bconst)
+    k_residual<true><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
+  else
+    k_residual<false><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
   check_launch();
 }
 
@@ -499,8 +520,12 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
                        const double *a, const double *b, const BoxArgs &fg, const StencilCoefs &s,
                        hipStream_t st, bool accumulate) {
   if (cg.nx <= 0 || cg.ny <= 0 || cg.nz <= 0) return;
-  k_restrict<<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s,
-                                                                  accumulate ? 1 : 0);
+  if (s.bconst)
+    k_restrict<true><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s,
+                                                                        accumulate ? 1 : 0);
+  else
+    k_restrict<false><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg,
+                                                                         s, accumulate ? 1 : 0);
   check_launch();
 }
 
@@ -575,6 +600,8 @@ int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
     case 1: k_reduce_partial<1><<<grid, block, 0, st>>>(x, y, g, partials); break;
     case 2: k_reduce_partial<2><<<grid, block, 0, st>>>(x, y, g, partials); break;
     case 3: k_reduce_partial<3><<<grid, block, 0, st>>>(x, y, g, partials); break;
+    case 4: k_reduce_partial<4><<<grid, block, 0, st>>>(x, y, g, partials); break;
+    case 5: k_reduce_partial<5><<<grid, block, 0, st>>>(x, y, g, partials); break;
     default: throw Error(kBadArg, "reduce: bad kind");
   }
   check_launch();
@@ -587,6 +614,8 @@ void reduce_final(int kind, const double *partials, int n, double *out, hipStrea
     case 1: k_reduce_final<1><<<1, RB, 0, st>>>(partials, n, out); break;
     case 2: k_reduce_final<2><<<1, RB, 0, st>>>(partials, n, out); break;
     case 3: k_reduce_final<3><<<1, RB, 0, st>>>(partials, n, out); break;
+    case 4: k_reduce_final<4><<<1, RB, 0, st>>>(partials, n, out); break;
+    case 5: k_reduce_final<5><<<1, RB, 0, st>>>(partials, n, out); break;
     default: throw Error(kBadArg, "reduce: bad kind");
   }
   check_launch();

@@ -59,7 +59,8 @@ void fill_bc(double *u, const BoxArgs &g, hipStream_t st);
 // 4 x = s*y + t*z, 5 x = s (setVal)
 void blas(int kind, double *x, const double *y, const double *z, double s, double t,
           const BoxArgs &g, hipStream_t st);
-// Deterministic reductions: kind 0 dot(x,y), 1 sum|x|, 2 sum x^2, 3 max|x|.
+// Deterministic reductions: kind 0 dot(x,y), 1 sum|x|, 2 sum x^2, 3 max|x|,
+// 4 max x, 5 max(-x).
 // Writes nparts partials at partials[0..nparts); returns nparts.
 int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
                    double *partials, hipStream_t st);

@@ -165,6 +165,11 @@ struct StencilCoefs {
   double alpha, beta, dx;
   double dxinv;    // 1/(dx*dx)            (.ChF:89)
   double lamshift; // 2*3*beta/(dx*dx)     (.cpp:240)
+  // bCoef is one value everywhere (set_b_coef writes 1, SetLevelData.cpp:
+  // 330-340, and averaging keeps it): kernels use bval instead of loading
+  // the field -- the same operand, so bit-identical, 8 B/cell less traffic
+  int bconst = 0;
+  double bval = 1.0;
 };
 
 }  // namespace mgic

@@ -99,13 +99,16 @@ const BoxArgs &VariableCoeffPoissonOperator::args(int n, bool homogeneous) {
   return homogeneous ? args_hom_[n] : args_inhom_[n];
 }
 
-StencilCoefs VariableCoeffPoissonOperator::coefs() const {
+StencilCoefs VariableCoeffPoissonOperator::coefs() {
+  resetLambda();  // lazy: lambda and the constant-b test follow coefficient changes
   StencilCoefs s;
   s.alpha = m_alpha;
   s.beta = m_beta;
   s.dx = m_dx;
   s.dxinv = 1.0 / (m_dx * m_dx);                    // .ChF:89
   s.lamshift = 2.0 * 3 * m_beta / (m_dx * m_dx);    // .cpp:240
+  s.bconst = b_const_ ? 1 : 0;
+  s.bval = b_val_;
   return s;
 }
 
@@ -210,11 +213,15 @@ void VariableCoeffPoissonOperator::setCoefs(std::shared_ptr<LevelData> a,
 
 void VariableCoeffPoissonOperator::resetLambda() {
   if (!m_lambdaNeedsResetting) return;  // .cpp:222
+  m_lambdaNeedsResetting = false;
   if (!m_lambda) m_lambda = std::make_unique<LevelData>(grid);
+  // is bCoef one value everywhere?  (max b == min b over all ranks' boxes)
+  const double bmax = reduce(4, *m_bCoef, nullptr), bmin = -reduce(5, *m_bCoef, nullptr);
+  b_const_ = bmax == bmin && std::isfinite(bmax);
+  b_val_ = b_const_ ? bmax : 1.0;
   const StencilCoefs s = coefs();
   for (int n = 0; n < grid->nlocal(); ++n)
     kern::lambda(m_lambda->p[n], m_aCoef->p[n], args_plain_[n], s, stream());
-  m_lambdaNeedsResetting = false;
 }
 
 void VariableCoeffPoissonOperator::computeLambda() {
@@ -396,9 +403,13 @@ double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const 
   int total = 0;
   for (int n = 0; n < grid->nlocal(); ++n)
     total += kern::reduce_partial(kind, x.p[n], y ? y->p[n] : nullptr, args_plain_[n], parts + total, st);
-  if (total == 0) MGIC_HIP(hipMemsetAsync(c.d_result(), 0, sizeof(double), st));
+  if (total == 0) {  // no local cells: the identity of the reduction
+    c.h_result()[1] = kind >= 4 ? -HUGE_VAL : 0.0;  // pinned: safe for an async copy
+    MGIC_HIP(hipMemcpyAsync(c.d_result(), c.h_result() + 1, sizeof(double), hipMemcpyHostToDevice,
+                            st));
+  }
   else kern::reduce_final(kind, parts, total, c.d_result(), st);
-  c.allreduce(c.d_result(), kind == 3 ? 1 : 0);
+  c.allreduce(c.d_result(), kind >= 3 ? 1 : 0);
   MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
   MGIC_HIP(hipStreamSynchronize(st));
   return c.h_result()[0];

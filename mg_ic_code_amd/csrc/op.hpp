@@ -90,10 +90,12 @@ class VariableCoeffPoissonOperator {
   std::unique_ptr<LevelData> m_lambda;
   bool m_lambdaNeedsResetting = true;
   bool coef_ghosts_ = false;  // aCoef/bCoef face ghosts exchanged (fused sweep)
+  bool b_const_ = false;      // bCoef holds one value everywhere (all ranks)
+  double b_val_ = 1.0;
 
 
  private:
-  StencilCoefs coefs() const;
+  StencilCoefs coefs();  // refreshes lambda / coefficient state first
   const BoxArgs &args(int n, bool homogeneous);
   void build_args();
   double reduce(int kind, const LevelData &x, const LevelData *y);

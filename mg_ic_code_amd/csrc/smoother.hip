@@ -70,7 +70,7 @@ struct Fused6 {
 
 // One tile (x0, y0) of the box, planes [z0, z1): R/B are the 5-plane LDS
 // rings (5 * CP doubles each) holding the red / black element of each pair.
-template <int TX, int TY, int NT, bool ZIN>
+template <int TX, int TY, int NT, bool ZIN, bool BC>
 __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *__restrict__ B,
                                                double *__restrict__ uo,
                                                const double *__restrict__ ui,
@@ -162,7 +162,8 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
       const long off = rcoff[i] + pz;
       const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
       const double2 va = *reinterpret_cast<const double2 *>(a + off);
-      const double2 vb = *reinterpret_cast<const double2 *>(b + off);
+      const double2 vb = BC ? make_double2(s.bval, s.bval)
+                            : *reinterpret_cast<const double2 *>(b + off);
       nr0[i] = vr.x; nr1[i] = vr.y;
       na0[i] = va.x; na1[i] = va.y;
       nb0[i] = vb.x; nb1[i] = vb.y;
@@ -259,7 +260,7 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   }
 }
 
-template <int TX, int TY, int NT, bool ZIN>
+template <int TX, int TY, int NT, bool ZIN, bool BC>
 __global__ __launch_bounds__(NT) void k_gsrb_fused6(double *__restrict__ uo,
                                                     const double *__restrict__ ui,
                                                     const double *__restrict__ rhs,
@@ -276,8 +277,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused6(double *__restrict__ uo,
   const int L = xcd * q8 + min(xcd, r8) + i8;
   const int tx_ = L % ntx, ty_ = (L / ntx) % nty, tz_ = L / (ntx * nty);
   const int z0 = tz_ * kc;
-  fused6_segment<TX, TY, NT, ZIN>(R, B, uo, ui, rhs, a, b, g, s, tx_ * TX, ty_ * TY, z0,
-                                  min(z0 + kc, g.nz));
+  fused6_segment<TX, TY, NT, ZIN, BC>(R, B, uo, ui, rhs, a, b, g, s, tx_ * TX, ty_ * TY, z0,
+                                      min(z0 + kc, g.nz));
 }
 
 // ---- two sweeps per launch (temporal blocking) ---------------------------
@@ -305,7 +306,7 @@ struct Fused2x {
   static constexpr int S = 7;                // LDS ring planes p-5 .. p+1
 };
 
-template <int TX, int TY, int NT, bool ZIN>
+template <int TX, int TY, int NT, bool ZIN, bool BC>
 __global__ __launch_bounds__(NT) void k_gsrb_fused2x(double *__restrict__ uo,
                                                      const double *__restrict__ ui,
                                                      const double *__restrict__ rhs,
@@ -403,7 +404,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused2x(double *__restrict__ uo,
       const long off = rcoff[i] + pz;
       const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
       const double2 va = *reinterpret_cast<const double2 *>(a + off);
-      const double2 vb = *reinterpret_cast<const double2 *>(b + off);
+      const double2 vb = BC ? make_double2(s.bval, s.bval)
+                            : *reinterpret_cast<const double2 *>(b + off);
       nr0[i] = vr.x; nr1[i] = vr.y;
       na0[i] = va.x; na1[i] = va.y;
       nb0[i] = vb.x; nb1[i] = vb.y;
@@ -418,7 +420,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused2x(double *__restrict__ uo,
       const long off = rcoff[i] + pz + e;
       r[i] = rhs[off];
       av[i] = a[off];
-      bv[i] = b[off];
+      bv[i] = BC ? s.bval : b[off];
     }
   };
   auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
@@ -593,6 +595,35 @@ __global__ void k_fill_bc_faces(double *__restrict__ u, const BoxArgs g) {
 
 }  // namespace
 
+// workgroups of kernel `k` the whole device holds at once
+template <class K>
+static int resident_slots(K k, int nt) {
+  int dev = 0, ncu = 0, per = 0;
+  MGIC_HIP(hipGetDevice(&dev));
+  MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  MGIC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, nt, 0));
+  return (per > 0 ? per : 1) * (ncu > 0 ? ncu : 1);
+}
+
+// z chunk per workgroup: a workgroup streams kc planes plus `overlap` planes
+// of pipeline fill; minimise rounds(kc) * (kc + overlap), where rounds is
+// the number of waves of workgroups on `slots` resident slots (a partial
+// last round costs a full one)
+static int choose_kc(int tiles, int nz, int slots, int overlap) {
+  int best = nz;
+  double best_cost = 1e300;
+  for (int kc = nz; kc >= 8; --kc) {
+    const long nb = (long)tiles * ((nz + kc - 1) / kc);
+    const long rounds = (nb + slots - 1) / slots;
+    const double cost = (double)rounds * (kc + overlap);
+    if (cost < best_cost * 0.999) {
+      best_cost = cost;
+      best = kc;
+    }
+  }
+  return best;
+}
+
 template <int TX, int TY, int NT>
 static void launch_fused6(double *u_out, double *u_in, const double *rhs, const double *a,
                           const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
@@ -604,16 +635,23 @@ static void launch_fused6(double *u_out, double *u_in, const double *rhs, const 
                                                                                             g);
   }
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
-  int kc = g.nz;  // z chunk: >= ~3 workgroups per CU slot on 256 CUs
-  while (kc > 16 && (long)ntx * nty * ((g.nz + kc - 1) / kc) < 3072) kc = (kc + 1) / 2;
+  static const int slots = resident_slots(k_gsrb_fused6<TX, TY, NT, false, false>, NT);
+  const int kc = choose_kc(ntx * nty, g.nz, slots, 5);
   const int ntz = (g.nz + kc - 1) / kc;
   const int nblocks = ntx * nty * ntz;
-  if (zero_in)
-    k_gsrb_fused6<TX, TY, NT, true><<<dim3((unsigned)nblocks), dim3(NT), 0, st>>>(
-        u_out, u_in, rhs, a, b, g, s, kc, ntx, nty, nblocks);
+  const dim3 grid((unsigned)nblocks), block(NT);
+  if (zero_in && s.bconst)
+    k_gsrb_fused6<TX, TY, NT, true, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s, kc,
+                                                                  ntx, nty, nblocks);
+  else if (zero_in)
+    k_gsrb_fused6<TX, TY, NT, true, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
+                                                                   kc, ntx, nty, nblocks);
+  else if (s.bconst)
+    k_gsrb_fused6<TX, TY, NT, false, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
+                                                                   kc, ntx, nty, nblocks);
   else
-    k_gsrb_fused6<TX, TY, NT, false><<<dim3((unsigned)nblocks), dim3(NT), 0, st>>>(
-        u_out, u_in, rhs, a, b, g, s, kc, ntx, nty, nblocks);
+    k_gsrb_fused6<TX, TY, NT, false, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
+                                                                    kc, ntx, nty, nblocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw Error(kHipErr, std::string("fused sweep launch: ") + hipGetErrorString(e));
 }
@@ -627,12 +665,19 @@ static void launch_fused2x(double *u_out, const double *u_in, const double *rhs,
   while (kc > 32 && (long)ntx * nty * ((g.nz + kc - 1) / kc) < 2048) kc = (kc + 1) / 2;
   const int ntz = (g.nz + kc - 1) / kc;
   const int nblocks = ntx * nty * ntz;
-  if (zero_in)
-    k_gsrb_fused2x<TX, TY, NT, true><<<dim3((unsigned)nblocks), dim3(NT), 0, st>>>(
-        u_out, u_in, rhs, a, b, g, s, kc, ntx, nty, nblocks);
+  const dim3 grid((unsigned)nblocks), block(NT);
+  if (zero_in && s.bconst)
+    k_gsrb_fused2x<TX, TY, NT, true, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
+                                                                   kc, ntx, nty, nblocks);
+  else if (zero_in)
+    k_gsrb_fused2x<TX, TY, NT, true, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
+                                                                    kc, ntx, nty, nblocks);
+  else if (s.bconst)
+    k_gsrb_fused2x<TX, TY, NT, false, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
+                                                                    kc, ntx, nty, nblocks);
   else
-    k_gsrb_fused2x<TX, TY, NT, false><<<dim3((unsigned)nblocks), dim3(NT), 0, st>>>(
-        u_out, u_in, rhs, a, b, g, s, kc, ntx, nty, nblocks);
+    k_gsrb_fused2x<TX, TY, NT, false, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g,
+                                                                     s, kc, ntx, nty, nblocks);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw Error(kHipErr, std::string("fused sweep launch: ") + hipGetErrorString(e));
 }
@@ -649,18 +694,13 @@ void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, co
                         const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                         hipStream_t st) {
   switch (fused2x_variant()) {
-    case 1: launch_fused2x<120, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 2: launch_fused2x<56, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 3: launch_fused2x<56, 6, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 4: launch_fused2x<56, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 5: launch_fused2x<56, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 6: launch_fused2x<120, 4, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    default: launch_fused2x<56, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 1: launch_fused2x<56, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    default: launch_fused2x<56, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
   }
 }
 
 // tile shape, for measurement (MGIC_FUSED_VARIANT): 0 = 60x8 / 256 threads
-// (default), 1 = 124x12 / 512, 2 = 60x12 / 256
+// (default), 1 = 124x16 / 512, 2 = 60x32 / 1024
 static int fused_variant() {
   static int v = [] {
     const char *e = getenv("MGIC_FUSED_VARIANT");
@@ -673,8 +713,8 @@ void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const doub
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       hipStream_t st) {
   switch (fused_variant()) {
-    case 1: launch_fused6<124, 12, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 2: launch_fused6<60, 12, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 1: launch_fused6<124, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 2: launch_fused6<60, 32, 1024>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
     default: launch_fused6<60, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
   }
 }
