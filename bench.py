@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--size", type=int, default=512, help="cells per side of the fine level")
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--nsmooth", type=int, default=4)
     ap.add_argument("--no-fused", action="store_true", help="per-colour smoother launches")
@@ -65,8 +65,11 @@ def main():
     from mg_ic_code_amd.decomposition import decompose
     from mg_ic_code_amd.params import read_params_file
 
-    torch.cuda.set_device(local_rank)
-    mg.set_device(local_rank)
+    # MGIC_BENCH_DEVICE pins every rank to one device (rehearsing the
+    # multi-rank path on a one-GPU machine); default: one GPU per rank
+    dev = int(os.environ.get("MGIC_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev)
+    mg.set_device(dev)
 
     dist = None
     if world > 1:
@@ -81,7 +84,7 @@ def main():
         comm = mg.Comm()
 
     prm = read_params_file(os.path.join(ROOT, "tests", "golden", "params.txt"))
-    n = args.n
+    n = args.size
     dx = prm.L / n
     bh = prm.bh()
     bh["domain_length"] = dx * n
@@ -217,7 +220,7 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
     """The oracle (C restatement, OpenMP) on the same inputs: bounded sample
     of `cpu_baseline_iters` V-cycle iterations of the same workload."""
     import oracle
-    n = args.n
+    n = args.size
     a = fa.download(0)
     rhs = frhs.download(0)
     oracle.set_threads(args.cpu_threads)
