@@ -146,6 +146,13 @@ MGIC_API int mgic_field_copy_to(mgic_field src, mgic_field dst, int with_faces);
  *           bh1_bare_mass, bh2_bare_mass, bh1_spin, bh2_spin, bh1_offset,
  *           bh2_offset, bh1_momentum, bh2_momentum, constant_K} */
 MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]);
+/* the same at a general conformal factor psi (read with its ghost layer);
+ * psi = NULL is psi = 1 (NL iteration 0) */
+MGIC_API int mgic_field_nl_coefs(mgic_field psi, mgic_field acoef, mgic_field rhs,
+                                 const double bh[13]);
+/* every cell of the allocation, ghosts included (set_initial_conditions
+ * sets psi over the whole FAB, SetLevelData.cpp:31-72) */
+MGIC_API int mgic_field_set_val_all(mgic_field f, double v);
 
 /* ---- operator factory (defineOperatorFactory, Factory.cpp:29-49) */
 MGIC_API int mgic_factory_define(mgic_grid g, const mgic_op_params *p, mgic_field aCoef,
@@ -178,6 +185,10 @@ MGIC_API int mgic_op_set_coefs(mgic_op op, mgic_field aCoef, mgic_field bCoef, d
                                double beta);
 MGIC_API int mgic_op_reset_lambda(mgic_op op);
 MGIC_API int mgic_op_set_time(mgic_op op, double t);
+/* set_update_psi0 (SetLevelData.cpp:236-256): exchange dpsi, its domain
+ * ghosts = the inhomogeneous BC image, psi += dpsi over the valid cells and
+ * ghost layer 1 */
+MGIC_API int mgic_op_update_psi(mgic_op op, mgic_field psi, mgic_field dpsi);
 MGIC_API int mgic_op_fill_bc(mgic_op op, mgic_field u, int homogeneous);         /* m_bc */
 MGIC_API int mgic_op_set_to_zero(mgic_op op, mgic_field x);
 MGIC_API int mgic_op_assign(mgic_op op, mgic_field lhs, mgic_field rhs);

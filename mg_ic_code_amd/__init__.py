@@ -23,6 +23,7 @@ from .core import (  # noqa: F401
     prof_smoother,
     prof_smoother_read,
     set_binary_bh_coefs,
+    set_nl_coefs,
     set_device,
 )
 from ._lib import LIB_PATH, lib  # noqa: F401

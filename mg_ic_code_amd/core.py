@@ -45,6 +45,7 @@ __all__ = [
     "defineOperatorFactory",
     "bicgstab",
     "set_binary_bh_coefs",
+    "set_nl_coefs",
     "prof_smoother",
     "prof_smoother_read",
     "MgicError",
@@ -224,6 +225,10 @@ class LevelData:
     def set_zero(self) -> None:
         call("mgic_field_set_zero", self._h)
 
+    def set_val_all(self, v: float) -> None:
+        """Every cell of the allocation, ghosts included."""
+        call("mgic_field_set_val_all", self._h, ctypes.c_double(v))
+
     def exchange(self) -> None:
         call("mgic_field_exchange", self._h)
 
@@ -374,6 +379,10 @@ class VariableCoeffPoissonOperator:
 
     def fillBC(self, u: LevelData, homogeneous: bool = True):
         call("mgic_op_fill_bc", self._h, u.handle, int(bool(homogeneous)))
+
+    def update_psi(self, psi: LevelData, dpsi: LevelData):
+        """set_update_psi0 (SetLevelData.cpp:236-256): psi += dpsi incl. ghost layer 1."""
+        call("mgic_op_update_psi", self._h, psi.handle, dpsi.handle)
 
     # --- LinearOp vector interface
     def setToZero(self, x: LevelData):
@@ -592,6 +601,14 @@ class BiCGStabSolver:
 BH_KEYS = ("domain_length", "G_Newton", "phi_amplitude", "phi_wavelength", "bh1_bare_mass",
            "bh2_bare_mass", "bh1_spin", "bh2_spin", "bh1_offset", "bh2_offset", "bh1_momentum",
            "bh2_momentum", "constant_K")
+
+
+def set_nl_coefs(psi: Optional[LevelData], acoef: LevelData, rhs: LevelData, bh: dict) -> None:
+    """set_a_coef + set_rhs (SetLevelData.cpp:73-127, :281-325) at conformal factor psi
+    (None: psi = 1) on device."""
+    vals = (ctypes.c_double * 13)(*[float(bh[k]) for k in BH_KEYS])
+    call("mgic_field_nl_coefs", psi.handle if psi is not None else None, acoef.handle, rhs.handle,
+         vals)
 
 
 def set_binary_bh_coefs(acoef: LevelData, rhs: LevelData, bh: dict) -> None:

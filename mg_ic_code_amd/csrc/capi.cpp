@@ -498,29 +498,53 @@ MGIC_API int mgic_field_copy_to(mgic_field src, mgic_field dst, int with_faces) 
     MGIC_HIP(hipStreamSynchronize(dst->f->grid->comm->stream()));
   });
 }
-MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]) {
+static kern::BhParams bh_params(const double bh[13]) {
+  kern::BhParams p;
+  for (int d = 0; d < 3; ++d) p.domlen[d] = bh[0];
+  p.G_Newton = bh[1];
+  p.phi_amplitude = bh[2];
+  p.phi_wavelength = bh[3];
+  p.m1 = bh[4];
+  p.m2 = bh[5];
+  p.spin1 = bh[6];
+  p.spin2 = bh[7];
+  p.off1 = bh[8];
+  p.off2 = bh[9];
+  p.mom1 = bh[10];
+  p.mom2 = bh[11];
+  p.constant_K = bh[12];
+  return p;
+}
+MGIC_API int mgic_field_nl_coefs(mgic_field psi, mgic_field acoef, mgic_field rhs,
+                                 const double bh[13]) {
   return guard([&] {
     NEED(acoef);
     NEED(rhs);
     NEED(bh);
     const Grid &g = *acoef->f->grid;
-    kern::BhParams p;
-    for (int d = 0; d < 3; ++d) p.domlen[d] = bh[0];
-    p.G_Newton = bh[1];
-    p.phi_amplitude = bh[2];
-    p.phi_wavelength = bh[3];
-    p.m1 = bh[4];
-    p.m2 = bh[5];
-    p.spin1 = bh[6];
-    p.spin2 = bh[7];
-    p.off1 = bh[8];
-    p.off2 = bh[9];
-    p.mom1 = bh[10];
-    p.mom2 = bh[11];
-    p.constant_K = bh[12];
+    if (psi) check_same_layout(g, *psi->f, "psi");
+    check_same_layout(g, *rhs->f, "rhs");
+    const kern::BhParams p = bh_params(bh);
     for (int n = 0; n < g.nlocal(); ++n)
-      kern::binary_bh_coefs(acoef->f->p[n], rhs->f->p[n], g.box_args_plain(n), g.dx, p,
-                            g.comm->stream());
+      kern::binary_bh_coefs(acoef->f->p[n], rhs->f->p[n], psi ? psi->f->p[n] : nullptr,
+                            g.box_args_plain(n), g.dx, p, g.comm->stream());
+  });
+}
+MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]) {
+  return mgic_field_nl_coefs(nullptr, acoef, rhs, bh);
+}
+MGIC_API int mgic_field_set_val_all(mgic_field f, double v) {
+  return guard([&] {
+    NEED(f);
+    const Grid &g = *f->f->grid;
+    for (int n = 0; n < g.nlocal(); ++n) {  // the valid box grown by every ghost layer
+      BoxArgs a = g.box_args_plain(n);
+      a.nx += 2 * kGhost;
+      a.ny += 2 * kGhost;
+      a.nz += 2 * kGhost;
+      double *base = f->f->p[n] - kGhost * (1 + a.sy + a.sz);
+      kern::blas(5, base, nullptr, nullptr, v, 0.0, a, g.comm->stream());
+    }
   });
 }
 
@@ -638,6 +662,23 @@ MGIC_API int mgic_op_set_coefs(mgic_op op, mgic_field a, mgic_field b, double al
 }
 MGIC_API int mgic_op_reset_lambda(mgic_op op) { OPGUARD(o.resetLambda()); }
 MGIC_API int mgic_op_set_time(mgic_op op, double t) { OPGUARD(o.setTime(t)); }
+MGIC_API int mgic_op_update_psi(mgic_op op, mgic_field psi, mgic_field dpsi) {
+  return guard([&] {
+    NEED(op);
+    NEED(psi);
+    NEED(dpsi);
+    VariableCoeffPoissonOperator &o = *op->op;
+    check_same_layout(*o.grid, *psi->f, "psi");
+    check_same_layout(*o.grid, *dpsi->f, "dpsi");
+    // set_update_psi0 (SetLevelData.cpp:236-256): dpsi ghosts from the
+    // exchange (domain faces: the inhomogeneous BC image), psi += dpsi over
+    // the valid cells and the ghost layer the stencils read
+    dpsi->f->exchange(o.stream());
+    o.fillBC(*dpsi->f, false);
+    for (int n = 0; n < o.grid->nlocal(); ++n)
+      kern::incr_grown(psi->f->p[n], dpsi->f->p[n], o.grid->box_args_plain(n), 1, o.stream());
+  });
+}
 MGIC_API int mgic_op_fill_bc(mgic_op op, mgic_field u, int h) {
   OPGUARD(NEED(u); o.fillBC(*u->f, h != 0));
 }

@@ -422,9 +422,12 @@ __device__ double bh_Aij(int i, int j, double r1, double r2, const double *n1, c
   return Aij;
 }
 
+// set_a_coef + set_rhs (SetLevelData.cpp:73-127, :281-325); psi == nullptr:
+// psi = 1 everywhere (NL iteration 0), else psi read with its ghost layer
 __global__ __launch_bounds__(256) void k_binary_bh(double *__restrict__ acoef,
-                                                   double *__restrict__ rhs, const BoxArgs g,
-                                                   double dx, const BhParams p) {
+                                                   double *__restrict__ rhs,
+                                                   const double *__restrict__ psi,
+                                                   const BoxArgs g, double dx, const BhParams p) {
   const int i = blockIdx.x * TX + threadIdx.x;
   const int j = blockIdx.y * TY + threadIdx.y;
   const int k = blockIdx.z;
@@ -460,10 +463,15 @@ __global__ __launch_bounds__(256) void k_binary_bh(double *__restrict__ acoef,
   const double rho = 0.5 * 0.0 * 0.0 + 0.0;
   const double m = (2.0 / 3.0) * (p.constant_K * p.constant_K) - 16.0 * M_PI * p.G_Newton * rho;
   const double psi_bh = p.m1 / r1 + p.m2 / r2;  // SetBinaryBH.H:85-99
-  const double psi_0 = 1.0 + psi_bh;
-  double lap = 0.0;  // GETLAPLACIANPSIF of psi == 1
-  for (int d0 = 0; d0 < 3; ++d0) lap = lap + 1.0 / dx / dx * (+1.0 * 1.0 - 2.0 * 1.0 + 1.0 * 1.0);
   const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  const double psi_c = psi ? psi[idx] : 1.0;
+  const double psi_0 = psi_c + psi_bh;  // SetLevelData.cpp:319-320
+  double lap = 0.0;  // GETLAPLACIANPSIF, SetLevelDataF.ChF:15-58 (2nd order)
+  const long st[3] = {1, g.sy, g.sz};
+  for (int d0 = 0; d0 < 3; ++d0) {
+    const double pm = psi ? psi[idx - st[d0]] : 1.0, pp = psi ? psi[idx + st[d0]] : 1.0;
+    lap = lap + 1.0 / dx / dx * (+1.0 * pm - 2.0 * psi_c + 1.0 * pp);
+  }
   acoef[idx] = -0.625 * m * pow(psi_0, 4.0) - A2 * pow(psi_0, -8.0) +
                2.0 * M_PI * p.G_Newton * rho_grad;  // SetLevelData.cpp:321-322
   rhs[idx] = 0.125 * m * pow(psi_0, 5.0) - 0.125 * A2 * pow(psi_0, -7.0) -
@@ -631,10 +639,31 @@ void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *con
   check_launch();
 }
 
-void binary_bh_coefs(double *acoef, double *rhs, const BoxArgs &g, double dx, const BhParams &p,
-                     hipStream_t st) {
+void binary_bh_coefs(double *acoef, double *rhs, const double *psi, const BoxArgs &g, double dx,
+                     const BhParams &p, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  k_binary_bh<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(acoef, rhs, g, dx, p);
+  k_binary_bh<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(acoef, rhs, psi, g, dx, p);
+  check_launch();
+}
+
+// x += y over the valid box grown by `grow` cells (set_update_psi0 adds over
+// the whole FAB, SetLevelData.cpp:236-256; one ghost layer is all the
+// stencils read)
+__global__ __launch_bounds__(256) void k_incr_grown(double *__restrict__ x,
+                                                    const double *__restrict__ y, const BoxArgs g,
+                                                    int grow) {
+  const int i = (int)(blockIdx.x * TX + threadIdx.x) - grow;
+  const int j = (int)(blockIdx.y * TY + threadIdx.y) - grow;
+  const int k = (int)blockIdx.z - grow;
+  if (i >= g.nx + grow || j >= g.ny + grow) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  x[idx] = x[idx] + y[idx];
+}
+
+void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_incr_grown<<<grid_cells(g.nx + 2 * grow, g.ny + 2 * grow, g.nz + 2 * grow), kBlock, 0, st>>>(
+      x, y, g, grow);
   check_launch();
 }
 

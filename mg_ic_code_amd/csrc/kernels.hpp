@@ -78,8 +78,11 @@ struct BhParams {
   double G_Newton, phi_amplitude, phi_wavelength;
   double m1, m2, spin1, spin2, off1, off2, mom1, mom2, constant_K;
 };
-void binary_bh_coefs(double *acoef, double *rhs, const BoxArgs &g, double dx,
+// psi: nullptr = psi 1 everywhere, else read with its ghost layer
+void binary_bh_coefs(double *acoef, double *rhs, const double *psi, const BoxArgs &g, double dx,
                      const BhParams &p, hipStream_t st);
+// x += y over the valid box grown by `grow` (<= kGhost) cells
+void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStream_t st);
 
 }  // namespace kern
 }  // namespace mgic

@@ -65,7 +65,7 @@ int prof_read(double *total_ms, long *passes) {
 // --------------------------------------------------------------- operator
 int VariableCoeffPoissonOperator::s_maxCoarse = 2;
 
-static void check_same_layout(const Grid &g, const LevelData &x, const char *what) {
+void check_same_layout(const Grid &g, const LevelData &x, const char *what) {
   const Grid &h = *x.grid;
   bool ok = h.nlocal() == g.nlocal();
   for (int n = 0; ok && n < g.nlocal(); ++n)

@@ -115,6 +115,9 @@ class VariableCoeffPoissonOperator {
   void relaxFromZero(LevelData &e, const LevelData &r, int n);
 };
 
+// throws kBadArg unless x lives on g's boxes with g's fab geometry
+void check_same_layout(const Grid &g, const LevelData &x, const char *what);
+
 // CoarseAverage (arithmetic / harmonic) of a fine LevelData onto the layout
 // coarsened by `ratio` (same box order and owners).
 std::shared_ptr<LevelData> average_coef(const LevelData &fine, std::shared_ptr<Grid> cgrid,

@@ -636,7 +636,18 @@ static void launch_fused6(double *u_out, double *u_in, const double *rhs, const 
   }
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
   static const int slots = resident_slots(k_gsrb_fused6<TX, TY, NT, false, false>, NT);
-  const int kc = choose_kc(ntx * nty, g.nz, slots, 5);
+  static const int kc_mode = [] {
+    const char *e = getenv("MGIC_KC_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  int kc = g.nz;
+  if (kc_mode == 1) {  // >= 3072 workgroups
+    while (kc > 16 && (long)ntx * nty * ((g.nz + kc - 1) / kc) < 3072) kc = (kc + 1) / 2;
+  } else if (kc_mode >= 16) {
+    kc = kc_mode < g.nz ? kc_mode : g.nz;
+  } else {
+    kc = choose_kc(ntx * nty, g.nz, slots, 5);
+  }
   const int ntz = (g.nz + kc - 1) / kc;
   const int nblocks = ntx * nty * ntz;
   const dim3 grid((unsigned)nblocks), block(NT);

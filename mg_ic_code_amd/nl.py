@@ -1,0 +1,77 @@
+"""The nonlinear solve of Main_PoissonSolver.cpp on one AMR level, on device.
+
+`poisson_solve` mirrors `poissonSolve` (Main_PoissonSolver.cpp:51-250) for
+max_level = 0:
+
+    psi = 1, dpsi = 0                     set_initial_conditions (SetLevelData.cpp:31-72)
+    for NL_iter < max_NL_iterations:      :129-220
+        aCoef, rhs from psi               set_a_coef / set_rhs (:155-161)
+        bCoef = 1                         set_b_coef
+        factory, MG, BiCGStab             defineOperatorFactory, mlOp, solver (:163-178)
+        solver.solve(dpsi, rhs)           :184 (dpsi keeps its value between NL iterations)
+        psi += dpsi                       set_update_psi0 (:188-207)
+        stop if |dpsi| < tolerance or > 1e5   computeNorm (:210-217)
+
+Every field stays in HBM, and each step is a libmgic kernel. Not covered:
+AMR levels (max_level > 0), the periodic constant-K integrability condition
+(:133-147), and the HDF5 output.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from .core import (AMRMultiGrid, BiCGStabSolver, Grid, LevelData, MultilevelLinearOp,
+                   OperatorParams, SolverParams, defineOperatorFactory, set_nl_coefs)
+from .params import PoissonParameters
+
+
+@dataclass
+class NLResult:
+    psi: LevelData
+    dpsi: LevelData
+    dpsi_norms: List[float] = field(default_factory=list)
+    linear_iterations: List[int] = field(default_factory=list)
+    converged: bool = False
+
+
+def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
+                  prolong_type: int = 1, bottom_solver: int = 1,
+                  max_NL_iterations: Optional[int] = None) -> NLResult:
+    if any(prm.bc_lo[d] == 2 or prm.bc_hi[d] == 2 for d in range(3)) or prm.is_periodic:
+        raise NotImplementedError("periodic domains need the constant-K integrability step "
+                                  "(Main_PoissonSolver.cpp:133-147), not built yet")
+    psi, dpsi = LevelData(grid), LevelData(grid)
+    a, b, rhs = LevelData(grid), LevelData(grid), LevelData(grid)
+    psi.set_val_all(1.0)
+    dpsi.set_zero()
+    b.set_val(1.0)  # set_b_coef (SetLevelData.cpp:330-340)
+    bh = prm.bh(constant_K=0.0)
+    avg = prm.coefficient_average_type if prm.coefficient_average_type >= 0 else 0
+    op_params = OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                               bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
+                               coefficient_average_type=avg, prolong_type=prolong_type,
+                               relax_mode=1)
+    depth = prm.preCondSolverDepth if prm.preCondSolverDepth >= 0 else max_depth
+    res = NLResult(psi=psi, dpsi=dpsi)
+    n_nl = prm.max_NL_iterations if max_NL_iterations is None else max_NL_iterations
+    dx = grid.dx
+    for _ in range(n_nl):
+        set_nl_coefs(psi, a, rhs, bh)  # :155-161
+        fac = defineOperatorFactory(grid, a, b, op_params)
+        amg = AMRMultiGrid(fac, SolverParams(max_depth=depth, n_pre=prm.numMGsmooth,
+                                             n_post=prm.numMGsmooth, n_bottom=prm.numMGsmooth,
+                                             bottom_solver=bottom_solver))
+        solver = BiCGStabSolver(MultilevelLinearOp(amg, prm.numMGIterations),
+                                tolerance=prm.tolerance, max_iterations=prm.max_iterations,
+                                norm_type=0)
+        res.linear_iterations.append(solver.solve(dpsi, rhs))
+        op0 = amg.op(0)
+        op0.update_psi(psi, dpsi)
+        # computeNorm (L2 over the level, dV = dx^3)
+        nrm = op0.norm(dpsi, 2) * dx ** 1.5
+        res.dpsi_norms.append(nrm)
+        if nrm < prm.tolerance or nrm > 1e5:
+            res.converged = nrm < prm.tolerance
+            break
+    return res

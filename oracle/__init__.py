@@ -96,6 +96,8 @@ _sig = {
     "orc_mg_dot": [ctypes.c_void_p, c_int, c_int, c_int],
     "orc_mg_last_bicg_iters": [ctypes.c_void_p],
     "orc_binary_bh_coefs": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double), POINTER(c_double)],
+    "orc_nl_coefs": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double), POINTER(c_double),
+                     POINTER(c_double)],
     "orc_set_threads": [c_int],
     "orc_get_threads": [],
 }
@@ -167,17 +169,32 @@ def prolong(fine: Fab, coarse: Fab, frlo, frhi, cvlo, cvhi, avail_lo, avail_hi, 
                      _i3(avail_hi), int(ptype))
 
 
+def _bh_params(bh: dict) -> BHParams:
+    return BHParams(L=bh["domain_length"], G_Newton=bh["G_Newton"],
+                    phi_amplitude=bh["phi_amplitude"], phi_wavelength=bh["phi_wavelength"],
+                    bh1_bare_mass=bh["bh1_bare_mass"], bh2_bare_mass=bh["bh2_bare_mass"],
+                    bh1_spin=bh["bh1_spin"], bh2_spin=bh["bh2_spin"], bh1_offset=bh["bh1_offset"],
+                    bh2_offset=bh["bh2_offset"], bh1_momentum=bh["bh1_momentum"],
+                    bh2_momentum=bh["bh2_momentum"], constant_K=bh["constant_K"])
+
+
 def binary_bh(bh: dict, lo, hi, dx):
-    p = BHParams(L=bh["domain_length"], G_Newton=bh["G_Newton"],
-                 phi_amplitude=bh["phi_amplitude"], phi_wavelength=bh["phi_wavelength"],
-                 bh1_bare_mass=bh["bh1_bare_mass"], bh2_bare_mass=bh["bh2_bare_mass"],
-                 bh1_spin=bh["bh1_spin"], bh2_spin=bh["bh2_spin"], bh1_offset=bh["bh1_offset"],
-                 bh2_offset=bh["bh2_offset"], bh1_momentum=bh["bh1_momentum"],
-                 bh2_momentum=bh["bh2_momentum"], constant_K=bh["constant_K"])
+    """aCoef, rhs at psi = 1 over [lo, hi] (arrays (nz, ny, nx))."""
+    return nl_coefs(bh, lo, hi, dx, None)
+
+
+def nl_coefs(bh: dict, lo, hi, dx, psi=None):
+    """set_a_coef / set_rhs at psi given over [lo-1, hi+1] (None: psi = 1)."""
+    p = _bh_params(bh)
     shape = (hi[2] - lo[2] + 1, hi[1] - lo[1] + 1, hi[0] - lo[0] + 1)
     a = np.empty(shape)
     r = np.empty(shape)
-    _lib.orc_binary_bh_coefs(ctypes.byref(p), _i3(lo), _i3(hi), dx, _dp(a), _dp(r))
+    if psi is None:
+        _lib.orc_binary_bh_coefs(ctypes.byref(p), _i3(lo), _i3(hi), dx, _dp(a), _dp(r))
+    else:
+        g = np.ascontiguousarray(psi, dtype=np.float64)
+        assert g.shape == tuple(n + 2 for n in shape)
+        _lib.orc_nl_coefs(ctypes.byref(p), _i3(lo), _i3(hi), dx, _dp(g), _dp(a), _dp(r))
     return a, r
 
 

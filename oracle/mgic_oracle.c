@@ -855,8 +855,8 @@ static double get_Aij(int i, int j, double r1, double r2, const double *n1, cons
   return Aij;
 }
 
-void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
-                         double *acoef, double *rhs) {
+void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                  const double *psi, double *acoef, double *rhs) {
   const double domlen[3] = {p->L, p->L, p->L};
   const size_t nx = (size_t)(hi[0] - lo[0] + 1), ny = (size_t)(hi[1] - lo[1] + 1);
 #pragma omp parallel for schedule(static)
@@ -903,11 +903,19 @@ void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi, d
         double b1[3] = {loc[0], loc[1], loc[2]}, b2[3] = {loc[0], loc[1], loc[2]};
         const double rb1 = bh_radius(b1, p->bh1_offset), rb2 = bh_radius(b2, p->bh2_offset);
         const double psi_bh = p->bh1_bare_mass / rb1 + p->bh2_bare_mass / rb2;
-        const double psi_0 = 1.0 + psi_bh;
-        /* GETLAPLACIANPSIF of psi == 1 (SetLevelDataF.ChF:15-58) */
+        /* psi over the box grown by one (NULL: psi == 1, set_initial_conditions :54) */
+        const size_t gx = nx + 2, gy = ny + 2;
+        const size_t gc = (size_t)(i - lo[0] + 1) + gx * ((size_t)(j - lo[1] + 1) +
+                                                          gy * (size_t)(k - lo[2] + 1));
+        const size_t gs[3] = {1, gx, gx * gy};
+        const double psi_c = psi ? psi[gc] : 1.0;
+        const double psi_0 = psi_c + psi_bh; /* SetLevelData.cpp:319-320 */
+        /* GETLAPLACIANPSIF (SetLevelDataF.ChF:15-58), 2nd order */
         double lap = 0.0;
-        for (int d0 = 0; d0 < 3; ++d0)
-          lap = lap + 1.0 / dx / dx * (+1.0 * 1.0 - 2.0 * 1.0 + 1.0 * 1.0);
+        for (int d0 = 0; d0 < 3; ++d0) {
+          const double pm = psi ? psi[gc - gs[d0]] : 1.0, pp = psi ? psi[gc + gs[d0]] : 1.0;
+          lap = lap + 1.0 / dx / dx * (+1.0 * pm - 2.0 * psi_c + 1.0 * pp);
+        }
         const size_t n = (size_t)(i - lo[0]) + nx * ((size_t)(j - lo[1]) + ny * (size_t)(k - lo[2]));
         /* set_a_coef, SetLevelData.cpp:321-322 */
         acoef[n] = -0.625 * m * pow(psi_0, 4.0) - A2 * pow(psi_0, -8.0) +
@@ -916,6 +924,12 @@ void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi, d
         rhs[n] = 0.125 * m * pow(psi_0, 5.0) - 0.125 * A2 * pow(psi_0, -7.0) -
                  2.0 * M_PI * p->G_Newton * rho_grad * psi_0 - lap;
       }
+}
+
+/* aCoef / rhs at psi = 1 (NL iteration 0) */
+void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                         double *acoef, double *rhs) {
+  orc_nl_coefs(p, lo, hi, dx, NULL, acoef, rhs);
 }
 
 void orc_set_threads(int n) {

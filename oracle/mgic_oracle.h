@@ -169,6 +169,10 @@ typedef struct {
  * contiguous i fastest; dx is the cell spacing of that level */
 void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi,
                          double dx, double *acoef, double *rhs);
+/* set_a_coef + set_rhs (SetLevelData.cpp:73-127, :281-325) at a general
+ * psi given over the box grown by one (i fastest), constant_K from p */
+void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                  const double *psi, double *acoef, double *rhs);
 
 void orc_set_threads(int n);
 int orc_get_threads(void);

@@ -1,0 +1,38 @@
+"""Oracle side of the nonlinear loop (Main_PoissonSolver.cpp:129-220) on one
+box, for the NL tests: the same steps as mg_ic_code_amd/nl.py, run through
+the C oracle.  Test infrastructure only."""
+import numpy as np
+
+import oracle
+
+
+def oracle_poisson_solve(prm, n, max_depth, n_nl, bottom_solver=1):
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    dx = prm.domainLength[0] / n
+    bh = prm.bh(constant_K=0.0)
+    avg = prm.coefficient_average_type if prm.coefficient_average_type >= 0 else 0
+    o = oracle.OracleMG([dom], dom, dx, alpha=prm.alpha, beta=prm.beta, bc_lo=prm.bc_lo,
+                        bc_hi=prm.bc_hi, bc_value=prm.bc_value, nlevels=max_depth + 1,
+                        avg_type=avg, prolong_type=1, bottom_solver=bottom_solver,
+                        n_pre=prm.numMGsmooth, n_post=prm.numMGsmooth, n_bottom=prm.numMGsmooth)
+    psi = np.ones((n + 2,) * 3)          # set_initial_conditions: psi = 1 incl. ghosts
+    o.set(0, oracle.PHI, 0, np.zeros((n,) * 3))
+    norms, iters = [], []
+    for _ in range(n_nl):
+        a, r = oracle.nl_coefs(bh, (0, 0, 0), (n - 1,) * 3, dx, psi)
+        o.set(0, oracle.ACOEF, 0, a)
+        o.set(0, oracle.BCOEF, 0, np.ones_like(a))
+        o.set(0, oracle.RHS, 0, r)
+        o.setup()
+        it, _ = o.solve(mg_iters=prm.numMGIterations, imax=prm.max_iterations,
+                        eps=prm.tolerance, norm_type=0)
+        iters.append(it)
+        o.exchange(0, oracle.PHI)          # set_update_psi0
+        o.fill_bc(0, oracle.PHI, 0)
+        psi += o.get(0, oracle.PHI, 0, full=True)
+        dpsi = o.get(0, oracle.PHI, 0)
+        nrm = np.sqrt(np.sum(dpsi * dpsi)) * dx ** 1.5
+        norms.append(nrm)
+        if nrm < prm.tolerance or nrm > 1e5:
+            break
+    return psi, norms, iters

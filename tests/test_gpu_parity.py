@@ -404,3 +404,45 @@ def test_outer_bicgstab_solve_matches_oracle(comm, rng, parts):
     c = S["o"].get(0, oracle.PHI, 0)
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
     assert solver.final_norm <= 1e-9 * np.max(np.abs(S["rhs"]))  # true residual, max norm
+
+
+# --------------------------------------------- the NL loop
+def test_nl_coefs_on_device_match_oracle(comm, rng):
+    # set_a_coef / set_rhs at a non-trivial psi (with ghosts), params.txt BH
+    import os
+    from mg_ic_code_amd.params import read_params_file
+    prm = read_params_file(os.path.join(os.path.dirname(__file__), "golden", "params.txt"))
+    n = 32
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    dx = prm.domainLength[0] / n
+    grid = mg.Grid(comm, dom, [dom], dx)
+    psi, fa, fr = mg.LevelData(grid), mg.LevelData(grid), mg.LevelData(grid)
+    pg = 1.0 + 0.01 * rng.uniform(-1, 1, (n + 2,) * 3)
+    psi.upload(0, pg, with_ghosts=True)
+    mg.set_nl_coefs(psi, fa, fr, prm.bh())
+    a_o, r_o = oracle.nl_coefs(prm.bh(), (0, 0, 0), (n - 1,) * 3, dx, pg)
+    np.testing.assert_allclose(fa.download(0), a_o, rtol=1e-13, atol=1e-300)
+    np.testing.assert_allclose(fr.download(0), r_o, rtol=1e-12, atol=1e-14)
+
+
+def test_nonlinear_poisson_solve_matches_oracle(comm):
+    # Main_PoissonSolver's NL loop: coefficients from psi, MG-preconditioned
+    # BiCGStab, psi += dpsi, |dpsi| -- GPU against the oracle loop
+    import os
+    from mg_ic_code_amd.nl import poisson_solve
+    from mg_ic_code_amd.params import read_params_file
+    from tests.nl_ref import oracle_poisson_solve
+    prm = read_params_file(os.path.join(os.path.dirname(__file__), "golden", "params.txt"))
+    n = 32
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    grid = mg.Grid(comm, dom, [dom], prm.domainLength[0] / n)
+    res = poisson_solve(grid, prm, max_depth=3, max_NL_iterations=3)
+    psi_o, norms_o, iters_o = oracle_poisson_solve(prm, n, max_depth=3, n_nl=3)
+    # the first two NL steps carry the solution; the third dpsi is at the
+    # linear solver's roundoff floor, where the two dot-product orders differ
+    assert res.linear_iterations[:2] == iters_o[:2]
+    np.testing.assert_allclose(res.dpsi_norms[:2], norms_o[:2], rtol=1e-6)
+    assert abs(res.dpsi_norms[2] - norms_o[2]) <= 0.1 * norms_o[2]
+    g = res.psi.download(0, with_ghosts=True)[1:-1, 1:-1, 1:-1]
+    c = psi_o[1:-1, 1:-1, 1:-1]
+    assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
