@@ -253,7 +253,7 @@ static int sweeps_per_launch() {
 }
 
 void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
-                                              bool zero_in) {
+                                              bool zero_in, LevelData *acc) {
   resetLambda();  // .cpp:283
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
@@ -268,10 +268,11 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     }
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
-  const int per = sweeps_per_launch();
+  const int per = acc ? 1 : sweeps_per_launch();
   for (int it = 0; it < n;) {
     const bool zin = zero_in && it == 0;
     const int k = (per == 2 && !halo && n - it >= 2) ? 2 : 1;
+    const bool last = it + k == n;
     if (halo && !zin) src->exchange_shell(st);
     for (int b = 0; b < grid->nlocal(); ++b) {
       const long nc = grid->geom[b].valid.ncells();
@@ -281,15 +282,27 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
                                  args_hom_[b], s, zin, st);
       else
         kern::gsrb_sweep_fused(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
-                               args_hom_[b], s, zin, st);
+                               args_hom_[b], s, zin, last && acc ? acc->p[b] : nullptr, st);
       prof_mark(st, nc, false, 2 * k);
     }
     std::swap(src, dst);
     it += k;
   }
+  if (acc) return;   // the last sweep went into acc; dpsi is scratch now
   if (src != &dpsi)  // the result sits in the scratch buffer
     for (int b = 0; b < grid->nlocal(); ++b)
       kern::blas(0, dpsi.p[b], src->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
+}
+
+void VariableCoeffPoissonOperator::relaxAccumulate(LevelData &e, const LevelData &r, int n,
+                                                   LevelData &phi) {
+  if (n > 0 && prm.relax_mode == 1 && fusedSmootherApplies()) {
+    check_same_layout(*grid, phi, "phi");
+    fusedRelax(e, r, n, false, &phi);
+    return;
+  }
+  relax(e, r, n);
+  incr(phi, e, 1.0);
 }
 
 void VariableCoeffPoissonOperator::relaxFromZero(LevelData &e, const LevelData &r, int n) {
@@ -648,7 +661,7 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
   MGIC_HIP(hipStreamSynchronize(levels_[0].op->stream()));
 }
 
-void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero) {
+void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc) {
   VariableCoeffPoissonOperator &op = *levels_[d].op;
   const hipStream_t st = op.stream();
   if (d == (int)levels_.size() - 1) {  // bottom
@@ -660,6 +673,7 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero) {
     } else {
       op.relax(e, r, prm.n_bottom);
     }
+    if (phi_acc) op.incr(*phi_acc, e, 1.0);
     return;
   }
   if (e_zero)
@@ -674,14 +688,17 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero) {
     N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
   }
   // coarse correction e_c = 0 (folded into its first sweep when possible)
-  for (int c = 0; c < prm.cycles; ++c) cycle(d + 1, *N.e, *N.r, c == 0);
+  for (int c = 0; c < prm.cycles; ++c) cycle(d + 1, *N.e, *N.r, c == 0, nullptr);
   if (!N.agg) {
     op.prolongIncrement(e, *N.e);
   } else {
     N.prolong_plan->execute(*op.grid->comm, N.e->d_tab, N.e_stage->d_tab, st);
     op.prolongIncrementFilled(e, *N.e_stage);
   }
-  op.relax(e, r, prm.n_post);
+  if (phi_acc)  // phi += e folded into the last post-smoothing sweep
+    op.relaxAccumulate(e, r, prm.n_post, *phi_acc);
+  else
+    op.relax(e, r, prm.n_post);
 }
 
 // --------------------------------------------------------------- AMRMultiGrid
@@ -693,8 +710,7 @@ void AMRMultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MG
 double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &resid,
                                int normType, bool homogeneous) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
-  mg.oneCycleFromZero(*corr_, resid);  // e = 0; oneCycle(e, r)
-  op0.incr(phi, *corr_, 1.0);
+  mg.oneCycleFromZeroInto(*corr_, resid, phi);  // e = 0; oneCycle(e, r); phi += e
   op0.residual(resid, phi, rhs, homogeneous);
   return normType >= 0 ? op0.norm(resid, normType) : -1.0;
 }

@@ -109,7 +109,11 @@ class VariableCoeffPoissonOperator {
   // dpsi and the scratch buffer; the result always ends in dpsi).
   // zero_in: dpsi is taken as identically zero and not read (its memory
   // need not be zeroed).
-  void fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false);
+  void fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false,
+                  LevelData *acc = nullptr);
+  // relax(e, r, n); phi += e -- the increment folded into the last fused
+  // sweep (e is left as scratch in that case)
+  void relaxAccumulate(LevelData &e, const LevelData &r, int n, LevelData &phi);
   // e = 0; relax(e, r, n) -- without zeroing e in memory when the fused
   // smoother applies (the first sweep does not read its input)
   void relaxFromZero(LevelData &e, const LevelData &r, int n);
@@ -183,11 +187,15 @@ class MultiGrid {
  public:
   void define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &prm);
   void oneCycle(LevelData &e, const LevelData &r) {
-    cycle(0, e, const_cast<LevelData &>(r), false);
+    cycle(0, e, const_cast<LevelData &>(r), false, nullptr);
   }
   // e = 0; oneCycle(e, r)
   void oneCycleFromZero(LevelData &e, const LevelData &r) {
-    cycle(0, e, const_cast<LevelData &>(r), true);
+    cycle(0, e, const_cast<LevelData &>(r), true, nullptr);
+  }
+  // e = 0; oneCycle(e, r); phi += e (e is scratch afterwards)
+  void oneCycleFromZeroInto(LevelData &e, const LevelData &r, LevelData &phi) {
+    cycle(0, e, const_cast<LevelData &>(r), true, &phi);
   }
   int depths() const { return (int)levels_.size(); }
   VariableCoeffPoissonOperator &op(int d) { return *levels_[d].op; }
@@ -205,8 +213,9 @@ class MultiGrid {
     std::unique_ptr<LevelData> r_stage, e_stage;  // previous layout coarsened
     std::unique_ptr<CopyPlan> restrict_plan, prolong_plan;
   };
-  // e_zero: treat e as zero on entry (it is zeroed or never read)
-  void cycle(int d, LevelData &e, LevelData &r, bool e_zero);
+  // e_zero: treat e as zero on entry (it is zeroed or never read);
+  // phi_acc: phi += e at the end (at depth 0 folded into the last sweep)
+  void cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc);
   std::vector<Level> levels_;
 };
 

@@ -70,9 +70,10 @@ struct Fused6 {
 
 // One tile (x0, y0) of the box, planes [z0, z1): R/B are the 5-plane LDS
 // rings (5 * CP doubles each) holding the red / black element of each pair.
-template <int TX, int TY, int NT, bool ZIN, bool BC>
+template <int TX, int TY, int NT, bool ZIN, bool BC, bool ACC>
 __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *__restrict__ B,
                                                double *__restrict__ uo,
+                                               double *__restrict__ acc,
                                                const double *__restrict__ ui,
                                                const double *__restrict__ rhs,
                                                const double *__restrict__ a,
@@ -129,6 +130,7 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   double cr0[NP], cr1[NP], ca0[NP], ca1[NP], cb0[NP], cb1[NP];
   double nr0[NP], nr1[NP], na0[NP], na1[NP], nb0[NP], nb1[NP];
   double kr[NP], ka[NP], kb[NP];
+  double an0[NP], an1[NP], ak0[NP], ak1[NP];  // ACC: acc pairs of planes p and p-1
 
   auto fetch_u = [&](int p) {
     const long pz = (long)clampi(p, -2, nz + 1) * sz;
@@ -169,6 +171,15 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
       nb0[i] = vb.x; nb1[i] = vb.y;
     }
   };
+  auto fetch_acc = [&](int p) {  // the sum field, one step ahead of its store
+    const long pz = (long)clampi(p, 0, nz - 1) * sz;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const double2 v = *reinterpret_cast<const double2 *>(acc + rcoff[i] + pz);
+      an0[i] = v.x;
+      an1[i] = v.y;
+    }
+  };
   auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
                  double rv, double av, double bv) -> double {
     const double tx = (xp + xm) - 2.0 * uc;
@@ -194,10 +205,19 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
     ca0[i] = na0[i]; ca1[i] = na1[i];
     cb0[i] = nb0[i]; cb1[i] = nb1[i];
   }
+  if (ACC) fetch_acc(z0 - 1);
   for (int p = z0 - 1; p <= z1; ++p) {
     put_u(p + 1);
     fetch_u(p + 2);
     fetch_c(p + 1);
+    if (ACC) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        ak0[i] = an0[i];
+        ak1[i] = an1[i];
+      }
+      fetch_acc(p);
+    }
     __syncthreads();
     if (p >= rzlo && p <= rzhi) {  // RED cells of plane p on the ring
       double *Rs = R + slot(p) * CP;
@@ -237,13 +257,23 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
           const double xp = qb ? Rs[ci + 1] : Rs[ci];
           blk = upd(blk, xm, xp, Rs[ci - PW], Rs[ci + PW], Rm[ci], Rp[ci], kr[i], ka[i], kb[i]);
         }
-        if (rgx0[i] + 1 < nx) {
-          double2 w;
-          w.x = bsel(qb, red, blk);
-          w.y = bsel(qb, blk, red);
+        double2 w;
+        w.x = bsel(qb, red, blk);
+        w.y = bsel(qb, blk, red);
+        if (ACC) {  // acc += the swept value (incr, scale 1), u_out not written
+          double *ad = acc + (long)k * sz + roff[i];
+          if (rgx0[i] + 1 < nx) {
+            double2 t;
+            t.x = ak0[i] + w.x;
+            t.y = ak1[i] + w.y;
+            *reinterpret_cast<double2 *>(ad) = t;
+          } else {
+            ad[0] = ak0[i] + w.x;
+          }
+        } else if (rgx0[i] + 1 < nx) {
           *reinterpret_cast<double2 *>(dst + roff[i]) = w;
         } else {
-          dst[roff[i]] = bsel(qb, red, blk);
+          dst[roff[i]] = w.x;
         }
       }
     }
@@ -260,8 +290,9 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   }
 }
 
-template <int TX, int TY, int NT, bool ZIN, bool BC>
+template <int TX, int TY, int NT, bool ZIN, bool BC, bool ACC>
 __global__ __launch_bounds__(NT) void k_gsrb_fused6(double *__restrict__ uo,
+                                                    double *__restrict__ acc,
                                                     const double *__restrict__ ui,
                                                     const double *__restrict__ rhs,
                                                     const double *__restrict__ a,
@@ -277,8 +308,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused6(double *__restrict__ uo,
   const int L = xcd * q8 + min(xcd, r8) + i8;
   const int tx_ = L % ntx, ty_ = (L / ntx) % nty, tz_ = L / (ntx * nty);
   const int z0 = tz_ * kc;
-  fused6_segment<TX, TY, NT, ZIN, BC>(R, B, uo, ui, rhs, a, b, g, s, tx_ * TX, ty_ * TY, z0,
-                                      min(z0 + kc, g.nz));
+  fused6_segment<TX, TY, NT, ZIN, BC, ACC>(R, B, uo, acc, ui, rhs, a, b, g, s, tx_ * TX,
+                                           ty_ * TY, z0, min(z0 + kc, g.nz));
 }
 
 // ---- two sweeps per launch (temporal blocking) ---------------------------
@@ -627,7 +658,7 @@ static int choose_kc(int tiles, int nz, int slots, int overlap) {
 template <int TX, int TY, int NT>
 static void launch_fused6(double *u_out, double *u_in, const double *rhs, const double *a,
                           const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                          hipStream_t st) {
+                          double *acc, hipStream_t st) {
   if (!zero_in) {  // BC image of every face into the input's ghost layer
     const int m = (g.nx > g.ny ? g.nx : g.ny) + 2;
     const int m1 = (g.ny > g.nz ? g.ny : g.nz) + 2;
@@ -635,7 +666,7 @@ static void launch_fused6(double *u_out, double *u_in, const double *rhs, const 
                                                                                             g);
   }
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
-  static const int slots = resident_slots(k_gsrb_fused6<TX, TY, NT, false, false>, NT);
+  static const int slots = resident_slots(k_gsrb_fused6<TX, TY, NT, false, false, false>, NT);
   static const int kc_mode = [] {
     const char *e = getenv("MGIC_KC_MODE");
     return e ? atoi(e) : 0;
@@ -651,18 +682,21 @@ static void launch_fused6(double *u_out, double *u_in, const double *rhs, const 
   const int ntz = (g.nz + kc - 1) / kc;
   const int nblocks = ntx * nty * ntz;
   const dim3 grid((unsigned)nblocks), block(NT);
-  if (zero_in && s.bconst)
-    k_gsrb_fused6<TX, TY, NT, true, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s, kc,
-                                                                  ntx, nty, nblocks);
-  else if (zero_in)
-    k_gsrb_fused6<TX, TY, NT, true, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
-                                                                   kc, ntx, nty, nblocks);
-  else if (s.bconst)
-    k_gsrb_fused6<TX, TY, NT, false, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
-                                                                   kc, ntx, nty, nblocks);
-  else
-    k_gsrb_fused6<TX, TY, NT, false, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
-                                                                    kc, ntx, nty, nblocks);
+#define MGIC_F6(Z, B, A)                                                                     \
+  k_gsrb_fused6<TX, TY, NT, Z, B, A><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, b, g, s, \
+                                                             kc, ntx, nty, nblocks)
+  if (acc) {  // last sweep of a V-cycle at depth 0: phi += e in the same pass
+    if (zero_in) throw Error(kBadArg, "fused sweep: accumulate on a zero input");
+    if (s.bconst) MGIC_F6(false, true, true);
+    else MGIC_F6(false, false, true);
+  } else if (zero_in) {
+    if (s.bconst) MGIC_F6(true, true, false);
+    else MGIC_F6(true, false, false);
+  } else {
+    if (s.bconst) MGIC_F6(false, true, false);
+    else MGIC_F6(false, false, false);
+  }
+#undef MGIC_F6
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw Error(kHipErr, std::string("fused sweep launch: ") + hipGetErrorString(e));
 }
@@ -710,8 +744,10 @@ void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, co
   }
 }
 
-// tile shape, for measurement (MGIC_FUSED_VARIANT): 0 = 60x8 / 256 threads
-// (default), 1 = 124x16 / 512, 2 = 60x32 / 1024
+// tile shape, for measurement (MGIC_FUSED_VARIANT): 0 = 128x16 / 512 threads
+// (default: one 106 KB workgroup per CU, 1 KB contiguous rows, u halo 1.29x,
+// coefficient ring 1.16x), 1 = 60x8 / 256 (4 workgroups per CU), 2 = 256x8 / 512.
+// 512^3 sweep: 0.89 / 1.05 / 0.90 ms; 256^3: 0.142 / 0.168 / 0.145 ms.
 static int fused_variant() {
   static int v = [] {
     const char *e = getenv("MGIC_FUSED_VARIANT");
@@ -722,11 +758,11 @@ static int fused_variant() {
 
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                      hipStream_t st) {
+                      double *acc, hipStream_t st) {
   switch (fused_variant()) {
-    case 1: launch_fused6<124, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 2: launch_fused6<60, 32, 1024>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    default: launch_fused6<60, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 1: launch_fused6<60, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
+    case 2: launch_fused6<256, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
+    default: launch_fused6<128, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
   }
 }
 
