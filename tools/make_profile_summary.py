@@ -35,11 +35,21 @@ def short(name):
 
 
 def counters(path):
-    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    """(kernel, grid) -> counter -> per-dispatch values, keeping only the
+    longest-running cluster of dispatches (the finest MG level: the same
+    kernel and grid can serve several levels)."""
+    per = collections.defaultdict(list)
     for f in glob.glob(path):
         for r in csv.DictReader(open(f)):
-            vals[(short(r["Kernel_Name"]), int(r["Grid_Size"]))][r["Counter_Name"]].append(
-                float(r["Counter_Value"]))
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            per[(short(r["Kernel_Name"]), int(r["Grid_Size"]))].append(
+                (dur, r["Counter_Name"], float(r["Counter_Value"])))
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for k, rows in per.items():
+        top = max(d for d, _, _ in rows)
+        for d, name, v in rows:
+            if d >= top / 1.8:
+                vals[k][name].append(v)
     return vals
 
 

@@ -14,10 +14,30 @@ def summarise(path):
         name = m.group(1) if m else r["Kernel_Name"][:40]
         g = (r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"])
         agg[(name, g)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    # one (kernel, grid) can serve several MG levels (the streaming sweep
+    # launches one workgroup per CU slot at every level): split by duration
+    rows = []
+    for k, v in agg.items():
+        for c in clusters(v):
+            rows.append((k, c))
     out = []
-    for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+    for k, v in sorted(rows, key=lambda kv: -sum(kv[1])):
         out.append(f"{k[0]:28s} grid={'x'.join(k[1]):18s} n={len(v):4d} "
                    f"avg={sum(v) / len(v) / 1e3:9.1f}us total={sum(v) / 1e6:8.2f}ms")
+    return out
+
+
+def clusters(durations, gap=1.8):
+    """Split durations into groups separated by a jump of more than `gap`x."""
+    v = sorted(durations)
+    out, cur = [], [v[0]]
+    for d in v[1:]:
+        if d > gap * cur[-1]:
+            out.append(cur)
+            cur = [d]
+        else:
+            cur.append(d)
+    out.append(cur)
     return out
 
 
