@@ -53,8 +53,13 @@ __device__ __forceinline__ double ghost_of(int mode, double c, double near) {
 // register arrays is otherwise turned into a select of two stack addresses
 // and lowered to scratch memory.  Exact (no arithmetic on the values).
 __device__ __forceinline__ double bsel(int q, double x, double y) {
-  const long long m = -(long long)(q & 1);
-  return __longlong_as_double((__double_as_longlong(x) & m) | (__double_as_longlong(y) & ~m));
+  // per 32-bit half, so each half is one v_bitop3 / v_bfi
+  const unsigned m = 0u - (unsigned)(q & 1);
+  const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
+  const unsigned long long yb = (unsigned long long)__double_as_longlong(y);
+  const unsigned lo = ((unsigned)xb & m) | ((unsigned)yb & ~m);
+  const unsigned hi = ((unsigned)(xb >> 32) & m) | ((unsigned)(yb >> 32) & ~m);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 template <int TX, int TY, int NT>
