@@ -7,6 +7,8 @@
 // wavefronts along x so every wave touches whole 128-byte lines.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace mgic {
@@ -105,6 +107,49 @@ __global__ __launch_bounds__(256) void k_residual(double *__restrict__ r,
   double ldpsi = lap7(u, idx, uc, i, j, k, g);                   // .ChF:320-329
   ldpsi = ldpsi * s.dxinv * s.beta * (BC ? s.bval : b[idx]);     // .ChF:331
   r[idx] = res + ldpsi;                                          // .ChF:333
+}
+
+// z-streaming residual: a thread owns one (i, j) column of a z chunk and
+// carries u(k-1), u(k) in registers; u(k+1) is the only new u load per cell
+// (the x/y neighbours come from L1/L2, loaded as centres by the neighbours).
+// Same expressions as k_residual.
+template <bool BC>
+__global__ __launch_bounds__(256) void k_residual_z(double *__restrict__ r,
+                                                    const double *__restrict__ u,
+                                                    const double *__restrict__ rhs,
+                                                    const double *__restrict__ a,
+                                                    const double *__restrict__ b, const BoxArgs g,
+                                                    const StencilCoefs s, int kc) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, g.nz);
+  if (i >= g.nx || j >= g.ny) return;
+  const long col = (long)i + (long)j * g.sy;
+  const bool fx0 = i == 0 && g.bcm[0], fx1 = i == g.nx - 1 && g.bcm[1];
+  const bool fy0 = j == 0 && g.bcm[2], fy1 = j == g.ny - 1 && g.bcm[3];
+  double um = u[col + (long)(k0 - 1) * g.sz];  // ghost plane -1 is allocated
+  double uc = u[col + (long)k0 * g.sz];
+  for (int k = k0; k < k1; ++k) {
+    const long idx = col + (long)k * g.sz;
+    const double up = u[idx + g.sz];  // plane nz (ghost) when k = nz - 1
+    double xm = u[idx - 1], xp = u[idx + 1], ym = u[idx - g.sy], yp = u[idx + g.sy];
+    double zm = um, zp = up;
+    if (fx0) xm = ghost_of(g.bcm[0], g.bcc[0], uc);
+    if (fx1) xp = ghost_of(g.bcm[1], g.bcc[1], uc);
+    if (fy0) ym = ghost_of(g.bcm[2], g.bcc[2], uc);
+    if (fy1) yp = ghost_of(g.bcm[3], g.bcc[3], uc);
+    if (k == 0 && g.bcm[4]) zm = ghost_of(g.bcm[4], g.bcc[4], uc);
+    if (k == g.nz - 1 && g.bcm[5]) zp = ghost_of(g.bcm[5], g.bcc[5], uc);
+    const double res = rhs[idx] - s.alpha * a[idx] * uc;           // .ChF:314-316
+    const double tx = (xp + xm) - 2.0 * uc;
+    const double ty = (yp + ym) - 2.0 * uc;
+    const double tz = (zp + zm) - 2.0 * uc;
+    double ldpsi = (tx + ty) + tz;                                  // .ChF:320-329
+    ldpsi = ldpsi * s.dxinv * s.beta * (BC ? s.bval : b[idx]);     // .ChF:331
+    r[idx] = res + ldpsi;                                           // .ChF:333
+    um = uc;
+    uc = up;
+  }
 }
 
 // One thread per coarse cell; the 8 fine children are visited in the
@@ -517,10 +562,21 @@ void apply_op(double *lu, const double *u, const double *a, const double *b, con
 void residual(double *r, const double *u, const double *rhs, const double *a, const double *b,
               const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  if (s.bconst)
+  static const int mode = [] {
+    const char *e = getenv("MGIC_RESIDUAL_KC");
+    return e ? atoi(e) : 16;
+  }();
+  if (mode > 0) {  // z-streaming, chunks of `mode` planes
+    const int kc = mode < g.nz ? mode : g.nz;
+    dim3 grid = grid_cells(g.nx, g.ny, g.nz);
+    grid.z = (unsigned)((g.nz + kc - 1) / kc);
+    if (s.bconst) k_residual_z<true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+    else k_residual_z<false><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  } else if (s.bconst) {
     k_residual<true><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
-  else
+  } else {
     k_residual<false><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
+  }
   check_launch();
 }
 

@@ -711,8 +711,8 @@ static void launch_fused2x(double *u_out, const double *u_in, const double *rhs,
                            const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                            hipStream_t st) {
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
-  int kc = g.nz;
-  while (kc > 32 && (long)ntx * nty * ((g.nz + kc - 1) / kc) < 2048) kc = (kc + 1) / 2;
+  static const int slots = resident_slots(k_gsrb_fused2x<TX, TY, NT, false, false>, NT);
+  const int kc = choose_kc(ntx * nty, g.nz, slots, 7);
   const int ntz = (g.nz + kc - 1) / kc;
   const int nblocks = ntx * nty * ntz;
   const dim3 grid((unsigned)nblocks), block(NT);
@@ -745,6 +745,9 @@ void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, co
                         hipStream_t st) {
   switch (fused2x_variant()) {
     case 1: launch_fused2x<56, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 2: launch_fused2x<120, 12, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 3: launch_fused2x<128, 12, 768>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
+    case 4: launch_fused2x<120, 12, 1024>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
     default: launch_fused2x<56, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
   }
 }
