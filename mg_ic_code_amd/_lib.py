@@ -165,6 +165,8 @@ SIGNATURES = {
     "vccomputeop3d_": None,
     "vccomputeres3d_": None,
     "restrictresvc3d_": None,
+    "getlaplacianpsif_": None,
+    "getrhogradphif_": None,
 }
 
 _RESTYPE = {
@@ -177,6 +179,8 @@ _RESTYPE = {
     "vccomputeop3d_": None,
     "vccomputeres3d_": None,
     "restrictresvc3d_": None,
+    "getlaplacianpsif_": None,
+    "getrhogradphif_": None,
 }
 
 

@@ -265,4 +265,41 @@ void restrictresvc3d_(MGIC_CHF_FRA(res), MGIC_CHF_CONST_FRA(dpsi), MGIC_CHF_CONS
   });
 }
 
+static void fra1_unary(const char *name, double *out, const int *ol0, const int *ol1,
+                       const int *ol2, const int *oh0, const int *oh1, const int *oh2,
+                       const double *in, const int *il0, const int *il1, const int *il2,
+                       const int *ih0, const int *ih1, const int *ih2, const double *dx,
+                       const int *b0, const int *b1, const int *b2, const int *e0, const int *e1,
+                       const int *e2, bool laplacian) {
+  run(name, [&] {
+    const int one = 1;
+    HostFab fo = fab(out, ol0, ol1, ol2, oh0, oh1, oh2, &one);
+    HostFab fi = fab(in, il0, il1, il2, ih0, ih1, ih2, &one);
+    const int lohi[6] = {*b0, *b1, *b2, *e0, *e1, *e2};
+    const Box R = Box::make(lohi);
+    if (R.empty()) return;
+    if (!fi.box.contains(grow1(R))) mayday("operand must cover the box grown by one");
+    Stage so(R), si(R);
+    transfer(si, fi, 0, grow1(R), true);
+    if (laplacian) kern::lap_psi(so.p, si.p, si.args(), *dx, 0);
+    else kern::rho_grad_phi(so.p, si.p, si.args(), *dx, 0);
+    MGIC_HIP(hipDeviceSynchronize());
+    transfer(so, fo, 0, R, false);
+  });
+}
+
+void getlaplacianpsif_(MGIC_CHF_FRA1(l_of_psi), MGIC_CHF_CONST_FRA1(psi), const double *dx,
+                       MGIC_CHF_BOX(box)) {
+  fra1_unary("getlaplacianpsif_", l_of_psi, l_of_psilo0, l_of_psilo1, l_of_psilo2, l_of_psihi0,
+             l_of_psihi1, l_of_psihi2, psi, psilo0, psilo1, psilo2, psihi0, psihi1, psihi2, dx,
+             boxlo0, boxlo1, boxlo2, boxhi0, boxhi1, boxhi2, true);
+}
+
+void getrhogradphif_(MGIC_CHF_FRA1(rho_grad_phi), MGIC_CHF_CONST_FRA1(phi), const double *dx,
+                     MGIC_CHF_BOX(box)) {
+  fra1_unary("getrhogradphif_", rho_grad_phi, rho_grad_philo0, rho_grad_philo1, rho_grad_philo2,
+             rho_grad_phihi0, rho_grad_phihi1, rho_grad_phihi2, phi, philo0, philo1, philo2,
+             phihi0, phihi1, phihi2, dx, boxlo0, boxlo1, boxlo2, boxhi0, boxhi1, boxhi2, false);
+}
+
 }  // extern "C"

@@ -523,6 +523,44 @@ __global__ __launch_bounds__(256) void k_binary_bh(double *__restrict__ acoef,
              2.0 * M_PI * p.G_Newton * rho_grad * psi_0 - lap;  // SetLevelData.cpp:121-124
 }
 
+// GETLAPLACIANPSIF (SetLevelDataF.ChF:15-58), 2nd-order branch, and
+// GETRHOGRADPHIF (:65-103): undivided-difference loops over `box` with the
+// operand's ghost layer read as is (no BC)
+__global__ __launch_bounds__(256) void k_lap_psi(double *__restrict__ l,
+                                                 const double *__restrict__ psi, const BoxArgs g,
+                                                 double dx) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  const long st[3] = {1, g.sy, g.sz};
+  double acc = 0.0;
+  for (int d0 = 0; d0 < 3; ++d0) {
+    const double d2 = 1.0 / dx / dx * (+1.0 * psi[idx - st[d0]] - 2.0 * psi[idx] +
+                                       1.0 * psi[idx + st[d0]]);
+    acc = acc + d2;
+  }
+  l[idx] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_rho_grad_phi(double *__restrict__ r,
+                                                      const double *__restrict__ phi,
+                                                      const BoxArgs g, double dx) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  const long st[3] = {1, g.sy, g.sz};
+  double acc = 0.0;
+  for (int d0 = 0; d0 < 3; ++d0) {
+    const double dphidx = 0.5 / dx * (+phi[idx + st[d0]] - phi[idx - st[d0]]);
+    acc = acc + 0.5 * dphidx * dphidx;
+  }
+  r[idx] = acc;
+}
+
 inline dim3 grid_cells(int nx, int ny, int nz) {
   return dim3((unsigned)((nx + TX - 1) / TX), (unsigned)((ny + TY - 1) / TY), (unsigned)nz);
 }
@@ -699,6 +737,18 @@ void binary_bh_coefs(double *acoef, double *rhs, const double *psi, const BoxArg
                      const BhParams &p, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
   k_binary_bh<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(acoef, rhs, psi, g, dx, p);
+  check_launch();
+}
+
+void lap_psi(double *l, const double *psi, const BoxArgs &g, double dx, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_lap_psi<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(l, psi, g, dx);
+  check_launch();
+}
+
+void rho_grad_phi(double *r, const double *phi, const BoxArgs &g, double dx, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_rho_grad_phi<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, phi, g, dx);
   check_launch();
 }
 

@@ -82,6 +82,9 @@ struct BhParams {
 // psi: nullptr = psi 1 everywhere, else read with its ghost layer
 void binary_bh_coefs(double *acoef, double *rhs, const double *psi, const BoxArgs &g, double dx,
                      const BhParams &p, hipStream_t st);
+// GETLAPLACIANPSIF / GETRHOGRADPHIF (SetLevelDataF.ChF), operand ghosts as is
+void lap_psi(double *l, const double *psi, const BoxArgs &g, double dx, hipStream_t st);
+void rho_grad_phi(double *r, const double *phi, const BoxArgs &g, double dx, hipStream_t st);
 // x += y over the valid box grown by `grow` (<= kGhost) cells
 void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStream_t st);
 

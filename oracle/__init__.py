@@ -98,6 +98,7 @@ _sig = {
     "orc_binary_bh_coefs": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double), POINTER(c_double)],
     "orc_nl_coefs": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double), POINTER(c_double),
                      POINTER(c_double)],
+    "orc_getlaplacianpsif": [POINTER(c_double), POINTER(c_double), PI, PI, c_double, c_int],
     "orc_set_threads": [c_int],
     "orc_get_threads": [],
 }
@@ -196,6 +197,24 @@ def nl_coefs(bh: dict, lo, hi, dx, psi=None):
         assert g.shape == tuple(n + 2 for n in shape)
         _lib.orc_nl_coefs(ctypes.byref(p), _i3(lo), _i3(hi), dx, _dp(g), _dp(a), _dp(r))
     return a, r
+
+
+def getlaplacianpsif(psi_g, lo, hi, dx):
+    """GETLAPLACIANPSIF over [lo, hi]; psi_g over the box grown by one."""
+    return _fd(psi_g, lo, hi, dx, 1)
+
+
+def getrhogradphif(phi_g, lo, hi, dx):
+    """GETRHOGRADPHIF over [lo, hi]; phi_g over the box grown by one."""
+    return _fd(phi_g, lo, hi, dx, 0)
+
+
+def _fd(g, lo, hi, dx, lap):
+    g = np.ascontiguousarray(g, dtype=np.float64)
+    out = np.empty((hi[2] - lo[2] + 1, hi[1] - lo[1] + 1, hi[0] - lo[0] + 1))
+    assert g.shape == tuple(n + 2 for n in out.shape)
+    _lib.orc_getlaplacianpsif(_dp(out), _dp(g), _i3(lo), _i3(hi), float(dx), int(lap))
+    return out
 
 
 def set_threads(n: int) -> None:

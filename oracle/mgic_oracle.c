@@ -926,6 +926,32 @@ void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double d
       }
 }
 
+/* GETLAPLACIANPSIF / GETRHOGRADPHIF (SetLevelDataF.ChF:15-58, :65-103) on
+ * [lo, hi]; `in` over the box grown by one, `out` over the box, i fastest */
+void orc_getlaplacianpsif(double *out, const double *in, const int *lo, const int *hi, double dx,
+                          int laplacian) {
+  const size_t nx = (size_t)(hi[0] - lo[0] + 1), ny = (size_t)(hi[1] - lo[1] + 1);
+  const size_t gx = nx + 2, gy = ny + 2, gs[3] = {1, gx, gx * gy};
+  for (int k = lo[2]; k <= hi[2]; ++k)
+    for (int j = lo[1]; j <= hi[1]; ++j)
+      for (int i = lo[0]; i <= hi[0]; ++i) {
+        const size_t c = (size_t)(i - lo[0] + 1) + gx * ((size_t)(j - lo[1] + 1) +
+                                                          gy * (size_t)(k - lo[2] + 1));
+        double acc = 0.0;
+        for (int d0 = 0; d0 < 3; ++d0) {
+          if (laplacian) {
+            const double d2 =
+                1.0 / dx / dx * (+1.0 * in[c - gs[d0]] - 2.0 * in[c] + 1.0 * in[c + gs[d0]]);
+            acc = acc + d2;
+          } else {
+            const double dphidx = 0.5 / dx * (+in[c + gs[d0]] - in[c - gs[d0]]);
+            acc = acc + 0.5 * dphidx * dphidx;
+          }
+        }
+        out[(size_t)(i - lo[0]) + nx * ((size_t)(j - lo[1]) + ny * (size_t)(k - lo[2]))] = acc;
+      }
+}
+
 /* aCoef / rhs at psi = 1 (NL iteration 0) */
 void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
                          double *acoef, double *rhs) {

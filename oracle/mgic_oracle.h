@@ -174,6 +174,11 @@ void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi,
 void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
                   const double *psi, double *acoef, double *rhs);
 
+/* GETLAPLACIANPSIF (laplacian = 1) / GETRHOGRADPHIF (laplacian = 0) over
+ * [lo, hi]; `in` over the box grown by one */
+void orc_getlaplacianpsif(double *out, const double *in, const int *lo, const int *hi, double dx,
+                          int laplacian);
+
 void orc_set_threads(int n);
 int orc_get_threads(void);
 

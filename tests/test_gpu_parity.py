@@ -446,3 +446,21 @@ def test_nonlinear_poisson_solve_matches_oracle(comm):
     g = res.psi.download(0, with_ghosts=True)[1:-1, 1:-1, 1:-1]
     c = psi_o[1:-1, 1:-1, 1:-1]
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
+
+
+def test_chf_dropin_setleveldata_bitwise(rng):
+    # GETLAPLACIANPSIF / GETRHOGRADPHIF (SetLevelDataF_F.H:15-19, :43-47) on
+    # host FAB components: FRA1 operands with the box grown by one
+    lo = (3, -2, 5)
+    n = (17, 12, 9)
+    hi = tuple(lo[d] + n[d] - 1 for d in range(3))
+    g1 = tuple(l - 1 for l in lo)
+    src = rng.uniform(0.5, 1.5, (n[2] + 2, n[1] + 2, n[0] + 2))
+    dx = 100.0 / 64
+    for name, fn in (("getlaplacianpsif_", oracle.getlaplacianpsif),
+                     ("getrhogradphif_", oracle.getrhogradphif)):
+        out = np.zeros(n[::-1])
+        args = [dbl(out)] + ints(*lo) + ints(*hi) + [dbl(src)] + ints(*g1) + \
+            ints(*(h + 1 for h in hi)) + [ctypes.byref(ctypes.c_double(dx))] + ints(*lo) + ints(*hi)
+        getattr(mg.lib, name)(*args)
+        assert np.array_equal(out, fn(src, lo, hi, dx)), name
