@@ -150,6 +150,9 @@ MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double
  * psi = NULL is psi = 1 (NL iteration 0) */
 MGIC_API int mgic_field_nl_coefs(mgic_field psi, mgic_field acoef, mgic_field rhs,
                                  const double bh[13]);
+/* set_constant_K_integrand (SetLevelData.cpp:131-180) at psi (NULL: 1):
+ * the integrand of the periodic integrability condition for K */
+MGIC_API int mgic_field_nl_integrand(mgic_field psi, mgic_field out, const double bh[13]);
 /* every cell of the allocation, ghosts included (set_initial_conditions
  * sets psi over the whole FAB, SetLevelData.cpp:31-72) */
 MGIC_API int mgic_field_set_val_all(mgic_field f, double v);

@@ -99,6 +99,7 @@ SIGNATURES = {
     "mgic_grid_local_box": [H, c_int, PI, PI],
     "mgic_grid_coarsen": [H, c_int, PH],
     "mgic_field_nl_coefs": [H, H, H, PD],
+    "mgic_field_nl_integrand": [H, H, PD],
     "mgic_field_set_val_all": [H, c_double],
     "mgic_op_update_psi": [H, H, H],
     "mgic_plan_create": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PI, PI, c_int, c_int, PH],

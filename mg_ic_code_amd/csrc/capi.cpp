@@ -530,6 +530,18 @@ MGIC_API int mgic_field_nl_coefs(mgic_field psi, mgic_field acoef, mgic_field rh
                             g.box_args_plain(n), g.dx, p, g.comm->stream());
   });
 }
+MGIC_API int mgic_field_nl_integrand(mgic_field psi, mgic_field out, const double bh[13]) {
+  return guard([&] {
+    NEED(out);
+    NEED(bh);
+    const Grid &g = *out->f->grid;
+    if (psi) check_same_layout(g, *psi->f, "psi");
+    const kern::BhParams p = bh_params(bh);
+    for (int n = 0; n < g.nlocal(); ++n)
+      kern::constant_k_integrand(out->f->p[n], psi ? psi->f->p[n] : nullptr, g.box_args_plain(n),
+                                 g.dx, p, g.comm->stream());
+  });
+}
 MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]) {
   return mgic_field_nl_coefs(nullptr, acoef, rhs, bh);
 }

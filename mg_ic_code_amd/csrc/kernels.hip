@@ -469,6 +469,9 @@ __device__ double bh_Aij(int i, int j, double r1, double r2, const double *n1, c
 
 // set_a_coef + set_rhs (SetLevelData.cpp:73-127, :281-325); psi == nullptr:
 // psi = 1 everywhere (NL iteration 0), else psi read with its ghost layer
+// INTEGRAND: set_constant_K_integrand (SetLevelData.cpp:131-180) into acoef
+// instead (m taken at K = 0, rhs untouched)
+template <bool INTEGRAND>
 __global__ __launch_bounds__(256) void k_binary_bh(double *__restrict__ acoef,
                                                    double *__restrict__ rhs,
                                                    const double *__restrict__ psi,
@@ -506,7 +509,8 @@ __global__ __launch_bounds__(256) void k_binary_bh(double *__restrict__ acoef,
   const double A2 = pow(A11, 2.0) + pow(A22, 2.0) + pow(A33, 2.0) + 2 * pow(A12, 2.0) +
                     2 * pow(A13, 2.0) + 2 * pow(A23, 2.0);  // SetLevelData.cpp:312-317
   const double rho = 0.5 * 0.0 * 0.0 + 0.0;
-  const double m = (2.0 / 3.0) * (p.constant_K * p.constant_K) - 16.0 * M_PI * p.G_Newton * rho;
+  const double K = INTEGRAND ? 0.0 : p.constant_K;  // set_m_value(.., 0.0) for the integrand
+  const double m = (2.0 / 3.0) * (K * K) - 16.0 * M_PI * p.G_Newton * rho;
   const double psi_bh = p.m1 / r1 + p.m2 / r2;  // SetBinaryBH.H:85-99
   const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
   const double psi_c = psi ? psi[idx] : 1.0;
@@ -516,6 +520,12 @@ __global__ __launch_bounds__(256) void k_binary_bh(double *__restrict__ acoef,
   for (int d0 = 0; d0 < 3; ++d0) {
     const double pm = psi ? psi[idx - st[d0]] : 1.0, pp = psi ? psi[idx + st[d0]] : 1.0;
     lap = lap + 1.0 / dx / dx * (+1.0 * pm - 2.0 * psi_c + 1.0 * pp);
+  }
+  if (INTEGRAND) {  // SetLevelData.cpp:174-177
+    acoef[idx] = -1.5 * m + 1.5 * A2 * pow(psi_0, -12.0) +
+                 24.0 * M_PI * p.G_Newton * rho_grad * pow(psi_0, -4.0) +
+                 12.0 * lap * pow(psi_0, -5.0);
+    return;
   }
   acoef[idx] = -0.625 * m * pow(psi_0, 4.0) - A2 * pow(psi_0, -8.0) +
                2.0 * M_PI * p.G_Newton * rho_grad;  // SetLevelData.cpp:321-322
@@ -736,7 +746,14 @@ void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *con
 void binary_bh_coefs(double *acoef, double *rhs, const double *psi, const BoxArgs &g, double dx,
                      const BhParams &p, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  k_binary_bh<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(acoef, rhs, psi, g, dx, p);
+  k_binary_bh<false><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(acoef, rhs, psi, g, dx, p);
+  check_launch();
+}
+
+void constant_k_integrand(double *out, const double *psi, const BoxArgs &g, double dx,
+                          const BhParams &p, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_binary_bh<true><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(out, nullptr, psi, g, dx, p);
   check_launch();
 }
 

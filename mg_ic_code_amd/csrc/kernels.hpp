@@ -82,6 +82,9 @@ struct BhParams {
 // psi: nullptr = psi 1 everywhere, else read with its ghost layer
 void binary_bh_coefs(double *acoef, double *rhs, const double *psi, const BoxArgs &g, double dx,
                      const BhParams &p, hipStream_t st);
+// set_constant_K_integrand (SetLevelData.cpp:131-180) at psi (nullptr: 1)
+void constant_k_integrand(double *out, const double *psi, const BoxArgs &g, double dx,
+                          const BhParams &p, hipStream_t st);
 // GETLAPLACIANPSIF / GETRHOGRADPHIF (SetLevelDataF.ChF), operand ghosts as is
 void lap_psi(double *l, const double *psi, const BoxArgs &g, double dx, hipStream_t st);
 void rho_grad_phi(double *r, const double *phi, const BoxArgs &g, double dx, hipStream_t st);

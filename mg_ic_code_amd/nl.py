@@ -12,17 +12,23 @@ max_level = 0:
         psi += dpsi                       set_update_psi0 (:188-207)
         stop if |dpsi| < tolerance or > 1e5   computeNorm (:210-217)
 
-Every field stays in HBM, and each step is a libmgic kernel. Not covered:
-AMR levels (max_level > 0), the periodic constant-K integrability condition
-(:133-147), and the HDF5 output.
+On a periodic domain each NL iteration first sets K from the integrability
+condition: K = -sqrt(|sum(integrand) dV| / volume), with the integrand of
+set_constant_K_integrand (:133-147).  Every field stays in HBM, and each step
+is a libmgic kernel.  Not covered: AMR levels (max_level > 0) and the HDF5
+output.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
 from typing import List, Optional
 
+import ctypes
+import math
+
 from .core import (AMRMultiGrid, BiCGStabSolver, Grid, LevelData, MultilevelLinearOp,
-                   OperatorParams, SolverParams, defineOperatorFactory, set_nl_coefs)
+                   OperatorParams, SolverParams, defineOperatorFactory, set_nl_coefs, BH_KEYS)
+from ._lib import call
 from .params import PoissonParameters
 
 
@@ -33,14 +39,21 @@ class NLResult:
     dpsi_norms: List[float] = field(default_factory=list)
     linear_iterations: List[int] = field(default_factory=list)
     converged: bool = False
+    constant_K: List[float] = field(default_factory=list)
+
+
+def set_nl_integrand(psi: LevelData, out: LevelData, bh: dict) -> None:
+    """set_constant_K_integrand (SetLevelData.cpp:131-180) on device."""
+    vals = (ctypes.c_double * 13)(*[float(bh[k]) for k in BH_KEYS])
+    call("mgic_field_nl_integrand", psi.handle, out.handle, vals)
 
 
 def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
                   prolong_type: int = 1, bottom_solver: int = 1,
                   max_NL_iterations: Optional[int] = None) -> NLResult:
-    if any(prm.bc_lo[d] == 2 or prm.bc_hi[d] == 2 for d in range(3)) or prm.is_periodic:
-        raise NotImplementedError("periodic domains need the constant-K integrability step "
-                                  "(Main_PoissonSolver.cpp:133-147), not built yet")
+    periodic = bool(prm.is_periodic)
+    if periodic != all(grid.periodic):
+        raise ValueError("grid periodicity must match params is_periodic")
     psi, dpsi = LevelData(grid), LevelData(grid)
     a, b, rhs = LevelData(grid), LevelData(grid), LevelData(grid)
     psi.set_val_all(1.0)
@@ -56,7 +69,19 @@ def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
     res = NLResult(psi=psi, dpsi=dpsi)
     n_nl = prm.max_NL_iterations if max_NL_iterations is None else max_NL_iterations
     dx = grid.dx
+    ones = integrand = None
+    volume = prm.domainLength[0] * prm.domainLength[1] * prm.domainLength[2]
     for _ in range(n_nl):
+        if periodic:  # integrability condition for K (:133-147)
+            if integrand is None:
+                integrand, ones = LevelData(grid), LevelData(grid)
+                ones.set_val(1.0)
+            bh["constant_K"] = 0.0
+            set_nl_integrand(psi, integrand, bh)
+            tmp_op = defineOperatorFactory(grid, a, b, op_params).AMRnewOp()
+            integral = tmp_op.dotProduct(integrand, ones) * dx ** 3  # computeSum
+            bh["constant_K"] = -math.sqrt(abs(integral) / volume)
+            res.constant_K.append(bh["constant_K"])
         set_nl_coefs(psi, a, rhs, bh)  # :155-161
         fac = defineOperatorFactory(grid, a, b, op_params)
         amg = AMRMultiGrid(fac, SolverParams(max_depth=depth, n_pre=prm.numMGsmooth,

@@ -98,6 +98,8 @@ _sig = {
     "orc_binary_bh_coefs": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double), POINTER(c_double)],
     "orc_nl_coefs": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double), POINTER(c_double),
                      POINTER(c_double)],
+    "orc_nl_integrand": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double),
+                         POINTER(c_double)],
     "orc_getlaplacianpsif": [POINTER(c_double), POINTER(c_double), PI, PI, c_double, c_int],
     "orc_set_threads": [c_int],
     "orc_get_threads": [],
@@ -197,6 +199,16 @@ def nl_coefs(bh: dict, lo, hi, dx, psi=None):
         assert g.shape == tuple(n + 2 for n in shape)
         _lib.orc_nl_coefs(ctypes.byref(p), _i3(lo), _i3(hi), dx, _dp(g), _dp(a), _dp(r))
     return a, r
+
+
+def nl_integrand(bh: dict, lo, hi, dx, psi):
+    """set_constant_K_integrand at psi over [lo-1, hi+1]."""
+    p = _bh_params(bh)
+    g = np.ascontiguousarray(psi, dtype=np.float64)
+    out = np.empty((hi[2] - lo[2] + 1, hi[1] - lo[1] + 1, hi[0] - lo[0] + 1))
+    assert g.shape == tuple(n + 2 for n in out.shape)
+    _lib.orc_nl_integrand(ctypes.byref(p), _i3(lo), _i3(hi), dx, _dp(g), _dp(out))
+    return out
 
 
 def getlaplacianpsif(psi_g, lo, hi, dx):

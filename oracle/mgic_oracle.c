@@ -855,8 +855,8 @@ static double get_Aij(int i, int j, double r1, double r2, const double *n1, cons
   return Aij;
 }
 
-void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
-                  const double *psi, double *acoef, double *rhs) {
+static void nl_core(const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                    const double *psi, double *acoef, double *rhs, int integrand) {
   const double domlen[3] = {p->L, p->L, p->L};
   const size_t nx = (size_t)(hi[0] - lo[0] + 1), ny = (size_t)(hi[1] - lo[1] + 1);
 #pragma omp parallel for schedule(static)
@@ -897,8 +897,8 @@ void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double d
                           2 * pow(A13, 2.0) + 2 * pow(A23, 2.0);
         /* set_m_value, :266-278 (Pi = V = 0) */
         const double rho = 0.5 * 0.0 * 0.0 + 0.0;
-        const double m = (2.0 / 3.0) * (p->constant_K * p->constant_K) -
-                         16.0 * M_PI * p->G_Newton * rho;
+        const double K = integrand ? 0.0 : p->constant_K; /* :161 set_m_value(.., 0.0) */
+        const double m = (2.0 / 3.0) * (K * K) - 16.0 * M_PI * p->G_Newton * rho;
         /* set_binary_bh_psi, SetBinaryBH.H:85-99; psi = 1 (:54) */
         double b1[3] = {loc[0], loc[1], loc[2]}, b2[3] = {loc[0], loc[1], loc[2]};
         const double rb1 = bh_radius(b1, p->bh1_offset), rb2 = bh_radius(b2, p->bh2_offset);
@@ -917,6 +917,12 @@ void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double d
           lap = lap + 1.0 / dx / dx * (+1.0 * pm - 2.0 * psi_c + 1.0 * pp);
         }
         const size_t n = (size_t)(i - lo[0]) + nx * ((size_t)(j - lo[1]) + ny * (size_t)(k - lo[2]));
+        if (integrand) { /* set_constant_K_integrand, SetLevelData.cpp:174-177 */
+          acoef[n] = -1.5 * m + 1.5 * A2 * pow(psi_0, -12.0) +
+                     24.0 * M_PI * p->G_Newton * rho_grad * pow(psi_0, -4.0) +
+                     12.0 * lap * pow(psi_0, -5.0);
+          continue;
+        }
         /* set_a_coef, SetLevelData.cpp:321-322 */
         acoef[n] = -0.625 * m * pow(psi_0, 4.0) - A2 * pow(psi_0, -8.0) +
                    2.0 * M_PI * p->G_Newton * rho_grad;
@@ -950,6 +956,16 @@ void orc_getlaplacianpsif(double *out, const double *in, const int *lo, const in
         }
         out[(size_t)(i - lo[0]) + nx * ((size_t)(j - lo[1]) + ny * (size_t)(k - lo[2]))] = acc;
       }
+}
+
+void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                  const double *psi, double *acoef, double *rhs) {
+  nl_core(p, lo, hi, dx, psi, acoef, rhs, 0);
+}
+
+void orc_nl_integrand(const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                      const double *psi, double *out) {
+  nl_core(p, lo, hi, dx, psi, out, NULL, 1);
 }
 
 /* aCoef / rhs at psi = 1 (NL iteration 0) */

@@ -173,6 +173,9 @@ void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi,
  * psi given over the box grown by one (i fastest), constant_K from p */
 void orc_nl_coefs(const orc_bh_params *p, const int *lo, const int *hi, double dx,
                   const double *psi, double *acoef, double *rhs);
+/* set_constant_K_integrand (SetLevelData.cpp:131-180) at psi */
+void orc_nl_integrand(const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                      const double *psi, double *out);
 
 /* GETLAPLACIANPSIF (laplacian = 1) / GETRHOGRADPHIF (laplacian = 0) over
  * [lo, hi]; `in` over the box grown by one */

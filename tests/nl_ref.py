@@ -11,14 +11,22 @@ def oracle_poisson_solve(prm, n, max_depth, n_nl, bottom_solver=1):
     dx = prm.domainLength[0] / n
     bh = prm.bh(constant_K=0.0)
     avg = prm.coefficient_average_type if prm.coefficient_average_type >= 0 else 0
-    o = oracle.OracleMG([dom], dom, dx, alpha=prm.alpha, beta=prm.beta, bc_lo=prm.bc_lo,
+    per = (1, 1, 1) if prm.is_periodic else (0, 0, 0)
+    volume = prm.domainLength[0] * prm.domainLength[1] * prm.domainLength[2]
+    o = oracle.OracleMG([dom], dom, dx, alpha=prm.alpha, beta=prm.beta, periodic=per,
+                        bc_lo=prm.bc_lo,
                         bc_hi=prm.bc_hi, bc_value=prm.bc_value, nlevels=max_depth + 1,
                         avg_type=avg, prolong_type=1, bottom_solver=bottom_solver,
                         n_pre=prm.numMGsmooth, n_post=prm.numMGsmooth, n_bottom=prm.numMGsmooth)
     psi = np.ones((n + 2,) * 3)          # set_initial_conditions: psi = 1 incl. ghosts
     o.set(0, oracle.PHI, 0, np.zeros((n,) * 3))
-    norms, iters = [], []
+    norms, iters, ks = [], [], []
     for _ in range(n_nl):
+        if prm.is_periodic:  # integrability condition for K (Main_PoissonSolver.cpp:133-147)
+            bh["constant_K"] = 0.0
+            integ = oracle.nl_integrand(bh, (0, 0, 0), (n - 1,) * 3, dx, psi)
+            bh["constant_K"] = -np.sqrt(abs(np.sum(integ) * dx ** 3) / volume)
+            ks.append(bh["constant_K"])
         a, r = oracle.nl_coefs(bh, (0, 0, 0), (n - 1,) * 3, dx, psi)
         o.set(0, oracle.ACOEF, 0, a)
         o.set(0, oracle.BCOEF, 0, np.ones_like(a))
@@ -35,4 +43,4 @@ def oracle_poisson_solve(prm, n, max_depth, n_nl, bottom_solver=1):
         norms.append(nrm)
         if nrm < prm.tolerance or nrm > 1e5:
             break
-    return psi, norms, iters
+    return psi, norms, iters, ks

@@ -437,7 +437,7 @@ def test_nonlinear_poisson_solve_matches_oracle(comm):
     dom = (0, 0, 0, n - 1, n - 1, n - 1)
     grid = mg.Grid(comm, dom, [dom], prm.domainLength[0] / n)
     res = poisson_solve(grid, prm, max_depth=3, max_NL_iterations=3)
-    psi_o, norms_o, iters_o = oracle_poisson_solve(prm, n, max_depth=3, n_nl=3)
+    psi_o, norms_o, iters_o, _ = oracle_poisson_solve(prm, n, max_depth=3, n_nl=3)
     # the first two NL steps carry the solution; the third dpsi is at the
     # linear solver's roundoff floor, where the two dot-product orders differ
     assert res.linear_iterations[:2] == iters_o[:2]
@@ -446,6 +446,34 @@ def test_nonlinear_poisson_solve_matches_oracle(comm):
     g = res.psi.download(0, with_ghosts=True)[1:-1, 1:-1, 1:-1]
     c = psi_o[1:-1, 1:-1, 1:-1]
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
+
+
+def test_periodic_nonlinear_poisson_solve_matches_oracle(comm):
+    # periodic domain: K from the integrability condition each NL iteration
+    # (Main_PoissonSolver.cpp:133-147), then the same loop as above
+    import dataclasses
+    import os
+    from mg_ic_code_amd.nl import poisson_solve
+    from mg_ic_code_amd.params import read_params_file
+    from tests.nl_ref import oracle_poisson_solve
+    prm = read_params_file(os.path.join(os.path.dirname(__file__), "golden", "params.txt"))
+    prm = dataclasses.replace(prm, is_periodic=1)
+    n = 32
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    from mg_ic_code_amd.decomposition import split_domain
+    boxes = split_domain(dom, (2, 1, 1))
+    grid = mg.Grid(comm, dom, boxes, prm.domainLength[0] / n, periodic=(1, 1, 1))
+    res = poisson_solve(grid, prm, max_depth=3, max_NL_iterations=3)
+    psi_o, norms_o, iters_o, ks_o = oracle_poisson_solve(prm, n, max_depth=3, n_nl=3)
+    # K: a sum over n^3 cells, GPU tree order vs numpy pairwise order
+    np.testing.assert_allclose(res.constant_K, ks_o, rtol=1e-11)
+    assert res.linear_iterations[:2] == iters_o[:2]
+    np.testing.assert_allclose(res.dpsi_norms[:2], norms_o[:2], rtol=1e-6)
+    g = np.zeros((n, n, n))
+    for i, b in enumerate(boxes):
+        g[b[2]:b[5] + 1, b[1]:b[4] + 1, b[0]:b[3] + 1] = res.psi.download(i)
+    c = psi_o[1:-1, 1:-1, 1:-1]
+    assert np.linalg.norm(g - c) <= 1e-9 * np.linalg.norm(c)
 
 
 def test_chf_dropin_setleveldata_bitwise(rng):
