@@ -57,7 +57,8 @@ typedef struct {
   int coefficient_average_type; /* 0 arithmetic (default), 1 harmonic */
   int prolong_type;             /* 0 piecewise constant, 1 linear (default) */
   int relax_mode;               /* 1 GSRB (default), 4 Jacobi */
-  int fused_smoother;           /* 1: fused red+black sweep where valid */
+  int fused_smoother;           /* fused red+black sweep: 0 off (one launch per colour
+                                   pass), 1 kernel by box size, 2 z-streaming, 3 3D blocks */
 } mgic_op_params;
 
 /* MultiGrid / bottom-solver configuration (MultilevelLinearOp knobs:

@@ -24,9 +24,11 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
 // shell and rhs/a/b ghost layer 1.  zero_in: u_in is identically +0 and is
 // not read (first sweep on a freshly zeroed correction).  acc != nullptr:
 // acc += sweep(u_in) instead of writing u_out (phi += e of the last sweep).
+// kind: 1 = by size (one-shot 3D blocks for boxes <= 128^3, z-streaming
+// above), 2 = always z-streaming, 3 = always 3D blocks.
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                      double *acc, hipStream_t st);
+                      double *acc, int kind, hipStream_t st);
 // two red+black sweeps u_in -> u_out in one launch (temporal blocking);
 // BC folded in-kernel, u_in is not modified (zero_in: not read either)
 void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,

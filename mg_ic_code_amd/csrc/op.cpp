@@ -282,7 +282,8 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
                                  args_hom_[b], s, zin, st);
       else
         kern::gsrb_sweep_fused(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
-                               args_hom_[b], s, zin, last && acc ? acc->p[b] : nullptr, st);
+                               args_hom_[b], s, zin, last && acc ? acc->p[b] : nullptr,
+                               prm.fused_smoother, st);
       prof_mark(st, nc, false, 2 * k);
     }
     std::swap(src, dst);

@@ -26,7 +26,8 @@ struct OpParams {
   int coefficient_average_type = 0;  // 0 arithmetic (default), 1 harmonic
   int prolong_type = 1;              // 0 piecewise constant, 1 linear
   int relax_mode = 1;                // [Chombo] s_relaxMode: 1 GSRB, 4 Jacobi
-  int fused_smoother = 1;            // allow the fused red+black sweep kernel
+  int fused_smoother = 1;            // fused red+black sweep: 0 off (per-colour passes),
+                                     // 1 by box size, 2 z-streaming kernel, 3 3D-block kernel
 };
 
 class VariableCoeffPoissonOperator {

@@ -317,6 +317,213 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused6(double *__restrict__ uo,
                                            ty_ * TY, z0, min(z0 + kc, g.nz));
 }
 
+// ---- small levels: one 3D block per workgroup, no streaming ---------------
+// On a coarse level (<= 128^3 per box) the streaming kernel is latency bound:
+// a workgroup walks kc + 5 pipeline steps, each waiting on one global load,
+// so a 64^3 sweep costs as much as a 128^3 one.  Here a workgroup loads its
+// whole TX x TY x TZ tile plus the 2-cell u halo into LDS at once (all loads
+// in flight together), updates the RED cells of the tile grown by one, then
+// the BLACK cells of the tile, and stores: one memory round trip per sweep.
+// Same operands and expressions as k_gsrb_fused6 (bit-identical), same ring
+// extension across exchanged faces, same ZIN/BC/ACC variants, out of place.
+// The domain BC is applied to the LDS copy (no fill launch, u_in untouched).
+// The halo re-reads (u 2.9x, rhs/a 2.1x at 32x8x4) hit L2/MALL: the whole
+// level is cache resident at these sizes.
+template <int TX, int TY, int TZ, int NT>
+struct Blk {
+  static_assert(TX % 2 == 0, "TX must be even");
+  static constexpr int PW = TX / 2 + 2;          // pairs per region row (x0-2 .. x0+TX+1)
+  static constexpr int LH = TY + 4;              // region rows y0-2 .. y0+TY+1
+  static constexpr int CP = PW * LH;             // pairs per region plane
+  static constexpr int NREG = CP * (TZ + 4);     // region planes z0-2 .. z0+TZ+1
+  static constexpr int RH = TY + 2, RZ = TZ + 2;  // ring rows / planes
+  static constexpr int NRP = PW * RH * RZ;
+  static constexpr int NL = (NREG + NT - 1) / NT;
+  static constexpr int NP = (NRP + NT - 1) / NT;
+};
+
+template <int TX, int TY, int TZ, int NT, bool ZIN, bool BC, bool ACC>
+__global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
+                                                   double *__restrict__ acc,
+                                                   const double *__restrict__ ui,
+                                                   const double *__restrict__ rhs,
+                                                   const double *__restrict__ a,
+                                                   const double *__restrict__ b,
+                                                   const BoxArgs g, const StencilCoefs s, int ntx,
+                                                   int nty, int nblocks) {
+  using F = Blk<TX, TY, TZ, NT>;
+  constexpr int PW = F::PW, CP = F::CP, NREG = F::NREG, NRP = F::NRP, NL = F::NL, NP = F::NP;
+  __shared__ double R[NREG];  // red element of every region pair
+  __shared__ double B[NREG];  // black element
+  const int bid = blockIdx.x;  // XCD-aware: consecutive tiles on one XCD
+  const int q8 = nblocks / 8, r8 = nblocks % 8;
+  const int L = (bid % 8) * q8 + min(bid % 8, r8) + bid / 8;
+  const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY, z0 = (L / (ntx * nty)) * TZ;
+  const int tid = threadIdx.x;
+  const long sy = g.sy, sz = g.sz;
+  const int nx = g.nx, ny = g.ny, nz = g.nz;
+  const int xpmax = (nx + 1) & ~1;
+  const int rxlo = g.bcm[0] ? 0 : -1, rxhi = g.bcm[1] ? nx - 1 : nx;
+  const int rylo = g.bcm[2] ? 0 : -1, ryhi = g.bcm[3] ? ny - 1 : ny;
+  const int rzlo = g.bcm[4] ? 0 : -1, rzhi = g.bcm[5] ? nz - 1 : nz;
+  const int q0 = (x0 + g.glo[0] + g.glo[1] + g.glo[2]) & 1;
+  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+
+  // 1. issue every load: the u region (tile + 2) and the ring's rhs/a/b
+  double2 v[NL];
+  if (!ZIN) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + i * NT;
+      const int pz = c / CP, rem = c - pz * CP, r = rem / PW, m = rem - r * PW;
+      const long off = (long)min(x0 - 2 + 2 * m, xpmax) + (long)clampi(y0 - 2 + r, -2, ny + 1) * sy +
+                       (long)clampi(z0 - 2 + pz, -2, nz + 1) * sz;
+      v[i] = *reinterpret_cast<const double2 *>(ui + (c < NREG ? off : 0));
+    }
+  }
+  double cr[NP][2], ca[NP][2], cb[NP][2], ac[NP][2];
+  int rgx0[NP], rgy[NP], rgz[NP], rci[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int c = tid + i * NT;
+    const int rz = c / (PW * F::RH), rem = c - rz * (PW * F::RH), rr = rem / PW, m = rem - rr * PW;
+    rgx0[i] = x0 - 2 + 2 * m;
+    rgy[i] = y0 - 1 + rr;
+    rgz[i] = c < NRP ? z0 - 1 + rz : -1000;  // -1000: no pair (fails every range test)
+    rci[i] = ((rz + 1) * F::LH + rr + 1) * PW + m;
+    const long off = c < NRP ? (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], -1, ny) * sy +
+                                   (long)clampi(rgz[i], -1, nz) * sz
+                             : 0;
+    const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
+    const double2 va = *reinterpret_cast<const double2 *>(a + off);
+    const double2 vb = BC ? make_double2(s.bval, s.bval) : *reinterpret_cast<const double2 *>(b + off);
+    cr[i][0] = vr.x; cr[i][1] = vr.y;
+    ca[i][0] = va.x; ca[i][1] = va.y;
+    cb[i][0] = vb.x; cb[i][1] = vb.y;
+    if (ACC) {
+      const long ao = (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], 0, ny - 1) * sy +
+                      (long)clampi(rgz[i], 0, nz - 1) * sz;
+      const double2 w = *reinterpret_cast<const double2 *>(acc + (c < NRP ? ao : 0));
+      ac[i][0] = w.x; ac[i][1] = w.y;
+    }
+  }
+  // 2. the u region into LDS, red / black split
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = tid + i * NT;
+    if (NL * NT > NREG && c >= NREG) continue;
+    const int pz = c / CP, rem = c - pz * CP, r = rem / PW;
+    const int q = (q0 + y0 - 2 + r + z0 - 2 + pz) & 1;  // 1: the red element is the second
+    const double u0 = ZIN ? 0.0 : v[i].x, u1 = ZIN ? 0.0 : v[i].y;
+    R[c] = bsel(q, u1, u0);
+    B[c] = bsel(q, u0, u1);
+  }
+  // 2b. the domain BC, in LDS: each BC-face ghost of the region takes the
+  // image of the cell it touches -- the values k_fill_bc_faces would have
+  // written into u_in (same cells, including the extension onto exchanged
+  // faces' ghost layers), so the input is never written and the sweep is one
+  // launch.  Only tiles touching a BC face (a workgroup-uniform test) pay.
+  // (the region reaches the hi ghost at n once x0 + TX + 1 >= n)
+  if (!ZIN && ((g.bcm[0] && x0 == 0) || (g.bcm[1] && x0 + TX + 1 >= nx) || (g.bcm[2] && y0 == 0) ||
+               (g.bcm[3] && y0 + TY + 1 >= ny) || (g.bcm[4] && z0 == 0) ||
+               (g.bcm[5] && z0 + TZ + 1 >= nz))) {
+    __syncthreads();
+    const int n3[3] = {nx, ny, nz}, o3[3] = {x0 - 2, y0 - 2, z0 - 2};
+    constexpr int E3[3] = {TX + 4, TY + 4, TZ + 4};  // region extent per direction
+    auto lds = [&](int x, int y, int z) -> double * {  // the LDS slot of cell (x, y, z)
+      const int rx = x - o3[0];
+      const int idx = ((z - o3[2]) * F::LH + (y - o3[1])) * PW + (rx >> 1);
+      const int red = (rx & 1) == ((q0 + y + z) & 1);
+      return red ? &R[idx] : &B[idx];
+    };
+    for (int face = 0; face < 6; ++face) {
+      const int mode = g.bcm[face];
+      if (!mode) continue;
+      const int dir = face >> 1, side = face & 1;
+      const int gc = side == 0 ? -1 : n3[dir];  // ghost coordinate along dir
+      if (gc < o3[dir] || gc >= o3[dir] + E3[dir]) continue;  // face not in this region
+      const int d0 = dir == 0 ? 1 : 0, d1 = dir == 2 ? 1 : 2;
+      const int lo0 = max(g.bcm[2 * d0] ? 0 : -1, o3[d0]);
+      const int hi0 = min(g.bcm[2 * d0 + 1] ? n3[d0] - 1 : n3[d0], o3[d0] + E3[d0] - 1);
+      const int lo1 = max(g.bcm[2 * d1] ? 0 : -1, o3[d1]);
+      const int hi1 = min(g.bcm[2 * d1 + 1] ? n3[d1] - 1 : n3[d1], o3[d1] + E3[d1] - 1);
+      const int w0 = hi0 - lo0 + 1, cnt = w0 * (hi1 - lo1 + 1);
+      for (int t = tid; t < cnt; t += NT) {
+        int c[3];
+        c[dir] = gc;
+        c[d0] = lo0 + t % w0;
+        c[d1] = lo1 + t / w0;
+        double *gp = lds(c[0], c[1], c[2]);
+        c[dir] = side == 0 ? 0 : n3[dir] - 1;
+        *gp = ghost_of(mode, g.bcc[face], *lds(c[0], c[1], c[2]));
+      }
+    }
+  }
+  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
+                 double rv, double av, double bv) -> double {
+    const double tx = (xp + xm) - 2.0 * uc;
+    const double ty = (yp + ym) - 2.0 * uc;
+    const double tz = (zp + zm) - 2.0 * uc;
+    const double lap = (tx + ty) + tz;                     // .ChF:111-120
+    double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
+    const double ldpsi = lap * s.dxinv * bv;               // .ChF:122
+    lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
+    const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
+    return uc - lam * (lofdpsi - rv);                      // .ChF:127-128
+  };
+  __syncthreads();
+  // 3. RED cells of the ring (tile grown by one, clipped at BC faces)
+  const int gxlo = max(x0 - 1, rxlo), gxhi = min(x0 + TX, rxhi);
+  const int gylo = max(y0 - 1, rylo), gyhi = min(y0 + TY, ryhi);
+  const int gzlo = max(z0 - 1, rzlo), gzhi = min(z0 + TZ, rzhi);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int q = (q0 + rgy[i] + rgz[i]) & 1;
+    const int gx = rgx0[i] + q;
+    if (gx < gxlo || gx > gxhi || rgy[i] < gylo || rgy[i] > gyhi || rgz[i] < gzlo || rgz[i] > gzhi)
+      continue;
+    const int ci = rci[i];
+    const double xm = q ? B[ci] : B[ci - 1];
+    const double xp = q ? B[ci + 1] : B[ci];
+    R[ci] = upd(R[ci], xm, xp, B[ci - PW], B[ci + PW], B[ci - CP], B[ci + CP],
+                bsel(q, cr[i][1], cr[i][0]), bsel(q, ca[i][1], ca[i][0]), bsel(q, cb[i][1], cb[i][0]));
+  }
+  __syncthreads();
+  // 4. BLACK cells of the tile + store
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int gy = rgy[i], gz = rgz[i];
+    if (rgx0[i] < x0 || rgx0[i] >= x0 + TX || rgx0[i] >= nx || gy < y0 || gy >= y0 + TY || gy >= ny ||
+        gz < z0 || gz >= z0 + TZ || gz >= nz)
+      continue;
+    const int qb = 1 - ((q0 + gy + gz) & 1);  // 1: the black element is the second
+    const int gx = rgx0[i] + qb;
+    const int ci = rci[i];
+    const double red = R[ci];
+    double blk = B[ci];
+    if (gx < nx) {
+      const double xm = qb ? R[ci] : R[ci - 1];
+      const double xp = qb ? R[ci + 1] : R[ci];
+      blk = upd(blk, xm, xp, R[ci - PW], R[ci + PW], R[ci - CP], R[ci + CP], bsel(qb, cr[i][1], cr[i][0]),
+                bsel(qb, ca[i][1], ca[i][0]), bsel(qb, cb[i][1], cb[i][0]));
+    }
+    double2 w;
+    w.x = bsel(qb, red, blk);
+    w.y = bsel(qb, blk, red);
+    const long off = (long)rgx0[i] + (long)gy * sy + (long)gz * sz;
+    if (ACC) {
+      w.x = ac[i][0] + w.x;
+      w.y = ac[i][1] + w.y;
+      if (rgx0[i] + 1 < nx) *reinterpret_cast<double2 *>(acc + off) = w;
+      else acc[off] = w.x;
+    } else if (rgx0[i] + 1 < nx) {
+      *reinterpret_cast<double2 *>(uo + off) = w;
+    } else {
+      uo[off] = w.x;
+    }
+  }
+}
+
 // ---- two sweeps per launch (temporal blocking) ---------------------------
 // The same streaming scheme carried two sweeps deep: at step p the workgroup
 // updates RED(sweep 1) on plane p, BLACK(1) on p-1, RED(2) on p-2 and
@@ -631,6 +838,12 @@ __global__ void k_fill_bc_faces(double *__restrict__ u, const BoxArgs g) {
 
 }  // namespace
 
+static void fill_bc_faces(double *u, const BoxArgs &g, hipStream_t st) {
+  const int m = (g.nx > g.ny ? g.nx : g.ny) + 2;
+  const int m1 = (g.ny > g.nz ? g.ny : g.nz) + 2;
+  k_fill_bc_faces<<<dim3((unsigned)((m + 255) / 256), (unsigned)m1, 6), dim3(256), 0, st>>>(u, g);
+}
+
 // workgroups of kernel `k` the whole device holds at once
 template <class K>
 static int resident_slots(K k, int nt) {
@@ -664,12 +877,7 @@ template <int TX, int TY, int NT>
 static void launch_fused6(double *u_out, double *u_in, const double *rhs, const double *a,
                           const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                           double *acc, hipStream_t st) {
-  if (!zero_in) {  // BC image of every face into the input's ghost layer
-    const int m = (g.nx > g.ny ? g.nx : g.ny) + 2;
-    const int m1 = (g.ny > g.nz ? g.ny : g.nz) + 2;
-    k_fill_bc_faces<<<dim3((unsigned)((m + 255) / 256), (unsigned)m1, 6), dim3(256), 0, st>>>(u_in,
-                                                                                            g);
-  }
+  if (!zero_in) fill_bc_faces(u_in, g, st);  // BC image of every face into the input's ghost layer
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
   static const int slots = resident_slots(k_gsrb_fused6<TX, TY, NT, false, false, false>, NT);
   static const int kc_mode = [] {
@@ -764,9 +972,62 @@ static int fused_variant() {
   return v;
 }
 
+template <int TX, int TY, int TZ, int NT>
+static void launch_block(double *u_out, double *u_in, const double *rhs, const double *a,
+                         const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                         double *acc, hipStream_t st) {
+  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY, ntz = (g.nz + TZ - 1) / TZ;
+  const int nblocks = ntx * nty * ntz;
+  const dim3 grid((unsigned)nblocks), block(NT);
+#define MGIC_BK(Z, B, A)                                                                     \
+  k_gsrb_block<TX, TY, TZ, NT, Z, B, A><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, b, g, s, \
+                                                                ntx, nty, nblocks)
+  if (acc) {
+    if (zero_in) throw Error(kBadArg, "fused sweep: accumulate on a zero input");
+    if (s.bconst) MGIC_BK(false, true, true);
+    else MGIC_BK(false, false, true);
+  } else if (zero_in) {
+    if (s.bconst) MGIC_BK(true, true, false);
+    else MGIC_BK(true, false, false);
+  } else {
+    if (s.bconst) MGIC_BK(false, true, false);
+    else MGIC_BK(false, false, false);
+  }
+#undef MGIC_BK
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(kHipErr, std::string("block sweep launch: ") + hipGetErrorString(e));
+}
+
+// boxes of at most this many cells take the block kernel (MGIC_BLOCK_MAX_CELLS;
+// 0 = never); MGIC_BLOCK_VARIANT picks its tile for measurement
+static long block_max_cells() {
+  static long v = [] {
+    const char *e = getenv("MGIC_BLOCK_MAX_CELLS");
+    return e ? atol(e) : 128L * 128 * 128;
+  }();
+  return v;
+}
+
+static int block_variant() {
+  static int v = [] {
+    const char *e = getenv("MGIC_BLOCK_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                      double *acc, hipStream_t st) {
+                      double *acc, int kind, hipStream_t st) {
+  if (kind == 3 || (kind != 2 && (long)g.nx * g.ny * g.nz <= block_max_cells())) {
+    switch (block_variant()) {
+      case 1: launch_block<16, 8, 8, 128>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
+      case 2: launch_block<32, 8, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
+      case 3: launch_block<16, 8, 4, 128>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
+      case 4: launch_block<32, 4, 4, 128>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
+      default: launch_block<32, 8, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
+    }
+  }
   switch (fused_variant()) {
     case 1: launch_fused6<60, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
     case 2: launch_fused6<256, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;

@@ -234,9 +234,11 @@ def test_fill_bc_matches_oracle(comm, rng):
 
 @pytest.mark.parametrize("parts,prolong,avg", [((1, 1, 1), 1, 1), ((1, 1, 1), 0, 0),
                                                ((2, 2, 2), 1, 1), ((2, 1, 2), 0, 1)])
-def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg):
+@pytest.mark.parametrize("fused", [2, 3])  # z-streaming / 3D-block sweep kernel
+def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused):
     n = 32
-    S = build_pair(comm, rng, n, parts, prolong=prolong, avg=avg, nlevels=3, bottom=0)
+    S = build_pair(comm, rng, n, parts, prolong=prolong, avg=avg, nlevels=3, bottom=0,
+                   fused=fused)
     amg, o = S["amg"], S["o"]
     assert amg.num_depths == 3
     amg.init_residual(S["fphi"], S["frhs"], S["fres"])
@@ -248,7 +250,8 @@ def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg):
     assert np.array_equal(download_global(S["fphi"], S["grid"], (n,) * 3), o.get(0, oracle.PHI, 0))
 
 
-def test_vcycle_periodic_multibox_rccl_self_messages(rng):
+@pytest.mark.parametrize("fused", [2, 3])
+def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused):
     # the RCCL pack -> send/recv -> unpack path, exercised on one GPU by
     # routing same-rank copies through self send/recv
     c_local = mg.Comm()
@@ -259,7 +262,7 @@ def test_vcycle_periodic_multibox_rccl_self_messages(rng):
     out = []
     for c in (c_local, c_rccl):
         S = build_pair(c, np.random.default_rng(7), n, (2, 2, 2), periodic=(1, 1, 1), alpha=1.0,
-                       nlevels=3, bottom=0)
+                       nlevels=3, bottom=0, fused=fused)
         amg = S["amg"]
         amg.init_residual(S["fphi"], S["frhs"], S["fres"])
         norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
@@ -313,12 +316,14 @@ def test_binary_bh_inputs_on_device(comm):
 
 
 @pytest.mark.slow
-def test_large_vcycle_single_vs_multibox_and_oracle(comm):
+@pytest.mark.parametrize("fused", [2, 3])
+def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused):
     # 128^3: GPU single box == GPU 8 boxes == oracle, bit for bit
     n = 128
     res = []
     for parts in ((1, 1, 1), (2, 2, 2)):
-        S = build_pair(comm, np.random.default_rng(11), n, parts, nlevels=3, bottom=0, bvar=False)
+        S = build_pair(comm, np.random.default_rng(11), n, parts, nlevels=3, bottom=0, bvar=False,
+                       fused=fused)
         amg = S["amg"]
         amg.init_residual(S["fphi"], S["frhs"], S["fres"])
         norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
@@ -349,7 +354,7 @@ def test_fused_sweep_matches_oracle_and_passes(comm, rng, shape, lo, nsweeps):
     u0 = rng.uniform(-1, 1, (nz, ny, nx))
     bc_lo, bc_hi = (0, 1, 0), (1, 0, 1)
     outs = []
-    for fused in (1, 0):
+    for fused in (2, 3, 1, 0):  # z-streaming, 3D blocks, by size, per-colour passes
         grid = mg.Grid(comm, dom, [dom], dx)
         fa, fb, fr, fu = (mg.LevelData(grid) for _ in range(4))
         fa.upload(0, a)
@@ -362,7 +367,8 @@ def test_fused_sweep_matches_oracle_and_passes(comm, rng, shape, lo, nsweeps):
         op = fac.AMRnewOp()
         op.relax(fu, fr, nsweeps)
         outs.append(fu.download(0))
-    assert np.array_equal(outs[0], outs[1])
+    for x in outs[1:]:
+        assert np.array_equal(outs[0], x)
     o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi,
                         bc_value=0.5, nlevels=1)
     o.set(0, oracle.ACOEF, 0, a)

@@ -2,8 +2,8 @@
 """Micro-benchmark of the fine-level smoother: time `relax(nsweeps)` on one
 n^3 box (SetBinaryBH inputs) and print one JSON line with per-sweep time,
 effective GB/s (48 B/cell/pass credited) and a checksum of the result.
-Kernel selection: MGIC_SWEEPS_PER_LAUNCH (1 or 2), MGIC_FUSED_VARIANT /
-MGIC_FUSED2X_VARIANT (tile shapes)."""
+Kernel selection: --kind, MGIC_SWEEPS_PER_LAUNCH (1 or 2), MGIC_FUSED_VARIANT /
+MGIC_FUSED2X_VARIANT / MGIC_BLOCK_VARIANT (tile shapes)."""
 import argparse
 import hashlib
 import json
@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-fused", action="store_true")
     ap.add_argument("--tag", default=None)
+    ap.add_argument("--kind", type=int, default=1,
+                    help="fused_smoother: 1 by size, 2 z-streaming, 3 3D blocks")
     args = ap.parse_args()
     import mg_ic_code_amd as mg
     from mg_ic_code_amd.params import read_params_file
@@ -37,7 +39,7 @@ def main():
     fu.set_zero()
     op = mg.defineOperatorFactory(grid, fa, fb, mg.OperatorParams(
         alpha=1.0, beta=-1.0, coefficient_average_type=1,
-        fused_smoother=0 if args.no_fused else 1)).AMRnewOp()
+        fused_smoother=0 if args.no_fused else args.kind)).AMRnewOp()
     op.relax(fu, fr, 2)  # warm-up
     comm.synchronize()
     mg.prof_smoother(True, n ** 3)
