@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--boxes-per-rank", default="1,1,1",
                     help="split each rank's share into this many boxes (x,y,z) -- the multi-box "
                          "(exchange) path on one GPU")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="halo exchange overlapped with the sweep: 0 off, 1 auto (boxes >= 96^3), "
+                         "2 always")
     ap.add_argument("--cpu-baseline-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -98,7 +101,8 @@ def main():
     op_params = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
                                   bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
                                   coefficient_average_type=1, prolong_type=1, relax_mode=1,
-                                  fused_smoother=0 if args.no_fused else 1)
+                                  fused_smoother=0 if args.no_fused else 1,
+                                  overlap_exchange=args.overlap)
     fac = mg.defineOperatorFactory(grid, fa, fb, op_params)
     sp = mg.SolverParams(max_depth=args.levels - 1, n_pre=args.nsmooth, n_post=args.nsmooth,
                          n_bottom=args.nsmooth, bottom_solver=0)

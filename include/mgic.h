@@ -59,6 +59,10 @@ typedef struct {
   int relax_mode;               /* 1 GSRB (default), 4 Jacobi */
   int fused_smoother;           /* fused red+black sweep: 0 off (one launch per colour
                                    pass), 1 kernel by box size, 2 z-streaming, 3 3D blocks */
+  int overlap_exchange;         /* fused sweeps on exchanged layouts: boundary slabs +
+                                   ghost-shell exchange on a second stream, overlapping
+                                   the sweep.  0 off (default), 1 if every box >= 96^3,
+                                   2 always */
 } mgic_op_params;
 
 /* MultiGrid / bottom-solver configuration (MultilevelLinearOp knobs:

@@ -36,6 +36,7 @@ class OpParams(ctypes.Structure):
         ("prolong_type", c_int),
         ("relax_mode", c_int),
         ("fused_smoother", c_int),
+        ("overlap_exchange", c_int),
     ]
 
 

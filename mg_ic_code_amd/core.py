@@ -255,7 +255,8 @@ class OperatorParams:
     coefficient_average_type: int = 0  # 0 arithmetic, 1 harmonic
     prolong_type: int = 1               # 0 piecewise constant, 1 linear
     relax_mode: int = 1                 # 1 GSRB, 4 Jacobi
-    fused_smoother: int = 1
+    fused_smoother: int = 1             # 0 per-colour passes, 1 by size, 2 z-streaming, 3 3D blocks
+    overlap_exchange: int = 0           # halo exchange overlapped with the sweep: 0, 1 auto, 2 always
 
     def to_c(self) -> OpParams:
         p = OpParams()
@@ -267,6 +268,7 @@ class OperatorParams:
         p.prolong_type = self.prolong_type
         p.relax_mode = self.relax_mode
         p.fused_smoother = self.fused_smoother
+        p.overlap_exchange = self.overlap_exchange
         return p
 
 

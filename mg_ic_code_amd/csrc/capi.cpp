@@ -68,6 +68,7 @@ OpParams to_op(const mgic_op_params *p) {
   o.prolong_type = p->prolong_type;
   o.relax_mode = p->relax_mode;
   o.fused_smoother = p->fused_smoother;
+  o.overlap_exchange = p->overlap_exchange;
   return o;
 }
 
@@ -190,6 +191,7 @@ MGIC_API void mgic_op_params_default(mgic_op_params *p) {
   p->prolong_type = o.prolong_type;
   p->relax_mode = o.relax_mode;
   p->fused_smoother = o.fused_smoother;
+  p->overlap_exchange = o.overlap_exchange;
 }
 
 MGIC_API void mgic_mg_params_default(mgic_mg_params *p) {

@@ -29,6 +29,13 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       double *acc, int kind, hipStream_t st);
+// The same sweep, computed only on the cells within `depth` of each
+// exchanged face (bcm == 0): the part of u_out the neighbours' ghost shells
+// need.  Values are identical to gsrb_sweep_fused's, so it may run on a
+// second stream concurrently with the full sweep writing the same cells.
+void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const double *a,
+                      const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                      int depth, hipStream_t st);
 // two red+black sweeps u_in -> u_out in one launch (temporal blocking);
 // BC folded in-kernel, u_in is not modified (zero_in: not read either)
 void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,

@@ -28,8 +28,21 @@ std::shared_ptr<Comm> Comm::host_only(int rank, int size) {
   return c;
 }
 
+hipStream_t Comm::side_stream() {
+  if (!side_) MGIC_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  return side_;
+}
+
+hipEvent_t Comm::event(int i) {
+  if (!events_[i]) MGIC_HIP(hipEventCreateWithFlags(&events_[i], hipEventDisableTiming));
+  return events_[i];
+}
+
 Comm::~Comm() {
   if (nccl_) ncclCommDestroy(nccl_);
+  if (side_) (void)hipStreamDestroy(side_);
+  for (hipEvent_t e : events_)
+    if (e) (void)hipEventDestroy(e);
   if (d_partials_) (void)hipFree(d_partials_);
   if (d_result_) (void)hipFree(d_result_);
   if (h_result_) (void)hipHostFree(h_result_);

@@ -44,6 +44,10 @@ class Comm {
   ncclComm_t nccl() const { return nccl_; }
   hipStream_t stream() const { return stream_; }
   void set_stream(hipStream_t s) { stream_ = s; }
+  // a second stream (created on first use) for halo work that overlaps the
+  // main stream's sweeps, and two reusable events to order the two
+  hipStream_t side_stream();
+  hipEvent_t event(int i);
   // in-place allreduce of one device double (op: 0 sum, 1 max)
   void allreduce(double *d_val, int op);
   // scratch for reductions (device partials + result, pinned host result)
@@ -58,6 +62,8 @@ class Comm {
   ncclComm_t nccl_ = nullptr;
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;
+  hipStream_t side_ = nullptr;
+  hipEvent_t events_[2] = {nullptr, nullptr};
   double *d_partials_ = nullptr;
   int n_partials_ = 0;
   double *d_result_ = nullptr;

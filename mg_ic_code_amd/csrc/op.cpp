@@ -154,7 +154,7 @@ void VariableCoeffPoissonOperator::applyOpNoBoundary(LevelData &lhs, LevelData &
 }
 
 void VariableCoeffPoissonOperator::restrictResidual(LevelData &resC, LevelData &dpsiF,
-                                                    const LevelData &rhsF) {
+                                                    const LevelData &rhsF, bool exchange) {
   const Grid &cg = *resC.grid;
   MGIC_CHECK(cg.nlocal() == grid->nlocal(), "restrictResidual: coarse layout mismatch");
   for (int n = 0; n < grid->nlocal(); ++n) {
@@ -163,7 +163,7 @@ void VariableCoeffPoissonOperator::restrictResidual(LevelData &resC, LevelData &
                "restrictResidual: coarse box is not coarsen(fine box, 2)");
   }
   const hipStream_t st = stream();
-  dpsiF.exchange(st);  // .cpp:163 (BC of :158-161 folded, homogeneous)
+  if (exchange) dpsiF.exchange(st);  // .cpp:163 (BC of :158-161 folded, homogeneous)
   const StencilCoefs s = coefs();
   for (int n = 0; n < grid->nlocal(); ++n)
     kern::restrict_residual(resC.p[n], cg.box_args_plain(n), dpsiF.p[n], rhsF.p[n], m_aCoef->p[n],
@@ -252,15 +252,29 @@ static int sweeps_per_launch() {
   return v;
 }
 
+bool VariableCoeffPoissonOperator::overlapApplies() const {
+  if (prm.overlap_exchange == 0) return false;
+  if (prm.overlap_exchange == 2) return true;
+  static const long min_cells = [] {
+    const char *e = getenv("MGIC_OVERLAP_MIN_CELLS");
+    return e ? atol(e) : 96L * 96 * 96;
+  }();
+  // decided on the global layout, so every rank issues the same sequence
+  // of RCCL calls on the same streams
+  for (const Box &b : grid->boxes)
+    if (b.ncells() < min_cells) return false;
+  return true;
+}
+
 void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
-                                              bool zero_in, LevelData *acc) {
+                                              bool zero_in, LevelData *acc, int flags) {
   resetLambda();  // .cpp:283
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
   if (!sweep_tmp_) sweep_tmp_ = create();
   const bool halo = grid->has_memory_faces();
   if (halo) {  // ghost layer 1 of rhs / aCoef / bCoef for the red ring on the halo
-    const_cast<LevelData &>(rhs).exchange(st);
+    if (!(flags & kRhsHaloReady)) const_cast<LevelData &>(rhs).exchange(st);
     if (!coef_ghosts_) {
       m_aCoef->exchange(st);
       m_bCoef->exchange(st);
@@ -269,11 +283,35 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
   const int per = acc ? 1 : sweeps_per_launch();
+  const bool want_out = halo && (flags & kHaloOut) && !acc;
+  const bool overlap = halo && per == 1 && overlapApplies();
+  // Overlapped halo: sweep i runs on the main stream over the whole box;
+  // meanwhile the side stream recomputes the cells within 2 of every
+  // exchanged face (the same values) and exchanges that ghost shell, so the
+  // exchange sweep i+1 needs is in flight while sweep i runs.  Ordering:
+  // side step i waits for main up to sweep i-1 (evM: its input complete), main
+  // sweep i+1 waits for side step i (evE: its input's shell filled, and
+  // side step i done reading the buffer sweep i+1 overwrites).
+  hipStream_t side = nullptr;
+  hipEvent_t evM = nullptr, evE = nullptr;
+  if (overlap) {
+    side = grid->comm->side_stream();
+    evM = grid->comm->event(0);
+    evE = grid->comm->event(1);
+  }
+  bool side_pending = false;
   for (int it = 0; it < n;) {
     const bool zin = zero_in && it == 0;
     const int k = (per == 2 && !halo && n - it >= 2) ? 2 : 1;
     const bool last = it + k == n;
-    if (halo && !zin) src->exchange_shell(st);
+    if (halo && !zin && (!overlap || it == 0)) src->exchange_shell(st);
+    if (side_pending) {
+      MGIC_HIP(hipStreamWaitEvent(st, evE, 0));
+      side_pending = false;
+    }
+    // everything the main stream did so far (src's valid cells, the exposed
+    // first exchange, rhs/coefficient ghosts) is what the side step reads
+    if (overlap) MGIC_HIP(hipEventRecord(evM, st));
     for (int b = 0; b < grid->nlocal(); ++b) {
       const long nc = grid->geom[b].valid.ncells();
       prof_mark(st, nc, true, 2 * k);
@@ -286,33 +324,59 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
                                prm.fused_smoother, st);
       prof_mark(st, nc, false, 2 * k);
     }
+    if (overlap && (!last || want_out)) {
+      MGIC_HIP(hipStreamWaitEvent(side, evM, 0));
+      for (int b = 0; b < grid->nlocal(); ++b)
+        kern::gsrb_sweep_slabs(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
+                               args_hom_[b], s, zin, 2, side);
+      dst->exchange_shell(side);
+      MGIC_HIP(hipEventRecord(evE, side));
+      side_pending = true;
+    }
     std::swap(src, dst);
     it += k;
   }
+  if (side_pending) MGIC_HIP(hipStreamWaitEvent(st, evE, 0));
   if (acc) return;   // the last sweep went into acc; dpsi is scratch now
-  if (src != &dpsi)  // the result sits in the scratch buffer
+  if (src != &dpsi) {  // the result sits in the scratch buffer
     for (int b = 0; b < grid->nlocal(); ++b)
       kern::blas(0, dpsi.p[b], src->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
+    if (want_out) dpsi.exchange(st);
+  } else if (want_out && !overlap) {
+    dpsi.exchange(st);
+  }
 }
 
 void VariableCoeffPoissonOperator::relaxAccumulate(LevelData &e, const LevelData &r, int n,
-                                                   LevelData &phi) {
+                                                   LevelData &phi, int flags) {
   if (n > 0 && prm.relax_mode == 1 && fusedSmootherApplies()) {
     check_same_layout(*grid, phi, "phi");
-    fusedRelax(e, r, n, false, &phi);
+    fusedRelax(e, r, n, false, &phi, flags);
     return;
   }
   relax(e, r, n);
   incr(phi, e, 1.0);
 }
 
-void VariableCoeffPoissonOperator::relaxFromZero(LevelData &e, const LevelData &r, int n) {
+void VariableCoeffPoissonOperator::relaxFromZero(LevelData &e, const LevelData &r, int n,
+                                                 int flags) {
   if (n > 0 && prm.relax_mode == 1 && fusedSmootherApplies()) {
-    fusedRelax(e, r, n, true);
+    fusedRelax(e, r, n, true, nullptr, flags);
     return;
   }
   setToZero(e);
   relax(e, r, n);
+  if (flags & kHaloOut) e.exchange(stream());
+}
+
+void VariableCoeffPoissonOperator::relaxFlags(LevelData &e, const LevelData &r, int n,
+                                              int flags) {
+  if (n > 0 && prm.relax_mode == 1 && fusedSmootherApplies()) {
+    fusedRelax(e, r, n, false, nullptr, flags);
+    return;
+  }
+  relax(e, r, n);
+  if (flags & kHaloOut) e.exchange(stream());
 }
 
 void VariableCoeffPoissonOperator::relax(LevelData &e, const LevelData &r, int iterations) {
@@ -662,44 +726,58 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
   MGIC_HIP(hipStreamSynchronize(levels_[0].op->stream()));
 }
 
-void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc) {
+void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
+                      bool halo_out) {
   VariableCoeffPoissonOperator &op = *levels_[d].op;
   const hipStream_t st = op.stream();
+  // r's ghost layer once per level visit (the fused sweeps' red ring reads
+  // it; r does not change between pre- and post-smoothing)
+  int rf = 0;
+  if (op.grid->has_memory_faces() && op.fusedSmootherApplies() && op.prm.relax_mode == 1) {
+    r.exchange(st);
+    rf = kRhsHaloReady;
+  }
+  const int out = halo_out ? kHaloOut : 0;
   if (d == (int)levels_.size() - 1) {  // bottom
     if (prm.bottom_solver == 1) {
       if (e_zero) op.setToZero(e);
       bottom.solve(op, e, r, true);
+      if (halo_out) e.exchange(st);
     } else if (e_zero) {
-      op.relaxFromZero(e, r, prm.n_bottom);
+      op.relaxFromZero(e, r, prm.n_bottom, rf | out);
     } else {
-      op.relax(e, r, prm.n_bottom);
+      op.relaxFlags(e, r, prm.n_bottom, rf | out);
     }
     if (phi_acc) op.incr(*phi_acc, e, 1.0);
     return;
   }
+  // pre-smoothing leaves e's face ghosts exchanged for the restriction
   if (e_zero)
-    op.relaxFromZero(e, r, prm.n_pre);
+    op.relaxFromZero(e, r, prm.n_pre, rf | kHaloOut);
   else
-    op.relax(e, r, prm.n_pre);
+    op.relaxFlags(e, r, prm.n_pre, rf | kHaloOut);
   Level &N = levels_[d + 1];
   if (!N.agg) {
-    op.restrictResidual(*N.r, e, r);
+    op.restrictResidual(*N.r, e, r, false);
   } else {
-    op.restrictResidual(*N.r_stage, e, r);
+    op.restrictResidual(*N.r_stage, e, r, false);
     N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
   }
-  // coarse correction e_c = 0 (folded into its first sweep when possible)
-  for (int c = 0; c < prm.cycles; ++c) cycle(d + 1, *N.e, *N.r, c == 0, nullptr);
+  // coarse correction e_c = 0 (folded into its first sweep when possible);
+  // its last relax exchanges e_c's ghosts for the linear prolongation
+  const bool coarse_out = !N.agg && op.prm.prolong_type == 1;
+  for (int c = 0; c < prm.cycles; ++c)
+    cycle(d + 1, *N.e, *N.r, c == 0, nullptr, coarse_out && c == prm.cycles - 1);
   if (!N.agg) {
-    op.prolongIncrement(e, *N.e);
+    op.prolongIncrementFilled(e, *N.e);
   } else {
     N.prolong_plan->execute(*op.grid->comm, N.e->d_tab, N.e_stage->d_tab, st);
     op.prolongIncrementFilled(e, *N.e_stage);
   }
   if (phi_acc)  // phi += e folded into the last post-smoothing sweep
-    op.relaxAccumulate(e, r, prm.n_post, *phi_acc);
+    op.relaxAccumulate(e, r, prm.n_post, *phi_acc, rf);
   else
-    op.relax(e, r, prm.n_post);
+    op.relaxFlags(e, r, prm.n_post, rf | out);
 }
 
 // --------------------------------------------------------------- AMRMultiGrid

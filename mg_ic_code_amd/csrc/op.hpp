@@ -28,7 +28,17 @@ struct OpParams {
   int relax_mode = 1;                // [Chombo] s_relaxMode: 1 GSRB, 4 Jacobi
   int fused_smoother = 1;            // fused red+black sweep: 0 off (per-colour passes),
                                      // 1 by box size, 2 z-streaming kernel, 3 3D-block kernel
+  int overlap_exchange = 0;          // fused sweeps on exchanged layouts: compute the
+                                     // boundary slabs + ghost-shell exchange on a second
+                                     // stream while the main stream sweeps the box.
+                                     // 0 off (default: measured slower on one GPU, the
+                                     // slab sweeps cost more than the exchange they hide),
+                                     // 1 when every box has >= 96^3 cells, 2 always
 };
+
+// relax flags (MultiGrid::cycle): the caller exchanged rhs's ghost layer
+// already / wants the result's face ghosts exchanged on return
+enum RelaxFlags { kRhsHaloReady = 1, kHaloOut = 2 };
 
 class VariableCoeffPoissonOperator {
  public:
@@ -47,7 +57,8 @@ class VariableCoeffPoissonOperator {
   void applyOpI(LevelData &lhs, LevelData &dpsi, bool homogeneous);
   void applyOp(LevelData &lhs, LevelData &dpsi, bool homogeneous) { applyOpI(lhs, dpsi, homogeneous); }
   void applyOpNoBoundary(LevelData &lhs, LevelData &dpsi);
-  void restrictResidual(LevelData &resCoarse, LevelData &dpsiFine, const LevelData &rhsFine);
+  void restrictResidual(LevelData &resCoarse, LevelData &dpsiFine, const LevelData &rhsFine,
+                        bool exchange = true);
   // [Chombo] AMRPoissonOp::prolongIncrement (inherited)
   void prolongIncrement(LevelData &phiThisLevel, LevelData &correctCoarse);
   // same, with the coarse ghost layer already filled by the caller
@@ -111,13 +122,16 @@ class VariableCoeffPoissonOperator {
   // zero_in: dpsi is taken as identically zero and not read (its memory
   // need not be zeroed).
   void fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false,
-                  LevelData *acc = nullptr);
+                  LevelData *acc = nullptr, int flags = 0);
+  bool overlapApplies() const;
   // relax(e, r, n); phi += e -- the increment folded into the last fused
   // sweep (e is left as scratch in that case)
-  void relaxAccumulate(LevelData &e, const LevelData &r, int n, LevelData &phi);
+  void relaxAccumulate(LevelData &e, const LevelData &r, int n, LevelData &phi, int flags = 0);
   // e = 0; relax(e, r, n) -- without zeroing e in memory when the fused
   // smoother applies (the first sweep does not read its input)
-  void relaxFromZero(LevelData &e, const LevelData &r, int n);
+  void relaxFromZero(LevelData &e, const LevelData &r, int n, int flags = 0);
+  // relax(e, r, n) with RelaxFlags
+  void relaxFlags(LevelData &e, const LevelData &r, int n, int flags);
 };
 
 // throws kBadArg unless x lives on g's boxes with g's fab geometry
@@ -216,7 +230,8 @@ class MultiGrid {
   };
   // e_zero: treat e as zero on entry (it is zeroed or never read);
   // phi_acc: phi += e at the end (at depth 0 folded into the last sweep)
-  void cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc);
+  void cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
+             bool halo_out = false);
   std::vector<Level> levels_;
 };
 

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
                                                    const double *__restrict__ a,
                                                    const double *__restrict__ b,
                                                    const BoxArgs g, const StencilCoefs s, int ntx,
-                                                   int nty, int nblocks) {
+                                                   int nty, int nblocks, int ox, int oy, int oz) {
   using F = Blk<TX, TY, TZ, NT>;
   constexpr int PW = F::PW, CP = F::CP, NREG = F::NREG, NRP = F::NRP, NL = F::NL, NP = F::NP;
   __shared__ double R[NREG];  // red element of every region pair
@@ -358,7 +358,9 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
   const int bid = blockIdx.x;  // XCD-aware: consecutive tiles on one XCD
   const int q8 = nblocks / 8, r8 = nblocks % 8;
   const int L = (bid % 8) * q8 + min(bid % 8, r8) + bid / 8;
-  const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY, z0 = (L / (ntx * nty)) * TZ;
+  // tiles of the region starting at (ox, oy, oz); ox is even (16-B pairs)
+  const int x0 = ox + (L % ntx) * TX, y0 = oy + ((L / ntx) % nty) * TY;
+  const int z0 = oz + (L / (ntx * nty)) * TZ;
   const int tid = threadIdx.x;
   const long sy = g.sy, sz = g.sz;
   const int nx = g.nx, ny = g.ny, nz = g.nz;
@@ -972,16 +974,24 @@ static int fused_variant() {
   return v;
 }
 
+// the sweep on the tiles covering the region o + [0, e) of the box (the
+// whole box, or a slab along one face); cells of those tiles outside the
+// region are computed too (the same values)
 template <int TX, int TY, int TZ, int NT>
 static void launch_block(double *u_out, double *u_in, const double *rhs, const double *a,
                          const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                         double *acc, hipStream_t st) {
-  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY, ntz = (g.nz + TZ - 1) / TZ;
+                         double *acc, hipStream_t st, const int *o = nullptr,
+                         const int *e = nullptr) {
+  const int ox = o ? o[0] : 0, oy = o ? o[1] : 0, oz = o ? o[2] : 0;
+  const int ex = e ? e[0] : g.nx, ey = e ? e[1] : g.ny, ez = e ? e[2] : g.nz;
+  if (ox & 1) throw Error(kBadArg, "block sweep: odd x origin");
+  const int ntx = (ex + TX - 1) / TX, nty = (ey + TY - 1) / TY, ntz = (ez + TZ - 1) / TZ;
   const int nblocks = ntx * nty * ntz;
+  if (nblocks <= 0) return;
   const dim3 grid((unsigned)nblocks), block(NT);
 #define MGIC_BK(Z, B, A)                                                                     \
   k_gsrb_block<TX, TY, TZ, NT, Z, B, A><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, b, g, s, \
-                                                                ntx, nty, nblocks)
+                                                                ntx, nty, nblocks, ox, oy, oz)
   if (acc) {
     if (zero_in) throw Error(kBadArg, "fused sweep: accumulate on a zero input");
     if (s.bconst) MGIC_BK(false, true, true);
@@ -994,8 +1004,9 @@ static void launch_block(double *u_out, double *u_in, const double *rhs, const d
     else MGIC_BK(false, false, false);
   }
 #undef MGIC_BK
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw Error(kHipErr, std::string("block sweep launch: ") + hipGetErrorString(e));
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess)
+    throw Error(kHipErr, std::string("block sweep launch: ") + hipGetErrorString(err));
 }
 
 // boxes of at most this many cells take the block kernel (MGIC_BLOCK_MAX_CELLS;
@@ -1020,18 +1031,42 @@ void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const doub
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       double *acc, int kind, hipStream_t st) {
   if (kind == 3 || (kind != 2 && (long)g.nx * g.ny * g.nz <= block_max_cells())) {
-    switch (block_variant()) {
-      case 1: launch_block<16, 8, 8, 128>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
-      case 2: launch_block<32, 8, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
-      case 3: launch_block<16, 8, 4, 128>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
-      case 4: launch_block<32, 4, 4, 128>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
-      default: launch_block<32, 8, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); return;
-    }
+    // 32x8x4 / 256 threads: 64^3 0.0094 ms, 128^3 0.026 ms per sweep; 32x8x8
+    // 0.0116 / 0.0278; 16x8x8, 16x8x4, 32x4x4 (128 threads) were slower still
+    if (block_variant() == 1)
+      launch_block<32, 8, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+    else
+      launch_block<32, 8, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+    return;
   }
   switch (fused_variant()) {
     case 1: launch_fused6<60, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
     case 2: launch_fused6<256, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
     default: launch_fused6<128, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
+  }
+}
+
+void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const double *a,
+                      const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                      int depth, hipStream_t st) {
+  for (int face = 0; face < 6; ++face) {
+    if (g.bcm[face]) continue;  // a domain face: nobody reads a shell there
+    const int dir = face >> 1, side = face & 1;
+    const int n[3] = {g.nx, g.ny, g.nz};
+    int o[3] = {0, 0, 0}, e[3] = {g.nx, g.ny, g.nz};
+    const int d = depth < n[dir] ? depth : n[dir];
+    o[dir] = side == 0 ? 0 : n[dir] - d;
+    e[dir] = d;
+    if (dir == 0) {  // even x origin: widen the slab to the pair boundary
+      const int x0 = o[0] & ~1;
+      e[0] += o[0] - x0;
+      o[0] = x0;
+      launch_block<4, 16, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
+    } else if (dir == 1) {
+      launch_block<32, 2, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
+    } else {
+      launch_block<32, 8, 2, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
+    }
   }
 }
 

@@ -124,7 +124,7 @@ def test_chf_dropin_op_res_restrict_bitwise(rng):
 # ----------------------------------------------------------------- operator level
 def build_pair(comm, rng, n, parts, *, alpha=1.0, beta=-1.0, avg=1, prolong=1, bc_lo=(0, 0, 0),
                bc_hi=(0, 0, 0), bc_value=0.0, periodic=(0, 0, 0), nlevels=3, bottom=0,
-               relax_mode=1, agglomerate_below=0, fused=1, bvar=True):
+               relax_mode=1, agglomerate_below=0, fused=1, bvar=True, overlap=1):
     dom = (0, 0, 0, n - 1, n - 1, n - 1)
     dx = 100.0 / n
     boxes = split_domain(dom, parts)
@@ -138,7 +138,7 @@ def build_pair(comm, rng, n, parts, *, alpha=1.0, beta=-1.0, avg=1, prolong=1, b
     fphi.set_zero()
     prm = mg.OperatorParams(alpha=alpha, beta=beta, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bc_value,
                             coefficient_average_type=avg, prolong_type=prolong,
-                            relax_mode=relax_mode, fused_smoother=fused)
+                            relax_mode=relax_mode, fused_smoother=fused, overlap_exchange=overlap)
     fac = mg.defineOperatorFactory(grid, fa, fb, prm)
     amg = mg.AMRMultiGrid(fac, mg.SolverParams(max_depth=nlevels - 1, bottom_solver=bottom,
                                                 agglomerate_below=agglomerate_below))
@@ -235,10 +235,11 @@ def test_fill_bc_matches_oracle(comm, rng):
 @pytest.mark.parametrize("parts,prolong,avg", [((1, 1, 1), 1, 1), ((1, 1, 1), 0, 0),
                                                ((2, 2, 2), 1, 1), ((2, 1, 2), 0, 1)])
 @pytest.mark.parametrize("fused", [2, 3])  # z-streaming / 3D-block sweep kernel
-def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused):
+@pytest.mark.parametrize("overlap", [0, 2])  # halo exchange on a second stream
+def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused, overlap):
     n = 32
     S = build_pair(comm, rng, n, parts, prolong=prolong, avg=avg, nlevels=3, bottom=0,
-                   fused=fused)
+                   fused=fused, overlap=overlap)
     amg, o = S["amg"], S["o"]
     assert amg.num_depths == 3
     amg.init_residual(S["fphi"], S["frhs"], S["fres"])
@@ -251,7 +252,8 @@ def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused):
 
 
 @pytest.mark.parametrize("fused", [2, 3])
-def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused):
+@pytest.mark.parametrize("overlap", [0, 2])
+def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, overlap):
     # the RCCL pack -> send/recv -> unpack path, exercised on one GPU by
     # routing same-rank copies through self send/recv
     c_local = mg.Comm()
@@ -262,7 +264,7 @@ def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused):
     out = []
     for c in (c_local, c_rccl):
         S = build_pair(c, np.random.default_rng(7), n, (2, 2, 2), periodic=(1, 1, 1), alpha=1.0,
-                       nlevels=3, bottom=0, fused=fused)
+                       nlevels=3, bottom=0, fused=fused, overlap=overlap)
         amg = S["amg"]
         amg.init_residual(S["fphi"], S["frhs"], S["fres"])
         norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
@@ -289,9 +291,11 @@ def test_bicgstab_bottom_within_tolerance(comm, rng):
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
 
 
-def test_agglomerated_hierarchy_matches_single_box(comm, rng):
+@pytest.mark.parametrize("overlap", [0, 2])
+def test_agglomerated_hierarchy_matches_single_box(comm, rng, overlap):
     n = 32
-    S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16)
+    S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16,
+                   overlap=overlap)
     amg, o = S["amg"], S["o"]
     assert amg.num_depths == 5
     amg.init_residual(S["fphi"], S["frhs"], S["fres"])
@@ -316,14 +320,14 @@ def test_binary_bh_inputs_on_device(comm):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("fused", [2, 3])
-def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused):
+@pytest.mark.parametrize("fused,overlap", [(2, 0), (3, 2), (2, 2)])
+def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused, overlap):
     # 128^3: GPU single box == GPU 8 boxes == oracle, bit for bit
     n = 128
     res = []
     for parts in ((1, 1, 1), (2, 2, 2)):
         S = build_pair(comm, np.random.default_rng(11), n, parts, nlevels=3, bottom=0, bvar=False,
-                       fused=fused)
+                       fused=fused, overlap=overlap)
         amg = S["amg"]
         amg.init_residual(S["fphi"], S["frhs"], S["fres"])
         norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
@@ -336,6 +340,29 @@ def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused):
     assert onorms == res[0][0]
     assert np.array_equal(o.get(0, oracle.PHI, 0), res[0][1])
     assert onorms[1] < onorms[0]
+
+
+@pytest.mark.parametrize("rccl", [False, True])
+def test_overlapped_halo_large_periodic_box_bitwise(rng, rccl):
+    # 192^3 periodic single box (six exchanged faces): the side-stream slab
+    # sweeps + ghost-shell exchange must reproduce the serial schedule bit for
+    # bit (a missing stream dependency shows up here as a changed result)
+    if rccl:
+        c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+        c.set_self_messages(True)
+    else:
+        c = mg.Comm()
+    n = 192
+    out = []
+    for overlap in (0, 2):
+        S = build_pair(c, np.random.default_rng(5), n, (1, 1, 1), periodic=(1, 1, 1), alpha=1.0,
+                       nlevels=3, bottom=0, bvar=False, overlap=overlap)
+        amg = S["amg"]
+        amg.init_residual(S["fphi"], S["frhs"], S["fres"])
+        norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(3)]
+        out.append((norms, S["fphi"].download(0)))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])
 
 
 @pytest.mark.parametrize("shape,lo", [((70, 20, 13), (0, 0, 0)), ((37, 9, 40), (3, -5, 7)),

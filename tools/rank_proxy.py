@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Per-rank proxy of the N-GPU strong-scaling run on one GPU.
+
+At N = 8 each rank owns one 256^3 box of the 512^3 domain and exchanges its
+faces with RCCL.  One GPU cannot run 8 RCCL ranks, so this times one 256^3
+box, periodic in every direction (all six faces exchanged, with itself),
+with the exchange routed through RCCL self send/recv (the pack -> grouped
+ncclSend/ncclRecv -> unpack path the ranks use).  It prints V-cycles/s for
+the given overlap mode; xGMI latency is not modelled.
+
+usage: rank_proxy.py [--size 256] [--overlap 0|1|2] [--steps 30]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--overlap", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--levels", type=int, default=3)
+    ap.add_argument("--local", action="store_true", help="local copies instead of RCCL")
+    args = ap.parse_args()
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.params import read_params_file
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prm = read_params_file(os.path.join(root, "tests", "golden", "params.txt"))
+    n = args.size
+    if args.local:
+        comm = mg.Comm()
+    else:
+        comm = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+        comm.set_self_messages(True)
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    grid = mg.Grid(comm, dom, [dom], prm.L / n, periodic=(1, 1, 1))
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    bh = prm.bh()
+    mg.set_binary_bh_coefs(fa, frhs, bh)
+    fb.set_val(1.0)
+    fphi.set_zero()
+    op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, coefficient_average_type=1,
+                           prolong_type=1, relax_mode=1, fused_smoother=1,
+                           overlap_exchange=args.overlap)
+    fac = mg.defineOperatorFactory(grid, fa, fb, op)
+    amg = mg.AMRMultiGrid(fac, mg.SolverParams(max_depth=args.levels - 1, n_pre=4, n_post=4,
+                                               n_bottom=4, bottom_solver=0))
+    amg.init_residual(fphi, frhs, fres, norm_type=0)
+    for _ in range(args.warmup):
+        amg.iteration(fphi, frhs, fres, norm_type=-1)
+    comm.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        amg.iteration(fphi, frhs, fres, norm_type=-1)
+    comm.synchronize()
+    dt = time.perf_counter() - t0
+    r = amg.init_residual(fphi, frhs, fres, norm_type=0)
+    print(json.dumps({"size": n, "overlap": args.overlap, "rccl": not args.local,
+                      "vcycles_per_s": round(args.steps / dt, 2),
+                      "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
+
+
+if __name__ == "__main__":
+    main()
