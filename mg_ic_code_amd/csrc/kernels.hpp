@@ -19,8 +19,8 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
 // Fused red+black sweep (both passes of one levelGSRB, .cpp:290-331) in one
 // launch, staged through LDS, OUT OF PLACE: u_out = sweep(u_in); bit-
 // identical to two in-place gsrb_pass calls with an exchange before each.
-// Domain faces (bcm != 0): the BC images are written into u_in's ghost
-// layer first.  Exchanged faces (bcm == 0): u_in must hold the 2-deep ghost
+// Domain faces (bcm != 0): the BC images are applied to the kernel's LDS
+// copy of u_in (u_in itself is never written).  Exchanged faces (bcm == 0): u_in must hold the 2-deep ghost
 // shell and rhs/a/b ghost layer 1.  zero_in: u_in is identically +0 and is
 // not read (first sweep on a freshly zeroed correction).  acc != nullptr:
 // acc += sweep(u_in) instead of writing u_out (phi += e of the last sweep).

@@ -2,9 +2,9 @@
 //
 // One launch performs both colour passes of levelGSRB
 // (Source/VariableCoeffPoissonOperator.cpp:290-331; arithmetic of
-// GSRBHELMHOLTZVC3D, VariableCoeffPoissonOperatorF.ChF:56-139) on a box whose
-// six faces are all domain faces (one box per level, non-periodic).
-// Results are bit-identical to two per-colour k_gsrb launches (same
+// GSRBHELMHOLTZVC3D, VariableCoeffPoissonOperatorF.ChF:56-139) on one box:
+// domain faces take the BC on the fly, exchanged faces read a 2-deep ghost
+// shell (see gsrb_sweep_fused in kernels.hpp).  Results are bit-identical to two per-colour k_gsrb launches (same
 // expressions, -ffp-contract=off).
 //
 // Design (HBM-bound stencil, ~0.3 flop/B, no MFMA):
@@ -27,7 +27,8 @@
 //     bound at ~1.45 ms / 512^3 sweep: loads whose results merge at a join
 //     point got an s_waitcnt vmcnt(0) right after issue, so nothing stayed in
 //     flight across the barriers.  Hence unconditional clamped loads here and
-//     the BC pre-filled into the input's ghost faces;
+//     the BC applied as planes enter LDS (ghost pairs load the cells they
+//     image and transform them; an earlier separate fill launch cost ~4%);
 //   * `cond ? arr1[i] : arr0[i]` on register arrays (and runtime-indexed
 //     double2 elements) is lowered to scratch: use bsel() on scalars;
 //   * a persistent grid (exactly one wave of workgroups, equal contiguous
@@ -102,16 +103,39 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   auto slot = [](int p) { return ((p % 5) + 5) % 5; };
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
 
-  // region pairs owned by this thread (loads + LDS stores)
+  // region pairs owned by this thread (loads + LDS stores).  The domain BC
+  // is applied on the way into LDS: a pair holding a BC-face ghost loads
+  // the cells the ghost images instead and transforms them (lbc), so the
+  // ghost takes exactly the value ParseBC would write before the pass --
+  // including along exchanged faces, whose shell cells are loaded as they
+  // are.  Cells that are ghosts of two BC faces (never read) get garbage.
   long loff[NL];
-  int lgy[NL];
+  int lgy[NL], lbc[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int c = tid + i * NT;
     const int r = c / PW, m = c - r * PW;
     lgy[i] = y0 - 2 + r;
-    const int gx = min(x0 - 2 + 2 * m, xpmax);
-    loff[i] = c < CP ? (long)gx + (long)clampi(lgy[i], -2, ny + 1) * sy : 0;
+    const int ps = x0 - 2 + 2 * m;  // first x of the pair
+    int gx = min(ps, xpmax), bx = 0, gy = clampi(lgy[i], -2, ny + 1), by = 0;
+    if (g.bcm[0] && ps == -2) {  // (-2, -1) <- image of (0): load (0, 1)
+      gx = 0;
+      bx = 1;
+    } else if (g.bcm[1] && ps == nx) {  // (nx, nx+1) <- image of nx-1: load (nx-2, nx-1)
+      gx = nx - 2;
+      bx = 2;
+    } else if (g.bcm[1] && ps == nx - 1) {  // (nx-1, nx): element 1 <- image of element 0
+      bx = 3;
+    }
+    if (g.bcm[2] && lgy[i] == -1) {
+      gy = 0;
+      by = 1;
+    } else if (g.bcm[3] && lgy[i] == ny) {
+      gy = ny - 1;
+      by = 2;
+    }
+    lbc[i] = c < CP ? bx | (by << 2) : 0;
+    loff[i] = c < CP ? (long)gx + (long)gy * sy : 0;
   }
   // ring pairs owned by this thread (coefficient loads, red/black updates)
   long roff[NP], rcoff[NP];
@@ -138,7 +162,9 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   double an0[NP], an1[NP], ak0[NP], ak1[NP];  // ACC: acc pairs of planes p and p-1
 
   auto fetch_u = [&](int p) {
-    const long pz = (long)clampi(p, -2, nz + 1) * sz;
+    // a BC-face ghost plane loads the plane it images
+    const int pp = (g.bcm[4] && p == -1) ? 0 : (g.bcm[5] && p == nz) ? nz - 1 : clampi(p, -2, nz + 1);
+    const long pz = (long)pp * sz;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (ZIN) {  // the input is identically +0 (a freshly zeroed correction)
@@ -153,13 +179,30 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   };
   auto put_u = [&](int p) {
     double *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
+    const int zf = (g.bcm[4] && p == -1) ? 4 : (g.bcm[5] && p == nz) ? 5 : -1;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = tid + i * NT;
       if (NL * NT > CP && c >= CP) continue;
+      double u0 = pu0[i], u1 = pu1[i];
+      if (!ZIN) {  // BC images (a zero input images to zero: homogeneous BC)
+        const int bx = lbc[i] & 3, by = lbc[i] >> 2;
+        if (by) {
+          const int f = 1 + by;
+          u0 = ghost_of(g.bcm[f], g.bcc[f], u0);
+          u1 = ghost_of(g.bcm[f], g.bcc[f], u1);
+        }
+        if (bx == 1) u1 = ghost_of(g.bcm[0], g.bcc[0], u0);
+        else if (bx == 2) u0 = ghost_of(g.bcm[1], g.bcc[1], u1);
+        else if (bx == 3) u1 = ghost_of(g.bcm[1], g.bcc[1], u0);
+        if (zf >= 0) {
+          u0 = ghost_of(g.bcm[zf], g.bcc[zf], u0);
+          u1 = ghost_of(g.bcm[zf], g.bcc[zf], u1);
+        }
+      }
       const int q = (q0 + lgy[i] + p) & 1;  // 1: the red element is the second
-      Rs[c] = bsel(q, pu1[i], pu0[i]);
-      Bs[c] = bsel(q, pu0[i], pu1[i]);
+      Rs[c] = bsel(q, u1, u0);
+      Bs[c] = bsel(q, u0, u1);
     }
   };
   auto fetch_c = [&](int p) {
@@ -421,10 +464,9 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
     B[c] = bsel(q, u0, u1);
   }
   // 2b. the domain BC, in LDS: each BC-face ghost of the region takes the
-  // image of the cell it touches -- the values k_fill_bc_faces would have
-  // written into u_in (same cells, including the extension onto exchanged
-  // faces' ghost layers), so the input is never written and the sweep is one
-  // launch.  Only tiles touching a BC face (a workgroup-uniform test) pay.
+  // image of the cell it touches -- the values ParseBC writes before the
+  // pass (same cells, including the extension onto exchanged faces' ghost
+  // layers), so the input is never written and the sweep is one launch.  Only tiles touching a BC face (a workgroup-uniform test) pay.
   // (the region reaches the hi ghost at n once x0 + TX + 1 >= n)
   if (!ZIN && ((g.bcm[0] && x0 == 0) || (g.bcm[1] && x0 + TX + 1 >= nx) || (g.bcm[2] && y0 == 0) ||
                (g.bcm[3] && y0 + TY + 1 >= ny) || (g.bcm[4] && z0 == 0) ||
@@ -813,38 +855,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused2x(double *__restrict__ uo,
   }
 }
 
-// The ghost layer of every BC face of one box in one launch.  Along an
-// exchanged face the range extends one cell onto that face's ghost layer:
-// the sweep recomputes the neighbour's red values there, and the neighbour
-// would have seen its own BC image in these cells (ParseBC before each
-// pass).  Run after the shell exchange, which supplies the centre values.
-__global__ void k_fill_bc_faces(double *__restrict__ u, const BoxArgs g) {
-  const int face = blockIdx.z;
-  if (!g.bcm[face]) return;
-  const int dir = face >> 1, side = face & 1;
-  const int d0 = dir == 0 ? 1 : 0, d1 = dir == 2 ? 1 : 2;  // in-face directions
-  const int n[3] = {g.nx, g.ny, g.nz};
-  const int lo0 = g.bcm[2 * d0] ? 0 : -1, hi0 = g.bcm[2 * d0 + 1] ? n[d0] - 1 : n[d0];
-  const int lo1 = g.bcm[2 * d1] ? 0 : -1, hi1 = g.bcm[2 * d1 + 1] ? n[d1] - 1 : n[d1];
-  const int a0 = lo0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
-  const int a1 = lo1 + (int)blockIdx.y;
-  if (a0 > hi0 || a1 > hi1) return;
-  int c[3];
-  c[dir] = side == 0 ? 0 : n[dir] - 1;
-  c[d0] = a0;
-  c[d1] = a1;
-  const long st = dir == 0 ? 1 : dir == 1 ? g.sy : g.sz;
-  const long near = (long)c[0] + (long)c[1] * g.sy + (long)c[2] * g.sz;
-  u[near + (side == 0 ? -st : st)] = ghost_of(g.bcm[face], g.bcc[face], u[near]);
-}
-
 }  // namespace
-
-static void fill_bc_faces(double *u, const BoxArgs &g, hipStream_t st) {
-  const int m = (g.nx > g.ny ? g.nx : g.ny) + 2;
-  const int m1 = (g.ny > g.nz ? g.ny : g.nz) + 2;
-  k_fill_bc_faces<<<dim3((unsigned)((m + 255) / 256), (unsigned)m1, 6), dim3(256), 0, st>>>(u, g);
-}
 
 // workgroups of kernel `k` the whole device holds at once
 template <class K>
@@ -879,7 +890,7 @@ template <int TX, int TY, int NT>
 static void launch_fused6(double *u_out, double *u_in, const double *rhs, const double *a,
                           const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                           double *acc, hipStream_t st) {
-  if (!zero_in) fill_bc_faces(u_in, g, st);  // BC image of every face into the input's ghost layer
+  // the domain BC is applied as the planes enter LDS (no fill launch)
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
   static const int slots = resident_slots(k_gsrb_fused6<TX, TY, NT, false, false, false>, NT);
   static const int kc_mode = [] {
