@@ -50,6 +50,7 @@ def counters(path):
         for d, name, v in rows:
             if d >= top / 1.8:
                 vals[k][name].append(v)
+                vals[k]["_dur"].append(d)
     return vals
 
 
@@ -72,15 +73,15 @@ def main():
 
     fetch = counters(os.path.join(d, "pmc_fetch", f"{args.tag}_counter_collection.csv"))
     write = counters(os.path.join(d, "pmc_write", f"{args.tag}_counter_collection.csv"))
-    # finest level = the largest grid of the smoother kernel; among its
-    # instantiations the one launched most (the steady-state sweep)
+    # the dominant smoother launch: the (kernel, grid) with the most total
+    # time in its finest-level cluster (the steady-state fine sweep)
     keys = [k for k in fetch if k[0].startswith(args.kernel)]
     if not keys:
         raise SystemExit("no smoother dispatches in the PMC passes")
-    k = max(keys, key=lambda kk: (kk[1], len(fetch[kk]["FETCH_SIZE"])))
+    k = max(keys, key=lambda kk: sum(fetch[kk]["_dur"]))
     fb = sum(fetch[k]["FETCH_SIZE"]) / len(fetch[k]["FETCH_SIZE"]) * 1024 * 2
     wb = sum(write[k]["WRITE_SIZE"]) / len(write[k]["WRITE_SIZE"]) * 1024
-    fused = "fused" in k[0]
+    fused = "fused" in k[0] or "block" in k[0]
     out_path = os.path.join(ROOT, "profiles", "traffic_smoother.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
     data[f"n{args.n}_w{args.world}_{'fused' if fused else 'pass'}"] = {
