@@ -29,6 +29,16 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       double *acc, int kind, hipStream_t st);
+// The last pre-smoothing sweep fused with restrictResidual: u_out = sweep(
+// u_in) as gsrb_sweep_fused, and rc (the coarse box, coarsen(box, 2)) = the
+// restricted residual rhs - L(u_out) with the homogeneous BC of g (exactly
+// restrict_residual(rc, cg, u_out, rhs, a, b, g, s) with rc zeroed first).
+// Applies to boxes whose six faces are domain faces, even extents, taking
+// the z-streaming kernel (see _applies); the caller falls back otherwise.
+bool gsrb_sweep_fused_restrict_applies(const BoxArgs &g, const BoxArgs &cg, int kind);
+void gsrb_sweep_fused_restrict(double *u_out, double *u_in, const double *rhs, const double *a,
+                               const double *b, const BoxArgs &g, const StencilCoefs &s,
+                               double *rc, const BoxArgs &cg, hipStream_t st);
 // The same sweep, computed only on the cells within `depth` of each
 // exchanged face (bcm == 0): the part of u_out the neighbours' ghost shells
 // need.  Values are identical to gsrb_sweep_fused's, so it may run on a

@@ -266,8 +266,9 @@ bool VariableCoeffPoissonOperator::overlapApplies() const {
   return true;
 }
 
-void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
-                                              bool zero_in, LevelData *acc, int flags) {
+bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
+                                              bool zero_in, LevelData *acc, int flags,
+                                              LevelData *rst) {
   resetLambda();  // .cpp:283
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
@@ -299,6 +300,16 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     evM = grid->comm->event(0);
     evE = grid->comm->event(1);
   }
+  // the last sweep restricts too (single sweep kernel over every box)
+  bool restrict_last = rst != nullptr && !acc && !(zero_in && n == 1) && !halo && per == 1;
+  if (restrict_last) {
+    const Grid &cg = *rst->grid;
+    restrict_last = cg.nlocal() == grid->nlocal();
+    for (int b = 0; restrict_last && b < grid->nlocal(); ++b)
+      restrict_last = cg.geom[b].valid == grid->geom[b].valid.coarsened(2) &&
+                      kern::gsrb_sweep_fused_restrict_applies(args_hom_[b], cg.box_args_plain(b),
+                                                              prm.fused_smoother);
+  }
   bool side_pending = false;
   for (int it = 0; it < n;) {
     const bool zin = zero_in && it == 0;
@@ -318,6 +329,10 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
       if (k == 2)  // two sweeps in one launch (temporal blocking)
         kern::gsrb_sweep_fused2x(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
                                  args_hom_[b], s, zin, st);
+      else if (last && restrict_last)  // + restrictResidual(rst, result, rhs)
+        kern::gsrb_sweep_fused_restrict(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b],
+                                        m_bCoef->p[b], args_hom_[b], s, rst->p[b],
+                                        rst->grid->box_args_plain(b), st);
       else
         kern::gsrb_sweep_fused(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
                                args_hom_[b], s, zin, last && acc ? acc->p[b] : nullptr,
@@ -337,7 +352,7 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     it += k;
   }
   if (side_pending) MGIC_HIP(hipStreamWaitEvent(st, evE, 0));
-  if (acc) return;   // the last sweep went into acc; dpsi is scratch now
+  if (acc) return false;  // the last sweep went into acc; dpsi is scratch now
   if (src != &dpsi) {  // the result sits in the scratch buffer
     for (int b = 0; b < grid->nlocal(); ++b)
       kern::blas(0, dpsi.p[b], src->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
@@ -345,6 +360,7 @@ void VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   } else if (want_out && !overlap) {
     dpsi.exchange(st);
   }
+  return restrict_last;
 }
 
 void VariableCoeffPoissonOperator::relaxAccumulate(LevelData &e, const LevelData &r, int n,
@@ -367,6 +383,19 @@ void VariableCoeffPoissonOperator::relaxFromZero(LevelData &e, const LevelData &
   setToZero(e);
   relax(e, r, n);
   if (flags & kHaloOut) e.exchange(stream());
+}
+
+bool VariableCoeffPoissonOperator::relaxRestrict(LevelData &e, const LevelData &r, int n,
+                                                 bool zero_in, int flags, LevelData &resC) {
+  if (n > 0 && prm.relax_mode == 1 && fusedSmootherApplies()) {
+    resetLambda();
+    return fusedRelax(e, r, n, zero_in, nullptr, flags, &resC);
+  }
+  if (zero_in)
+    relaxFromZero(e, r, n, flags);
+  else
+    relaxFlags(e, r, n, flags);
+  return false;
 }
 
 void VariableCoeffPoissonOperator::relaxFlags(LevelData &e, const LevelData &r, int n,
@@ -751,18 +780,13 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
     if (phi_acc) op.incr(*phi_acc, e, 1.0);
     return;
   }
-  // pre-smoothing leaves e's face ghosts exchanged for the restriction
-  if (e_zero)
-    op.relaxFromZero(e, r, prm.n_pre, rf | kHaloOut);
-  else
-    op.relaxFlags(e, r, prm.n_pre, rf | kHaloOut);
+  // pre-smoothing leaves e's face ghosts exchanged for the restriction, or
+  // restricts in its last sweep
   Level &N = levels_[d + 1];
-  if (!N.agg) {
-    op.restrictResidual(*N.r, e, r, false);
-  } else {
-    op.restrictResidual(*N.r_stage, e, r, false);
-    N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
-  }
+  LevelData &rc = N.agg ? *N.r_stage : *N.r;
+  if (!op.relaxRestrict(e, r, prm.n_pre, e_zero, rf | kHaloOut, rc))
+    op.restrictResidual(rc, e, r, false);
+  if (N.agg) N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
   // coarse correction e_c = 0 (folded into its first sweep when possible);
   // its last relax exchanges e_c's ghosts for the linear prolongation
   const bool coarse_out = !N.agg && op.prm.prolong_type == 1;

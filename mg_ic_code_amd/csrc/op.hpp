@@ -121,8 +121,10 @@ class VariableCoeffPoissonOperator {
   // dpsi and the scratch buffer; the result always ends in dpsi).
   // zero_in: dpsi is taken as identically zero and not read (its memory
   // need not be zeroed).
-  void fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false,
-                  LevelData *acc = nullptr, int flags = 0);
+  // rst != nullptr: the last sweep also writes restrictResidual(rst, result,
+  // rhs) when the fused kernel can (returns whether it did)
+  bool fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false,
+                  LevelData *acc = nullptr, int flags = 0, LevelData *rst = nullptr);
   bool overlapApplies() const;
   // relax(e, r, n); phi += e -- the increment folded into the last fused
   // sweep (e is left as scratch in that case)
@@ -132,6 +134,11 @@ class VariableCoeffPoissonOperator {
   void relaxFromZero(LevelData &e, const LevelData &r, int n, int flags = 0);
   // relax(e, r, n) with RelaxFlags
   void relaxFlags(LevelData &e, const LevelData &r, int n, int flags);
+  // (e = 0 when zero_in;) relax(e, r, n); and, when the fused sweep can
+  // fold it into its last pass, restrictResidual(resC, e, r) -- returns
+  // whether the restriction was done (else the caller restricts)
+  bool relaxRestrict(LevelData &e, const LevelData &r, int n, bool zero_in, int flags,
+                     LevelData &resC);
 };
 
 // throws kBadArg unless x lives on g's boxes with g's fab geometry

@@ -568,6 +568,348 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
   }
 }
 
+// ---- last pre-smoothing sweep + restrictResidual in one pass -------------
+// The streaming sweep carried one stage deeper so that the residual of the
+// smoothed e can be restricted while its planes are still in LDS
+// (restrictResidual, VariableCoeffPoissonOperator.cpp:151-194 with
+// RESTRICTRESVC3D, .ChF:379-437): at step p the workgroup updates RED on
+// plane p over the tile grown by two and restricts the residual of plane p-3
+// (its neighbours p-4 .. p-2 are final), then updates BLACK on plane p-1
+// over the tile grown by one (written back into LDS) and stores e on plane
+// p-1.  The residual goes into the coarse cells of the tile -- one thread per coarse (x, y) cell, children
+// summed in the Fortran k, j, i order.  rhs/a of the residual come from L2
+// (the sweep loaded them two steps earlier), so the restriction adds no HBM
+// reads: the separate restrict kernel (25 B/cell) disappears.  A 6-plane
+// LDS ring (143 KB at 128x16).  Boxes whose faces are all domain faces (the
+// exchanged-face case would need a 3-deep shell); bit-identical to
+// gsrb_sweep_fused + restrict_residual.
+template <int TX, int TY, int NT>
+struct FRst {
+  static_assert(TX % 2 == 0 && TY % 2 == 0, "even tiles");
+  static_assert((TX / 2) * (TY / 2) == NT, "one thread per coarse (x, y) cell");
+  static constexpr int PW = TX / 2 + 4;  // pairs x0-4 .. x0+TX+3
+  static constexpr int LH = TY + 6;      // rows y0-3 .. y0+TY+2
+  static constexpr int CP = PW * LH;
+  static constexpr int NS = 6;           // LDS planes
+  static constexpr int RW = TX / 2 + 2;  // ring pairs per row (x0-2 .. x0+TX+1)
+  static constexpr int NRP = RW * (TY + 4);  // ring rows y0-2 .. y0+TY+1
+  static constexpr int NL = (CP + NT - 1) / NT;
+  static constexpr int NP = (NRP + NT - 1) / NT;
+};
+
+template <int TX, int TY, int NT, bool BC>
+__global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
+                                                       double *__restrict__ rc,
+                                                       const double *__restrict__ ui,
+                                                       const double *__restrict__ rhs,
+                                                       const double *__restrict__ a,
+                                                       const double *__restrict__ b,
+                                                       const BoxArgs g, const StencilCoefs s,
+                                                       const BoxArgs cg, int kc, int ntx, int nty,
+                                                       int nblocks) {
+  using F = FRst<TX, TY, NT>;
+  constexpr int PW = F::PW, CP = F::CP, NS = F::NS, RW = F::RW, NRP = F::NRP, NL = F::NL,
+                NP = F::NP;
+  __shared__ double R[NS * CP];  // red element of every pair
+  __shared__ double B[NS * CP];  // black element
+  const int bid = blockIdx.x;    // XCD-aware tile order, as k_gsrb_fused6
+  const int q8 = nblocks / 8, r8 = nblocks % 8;
+  const int L = (bid % 8) * q8 + min(bid % 8, r8) + bid / 8;
+  const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
+  const int z0 = (L / (ntx * nty)) * kc, z1 = min(z0 + kc, g.nz);
+  const int tid = threadIdx.x;
+  const long sy = g.sy, sz = g.sz;
+  const int nx = g.nx, ny = g.ny, nz = g.nz;
+  const int xpmax = (nx + 1) & ~1;
+  const int q0 = (x0 + g.glo[0] + g.glo[1] + g.glo[2]) & 1;
+  auto slot = [](int p) { return ((p % NS) + NS) % NS; };
+  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+
+  // region pairs: loads (BC images applied on entry, as k_gsrb_fused6)
+  long loff[NL];
+  int lgy[NL], lbc[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = tid + i * NT;
+    const int r = c / PW, m = c - r * PW;
+    lgy[i] = y0 - 3 + r;
+    const int ps = x0 - 4 + 2 * m;
+    int gx = clampi(ps, -2, xpmax), bx = 0, gy = clampi(lgy[i], -2, ny + 1), by = 0;
+    if (g.bcm[0] && ps == -2) {
+      gx = 0;
+      bx = 1;
+    } else if (g.bcm[1] && ps == nx) {
+      gx = nx - 2;
+      bx = 2;
+    } else if (g.bcm[1] && ps == nx - 1) {
+      bx = 3;
+    }
+    if (g.bcm[2] && lgy[i] == -1) {
+      gy = 0;
+      by = 1;
+    } else if (g.bcm[3] && lgy[i] == ny) {
+      gy = ny - 1;
+      by = 2;
+    }
+    lbc[i] = c < CP ? bx | (by << 2) : 0;
+    loff[i] = c < CP ? (long)gx + (long)gy * sy : 0;
+  }
+  // ring pairs (tile + 2): coefficient loads, red / black updates, stores
+  long rcoff[NP];
+  int rgy[NP], rgx0[NP], rci[NP], rfl[NP];  // rfl: 1 red row, 2 black row, 4 tile
+  const int rxlo = max(x0 - 2, 0), rxhi = min(x0 + TX + 1, nx - 1);
+  const int rylo = max(y0 - 2, 0), ryhi = min(y0 + TY + 1, ny - 1);
+  const int bxlo = max(x0 - 1, 0), bxhi = min(x0 + TX, nx - 1);
+  const int bylo = max(y0 - 1, 0), byhi = min(y0 + TY, ny - 1);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int c = tid + i * NT;
+    const int rr = c / RW, mm = c - rr * RW;
+    rgy[i] = y0 - 2 + rr;
+    rgx0[i] = x0 - 2 + 2 * mm;
+    rcoff[i] = c < NRP ? (long)clampi(rgx0[i], -2, xpmax) + (long)clampi(rgy[i], -1, ny) * sy : 0;
+    rci[i] = (rr + 1) * PW + mm + 1;
+    const int red = c < NRP && rgy[i] >= rylo && rgy[i] <= ryhi;
+    const int blk = c < NRP && rgy[i] >= bylo && rgy[i] <= byhi;
+    const int tile = c < NRP && rgy[i] >= y0 && rgy[i] < y0 + TY && rgy[i] < ny &&
+                     rgx0[i] >= x0 && rgx0[i] < x0 + TX && rgx0[i] < nx;
+    rfl[i] = red | (blk << 1) | (tile << 2);
+  }
+  // the coarse cell of this thread: fine pair (x0 + 2cx, +1), rows y0 + 2cy + {0, 1}
+  const int cx = tid % (TX / 2), cy = tid / (TX / 2);
+  const int fxr = x0 + 2 * cx, fyr = y0 + 2 * cy;
+  const bool rown = fxr < nx && fyr < ny;
+  const int cci = (2 * cy + 3) * PW + cx + 2;  // LDS index of the (fxr, fyr) pair
+  const long frow = (long)min(fxr, xpmax) + (long)min(fyr, ny - 1) * sy;
+
+  double pu0[NL], pu1[NL];
+  double cr0[NP], cr1[NP], ca0[NP], ca1[NP], cb0[NP], cb1[NP];
+  double nr0[NP], nr1[NP], na0[NP], na1[NP], nb0[NP], nb1[NP];
+  double kr[NP], ka[NP], kb[NP];
+  double2 qr[2], qa[2], qb[2];  // rhs/a/b of the residual plane, (fxr, fyr + jj)
+  double2 wr[2], wa[2], wb[2];  // ... of the next residual plane (one step ahead)
+  double sum = 0.0;
+
+  auto fetch_u = [&](int p) {
+    const int pp = (g.bcm[4] && p == -1) ? 0 : (g.bcm[5] && p == nz) ? nz - 1 : clampi(p, -2, nz + 1);
+    const long pz = (long)pp * sz;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const double2 v = *reinterpret_cast<const double2 *>(ui + loff[i] + pz);
+      pu0[i] = v.x;
+      pu1[i] = v.y;
+    }
+  };
+  auto put_u = [&](int p) {
+    double *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
+    const int zf = (g.bcm[4] && p == -1) ? 4 : (g.bcm[5] && p == nz) ? 5 : -1;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + i * NT;
+      if (NL * NT > CP && c >= CP) continue;
+      double u0 = pu0[i], u1 = pu1[i];
+      const int bx = lbc[i] & 3, by = lbc[i] >> 2;
+      if (by) {
+        const int f = 1 + by;
+        u0 = ghost_of(g.bcm[f], g.bcc[f], u0);
+        u1 = ghost_of(g.bcm[f], g.bcc[f], u1);
+      }
+      if (bx == 1) u1 = ghost_of(g.bcm[0], g.bcc[0], u0);
+      else if (bx == 2) u0 = ghost_of(g.bcm[1], g.bcc[1], u1);
+      else if (bx == 3) u1 = ghost_of(g.bcm[1], g.bcc[1], u0);
+      if (zf >= 0) {
+        u0 = ghost_of(g.bcm[zf], g.bcc[zf], u0);
+        u1 = ghost_of(g.bcm[zf], g.bcc[zf], u1);
+      }
+      const int q = (q0 + lgy[i] + p) & 1;
+      Rs[c] = bsel(q, u1, u0);
+      Bs[c] = bsel(q, u0, u1);
+    }
+  };
+  auto fetch_c = [&](int p) {
+    const long pz = (long)clampi(p, -1, nz) * sz;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const long off = rcoff[i] + pz;
+      const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
+      const double2 va = *reinterpret_cast<const double2 *>(a + off);
+      const double2 vb = BC ? make_double2(s.bval, s.bval) : *reinterpret_cast<const double2 *>(b + off);
+      nr0[i] = vr.x; nr1[i] = vr.y;
+      na0[i] = va.x; na1[i] = va.y;
+      nb0[i] = vb.x; nb1[i] = vb.y;
+    }
+  };
+  auto fetch_q = [&](int k) {  // the residual plane's coefficients (L2: loaded by the sweep)
+    const long pz = (long)clampi(k, 0, nz - 1) * sz;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const long off = frow + (long)(jj && fyr + 1 < ny ? sy : 0) + pz;
+      wr[jj] = *reinterpret_cast<const double2 *>(rhs + off);
+      wa[jj] = *reinterpret_cast<const double2 *>(a + off);
+      wb[jj] = BC ? make_double2(s.bval, s.bval) : *reinterpret_cast<const double2 *>(b + off);
+    }
+  };
+  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
+                 double rv, double av, double bv) -> double {
+    const double tx = (xp + xm) - 2.0 * uc;
+    const double ty = (yp + ym) - 2.0 * uc;
+    const double tz = (zp + zm) - 2.0 * uc;
+    const double lap = (tx + ty) + tz;                     // .ChF:111-120
+    double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
+    const double ldpsi = lap * s.dxinv * bv;               // .ChF:122
+    lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
+    const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
+    return uc - lam * (lofdpsi - rv);                      // .ChF:127-128
+  };
+
+  fetch_u(z0 - 3);
+  put_u(z0 - 3);
+  fetch_u(z0 - 2);
+  put_u(z0 - 2);
+  fetch_u(z0 - 1);
+  fetch_c(z0 - 2);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    cr0[i] = nr0[i]; cr1[i] = nr1[i];
+    ca0[i] = na0[i]; ca1[i] = na1[i];
+    cb0[i] = nb0[i]; cb1[i] = nb1[i];
+  }
+  for (int p = z0 - 2; p <= z1 + 2; ++p) {
+    put_u(p + 1);
+    fetch_u(p + 2);
+    fetch_c(p + 1);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {  // plane p-3's (fetched last step)
+      qr[jj] = wr[jj];
+      qa[jj] = wa[jj];
+      qb[jj] = wb[jj];
+    }
+    if (p - 2 >= z0 && p - 2 < z1) fetch_q(p - 2);
+    __syncthreads();
+    if (p >= 0 && p <= nz - 1 && p <= z1 + 1) {  // RED of plane p on the tile grown by two
+      double *Rs = R + slot(p) * CP;
+      const double *Bs = B + slot(p) * CP;
+      const double *Bm = B + slot(p - 1) * CP;
+      const double *Bp = B + slot(p + 1) * CP;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int q = (q0 + rgy[i] + p) & 1;
+        const int gx = rgx0[i] + q;
+        if (!(rfl[i] & 1) || gx < rxlo || gx > rxhi) continue;
+        const int ci = rci[i];
+        const double xm = q ? Bs[ci] : Bs[ci - 1];
+        const double xp = q ? Bs[ci + 1] : Bs[ci];
+        Rs[ci] = upd(Rs[ci], xm, xp, Bs[ci - PW], Bs[ci + PW], Bm[ci], Bp[ci],
+                     bsel(q, cr1[i], cr0[i]), bsel(q, ca1[i], ca0[i]), bsel(q, cb1[i], cb0[i]));
+      }
+    }
+    // residual of plane p-3 (final: its black was updated last step) -- it
+    // reads planes p-4 .. p-2 while RED writes plane p
+    const int kr3 = p - 3;
+    if (kr3 >= z0 && kr3 < z1) {  // residual of plane p-3 into the coarse cell
+      const double *Rs = R + slot(kr3) * CP, *Bs = B + slot(kr3) * CP;
+      const double *Rm = R + slot(kr3 - 1) * CP, *Bm = B + slot(kr3 - 1) * CP;
+      const double *Rp = R + slot(kr3 + 1) * CP, *Bp = B + slot(kr3 + 1) * CP;
+      const double denom = 2 * 2 * 2;  // .ChF:402
+      if ((kr3 & 1) == 0) sum = 0.0;  // rc zeroed first (.cpp:177)
+      // the colour of a row is uniform over the workgroup (fyr even), so each
+      // element comes from R or B by a uniform choice: element e of a pair
+      // is red iff e == (q0 + row + plane) & 1
+      auto el = [&](const double *Rp_, const double *Bp_, int ci, int e, int row, int k) {
+        return (e == ((q0 + row + k) & 1)) ? Rp_[ci] : Bp_[ci];
+      };
+      double v[4][2], zm[2][2], zp[2][2], xl[2], xr[2];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)  // rows fyr-1 .. fyr+2 of plane k
+#pragma unroll
+        for (int e = 0; e < 2; ++e) v[r][e] = el(Rs, Bs, cci + (r - 1) * PW, e, fyr + r - 1, kr3);
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int ci = cci + jj * PW, row = fyr + jj;
+        xl[jj] = el(Rs, Bs, ci - 1, 1, row, kr3);
+        xr[jj] = el(Rs, Bs, ci + 1, 0, row, kr3);
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          zm[jj][e] = el(Rm, Bm, ci, e, row, kr3 - 1);
+          zp[jj][e] = el(Rp, Bp, ci, e, row, kr3 + 1);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int j = fyr + jj;
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const int i = fxr + ii;
+          const double uc = v[jj + 1][ii];
+          double vxm = ii ? v[jj + 1][0] : xl[jj];
+          double vxp = ii ? xr[jj] : v[jj + 1][1];
+          double vym = v[jj][ii], vyp = v[jj + 2][ii];
+          double vzm = zm[jj][ii], vzp = zp[jj][ii];
+          if (i == 0 && g.bcm[0]) vxm = ghost_of(g.bcm[0], g.bcc[0], uc);
+          if (i == nx - 1 && g.bcm[1]) vxp = ghost_of(g.bcm[1], g.bcc[1], uc);
+          if (j == 0 && g.bcm[2]) vym = ghost_of(g.bcm[2], g.bcc[2], uc);
+          if (j == ny - 1 && g.bcm[3]) vyp = ghost_of(g.bcm[3], g.bcc[3], uc);
+          if (kr3 == 0 && g.bcm[4]) vzm = ghost_of(g.bcm[4], g.bcc[4], uc);
+          if (kr3 == nz - 1 && g.bcm[5]) vzp = ghost_of(g.bcm[5], g.bcc[5], uc);
+          const double tx = (vxp + vxm) - 2.0 * uc;
+          const double ty = (vyp + vym) - 2.0 * uc;
+          const double tz = (vzp + vzm) - 2.0 * uc;
+          double ldpsi = (tx + ty) + tz;                                        // .ChF:416-425
+          double lofdpsi = s.alpha * (ii ? qa[jj].y : qa[jj].x) * uc;          // .ChF:411-412
+          ldpsi = ldpsi * s.dxinv * s.beta * (ii ? qb[jj].y : qb[jj].x);       // .ChF:427
+          lofdpsi = lofdpsi - ldpsi;                                            // .ChF:429
+          sum = sum + ((ii ? qr[jj].y : qr[jj].x) - lofdpsi) / denom;          // .ChF:431-432
+        }
+      }
+      if ((kr3 & 1) == 1 && rown)
+        rc[(long)(fxr >> 1) + (long)(fyr >> 1) * cg.sy + (long)(kr3 >> 1) * cg.sz] = sum;
+    }
+    __syncthreads();
+    const int k = p - 1;
+    if (k >= 0 && k <= nz - 1 && k >= z0 - 1 && k <= z1) {  // BLACK of plane k, tile + 1
+      const double *Rs = R + slot(k) * CP;
+      double *Bs = B + slot(k) * CP;
+      const double *Rm = R + slot(k - 1) * CP;
+      const double *Rp = R + slot(k + 1) * CP;
+      double *dst = uo + (long)k * sz;
+      const bool store = k >= z0 && k < z1;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        if (!(rfl[i] & 2)) continue;
+        const int qb = 1 - ((q0 + rgy[i] + k) & 1);  // 1: the black element is the second
+        const int gx = rgx0[i] + qb;
+        const int ci = rci[i];
+        const double red = Rs[ci];
+        double blk = Bs[ci];
+        if (gx >= bxlo && gx <= bxhi) {
+          const double xm = qb ? Rs[ci] : Rs[ci - 1];
+          const double xp = qb ? Rs[ci + 1] : Rs[ci];
+          blk = upd(blk, xm, xp, Rs[ci - PW], Rs[ci + PW], Rm[ci], Rp[ci], kr[i], ka[i], kb[i]);
+          Bs[ci] = blk;
+        }
+        if (store && (rfl[i] & 4)) {
+          double2 w;
+          w.x = bsel(qb, red, blk);
+          w.y = bsel(qb, blk, red);
+          const long off = (long)rgx0[i] + (long)rgy[i] * sy;
+          if (rgx0[i] + 1 < nx) *reinterpret_cast<double2 *>(dst + off) = w;
+          else dst[off] = w.x;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {  // plane p's black coefficients wait one step
+      const int qb = 1 - ((q0 + rgy[i] + p) & 1);
+      kr[i] = bsel(qb, cr1[i], cr0[i]);
+      ka[i] = bsel(qb, ca1[i], ca0[i]);
+      kb[i] = bsel(qb, cb1[i], cb0[i]);
+      cr0[i] = nr0[i]; cr1[i] = nr1[i];
+      ca0[i] = na0[i]; ca1[i] = na1[i];
+      cb0[i] = nb0[i]; cb1[i] = nb1[i];
+    }
+  }
+}
+
 // ---- two sweeps per launch (temporal blocking) ---------------------------
 // The same streaming scheme carried two sweeps deep: at step p the workgroup
 // updates RED(sweep 1) on plane p, BLACK(1) on p-1, RED(2) on p-2 and
@@ -1055,6 +1397,48 @@ void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const doub
     case 2: launch_fused6<256, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
     default: launch_fused6<128, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
   }
+}
+
+template <int TX, int TY, int NT>
+static void launch_fused_rst(double *u_out, double *u_in, const double *rhs, const double *a,
+                             const double *b, const BoxArgs &g, const StencilCoefs &s, double *rc,
+                             const BoxArgs &cg, hipStream_t st) {
+  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
+  static const int slots = resident_slots(k_gsrb_fused_rst<TX, TY, NT, false>, NT);
+  int kc = choose_kc(ntx * nty, g.nz, slots, 6);
+  kc += kc & 1;  // coarse planes never straddle two workgroups
+  if (kc > g.nz) kc = g.nz;
+  const int ntz = (g.nz + kc - 1) / kc;
+  const int nblocks = ntx * nty * ntz;
+  const dim3 grid((unsigned)nblocks), block(NT);
+  if (s.bconst)
+    k_gsrb_fused_rst<TX, TY, NT, true><<<grid, block, 0, st>>>(u_out, rc, u_in, rhs, a, b, g, s, cg,
+                                                              kc, ntx, nty, nblocks);
+  else
+    k_gsrb_fused_rst<TX, TY, NT, false><<<grid, block, 0, st>>>(u_out, rc, u_in, rhs, a, b, g, s, cg,
+                                                               kc, ntx, nty, nblocks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    throw Error(kHipErr, std::string("fused sweep+restrict launch: ") + hipGetErrorString(e));
+}
+
+bool gsrb_sweep_fused_restrict_applies(const BoxArgs &g, const BoxArgs &cg, int kind) {
+  static const int enabled = [] {
+    const char *e = getenv("MGIC_FUSED_RESTRICT");
+    return e ? atoi(e) : 1;
+  }();
+  if (!enabled || kind == 0 || kind == 3) return false;
+  if (kind != 2 && (long)g.nx * g.ny * g.nz <= block_max_cells()) return false;  // block kernel
+  for (int f = 0; f < 6; ++f)
+    if (!g.bcm[f]) return false;  // exchanged faces would need a 3-deep shell
+  if ((g.nx | g.ny | g.nz) & 1) return false;
+  return cg.nx * 2 == g.nx && cg.ny * 2 == g.ny && cg.nz * 2 == g.nz;
+}
+
+void gsrb_sweep_fused_restrict(double *u_out, double *u_in, const double *rhs, const double *a,
+                               const double *b, const BoxArgs &g, const StencilCoefs &s,
+                               double *rc, const BoxArgs &cg, hipStream_t st) {
+  launch_fused_rst<128, 16, 512>(u_out, u_in, rhs, a, b, g, s, rc, cg, st);
 }
 
 void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const double *a,

@@ -252,6 +252,43 @@ def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused, overla
 
 
 @pytest.mark.parametrize("fused", [2, 3])
+@pytest.mark.parametrize("bvar", [False, True])
+def test_vcycle_ragged_mixed_bc_bitwise(rng, comm, fused, bvar):
+    # non-cubic box at an odd global offset, Dirichlet/Neumann faces with a BC
+    # value: covers the sweep+restriction kernel (fused=2: the last
+    # pre-smoothing sweep restricts in the same pass) against the oracle
+    shape = (48, 40, 56)  # x, y, z
+    lo = (-16, 8, 32)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    dx = 0.37
+    bc_lo, bc_hi, bcv = (0, 1, 0), (1, 0, 1), 0.25
+    nz, ny, nx = shape[2], shape[1], shape[0]
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    b = rng.uniform(0.5, 2.0, (nz, ny, nx)) if bvar else np.ones((nz, ny, nx))
+    rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    grid = mg.Grid(comm, dom, [dom], dx)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    fa.upload(0, a)
+    fb.upload(0, b)
+    frhs.upload(0, rhs)
+    fphi.set_zero()
+    prm = mg.OperatorParams(alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bcv,
+                            coefficient_average_type=1, prolong_type=1, fused_smoother=fused)
+    amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, prm),
+                          mg.SolverParams(max_depth=2, bottom_solver=0))
+    o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi,
+                        bc_value=bcv, nlevels=3, avg_type=1, prolong_type=1, bottom_solver=0)
+    for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs)):
+        o.set(0, f, 0, arr)
+    o.setup()
+    amg.init_residual(fphi, frhs, fres)
+    o.init_residual(0)
+    for _ in range(3):
+        assert amg.iteration(fphi, frhs, fres, 0) == o.iteration(0)
+    assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
+
+
+@pytest.mark.parametrize("fused", [2, 3])
 @pytest.mark.parametrize("overlap", [0, 2])
 def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, overlap):
     # the RCCL pack -> send/recv -> unpack path, exercised on one GPU by
