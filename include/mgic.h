@@ -47,6 +47,7 @@ typedef struct mgic_factory_s *mgic_factory; /* VariableCoeffPoissonOperatorFact
 typedef struct mgic_op_s *mgic_op;           /* VariableCoeffPoissonOperator */
 typedef struct mgic_mg_s *mgic_mg;           /* AMRMultiGrid on one AMR level */
 typedef struct mgic_plan_s *mgic_plan;       /* host-side view of a Copier plan */
+typedef struct mgic_mixed_s *mgic_mixed;     /* fp32-smoother / fp64-residual V-cycle */
 
 /* Operator constants and ParseBC state (params.txt keys alpha, beta, bc_lo,
  * bc_hi, bc_value, coefficient_average_type; [Chombo] statics). */
@@ -225,6 +226,28 @@ MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_
 MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
                                    mgic_field resid, int norm_type, int homogeneous,
                                    double *norm);
+/* full multigrid on the current resid (as left by init_residual /
+ * iteration): resid restricted to every depth, bottom solve, then per finer
+ * depth e = P e_coarse and `ncycles` V-cycles; phi += e; resid = rhs - L(phi) */
+MGIC_API int mgic_mg_fmg(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
+                         int norm_type, int homogeneous, int ncycles, double *norm);
+
+/* Mixed precision (BASELINE config C5): the same V-cycle schedule with the
+ * correction equation in fp32 (GSRB / restrictResidual / prolongIncrement in
+ * float, coefficients rounded from the fp64 hierarchy), the fine residual
+ * rhs - L(phi) in fp64 rounded once, phi += e in fp64.  Bottom: relax
+ * (n_bottom); no agglomeration.  resid (fp64) may be NULL unless a norm is
+ * requested (norm_type >= 0).  Inhomogeneous BC for the fine residual. */
+MGIC_API int mgic_mixed_create(mgic_factory f, const mgic_mg_params *p, mgic_mixed *out);
+MGIC_API int mgic_mixed_destroy(mgic_mixed m);
+MGIC_API int mgic_mixed_num_depths(mgic_mixed m, int *n);
+MGIC_API int mgic_mixed_init_residual(mgic_mixed m, mgic_field phi, mgic_field rhs,
+                                      mgic_field resid, int norm_type, double *norm);
+MGIC_API int mgic_mixed_iteration(mgic_mixed m, mgic_field phi, mgic_field rhs, mgic_field resid,
+                                  int norm_type, double *norm);
+MGIC_API int mgic_mixed_fmg(mgic_mixed m, mgic_field phi, mgic_field rhs, mgic_field resid,
+                            int norm_type, int ncycles, double *norm);
+
 /* MultilevelLinearOp::preCond: e = 0, then `iters` AMRMultiGrid iterations
  * on (e, r), homogeneous BC (Main_PoissonSolver.cpp:107-117) */
 MGIC_API int mgic_mg_precondition(mgic_mg mg, mgic_field e, mgic_field r, int iters);

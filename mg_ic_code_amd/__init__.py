@@ -12,6 +12,7 @@ from .core import (  # noqa: F401
     Grid,
     LevelData,
     MgicError,
+    MixedMultiGrid,
     MultilevelLinearOp,
     OperatorParams,
     SolverParams,

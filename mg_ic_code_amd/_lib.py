@@ -158,6 +158,13 @@ SIGNATURES = {
     "mgic_mg_iteration": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_precondition": [H, H, H, c_int],
+    "mgic_mg_fmg": [H, H, H, H, c_int, c_int, c_int, PD],
+    "mgic_mixed_create": [H, POINTER(MGParams), PH],
+    "mgic_mixed_destroy": [H],
+    "mgic_mixed_num_depths": [H, PI],
+    "mgic_mixed_init_residual": [H, H, H, H, c_int, PD],
+    "mgic_mixed_iteration": [H, H, H, H, c_int, PD],
+    "mgic_mixed_fmg": [H, H, H, H, c_int, c_int, PD],
     "mgic_solve_params_default": [POINTER(SolveParams)],
     "mgic_mg_solve": [H, H, H, POINTER(SolveParams), PI, PD],
     "mgic_prof_smoother": [c_int, c_long],

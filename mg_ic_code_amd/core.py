@@ -540,6 +540,15 @@ class AMRMultiGrid:
              int(norm_type), int(bool(homogeneous)), ctypes.byref(out))
         return out.value
 
+    def fmg(self, phi: LevelData, rhs: LevelData, resid: LevelData, norm_type: int = 0,
+            homogeneous: bool = False, ncycles: int = 1) -> float:
+        """Full multigrid on the current resid (from init_residual/iteration):
+        phi += FMG correction; resid = rhs - L(phi); returns its norm."""
+        out = ctypes.c_double()
+        call("mgic_mg_fmg", self._h, phi.handle, rhs.handle, resid.handle, int(norm_type),
+             int(bool(homogeneous)), int(ncycles), ctypes.byref(out))
+        return out.value
+
     def solve(self, phi: LevelData, rhs: LevelData, resid: LevelData, max_iter: int = 20,
               eps: float = 1e-10, norm_type: int = 0) -> List[float]:
         """AMRMultiGrid::solve: iterate until norm(resid) <= eps*norm(resid0)."""
@@ -554,6 +563,49 @@ class AMRMultiGrid:
         h = getattr(self, "_h", None)
         if h:
             lib.mgic_mg_destroy(h)
+            self._h = None
+
+
+class MixedMultiGrid:
+    """Mixed-precision V-cycle (BASELINE config C5): the correction equation
+    cycled in fp32 (GSRB / restrictResidual / prolongIncrement in float,
+    coefficients rounded from the fp64 hierarchy), the fine residual
+    rhs - L(phi) in fp64 rounded once, phi += e in fp64.  Bottom: relax."""
+
+    def __init__(self, factory: VariableCoeffPoissonOperatorFactory,
+                 params: Optional[SolverParams] = None):
+        self.factory = factory
+        self.params = params or SolverParams(bottom_solver=0)
+        h = ctypes.c_void_p()
+        p = self.params.to_c()
+        call("mgic_mixed_create", factory.handle, ctypes.byref(p), ctypes.byref(h))
+        self._h = h
+        n = ctypes.c_int()
+        call("mgic_mixed_num_depths", h, ctypes.byref(n))
+        self.num_depths = n.value
+
+    def _run(self, name, phi, rhs, resid, norm_type, *extra):
+        out = ctypes.c_double()
+        call(name, self._h, phi.handle, rhs.handle, resid.handle if resid is not None else None,
+             int(norm_type), *extra, ctypes.byref(out))
+        return out.value
+
+    def init_residual(self, phi: LevelData, rhs: LevelData, resid: Optional[LevelData] = None,
+                      norm_type: int = 0) -> float:
+        return self._run("mgic_mixed_init_residual", phi, rhs, resid, norm_type)
+
+    def iteration(self, phi: LevelData, rhs: LevelData, resid: Optional[LevelData] = None,
+                  norm_type: int = 0) -> float:
+        return self._run("mgic_mixed_iteration", phi, rhs, resid, norm_type)
+
+    def fmg(self, phi: LevelData, rhs: LevelData, resid: Optional[LevelData] = None,
+            norm_type: int = 0, ncycles: int = 1) -> float:
+        return self._run("mgic_mixed_fmg", phi, rhs, resid, norm_type, int(ncycles))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.mgic_mixed_destroy(h)
             self._h = None
 
 

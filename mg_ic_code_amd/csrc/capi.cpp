@@ -4,6 +4,7 @@
 #include <string>
 
 #include "../../include/mgic.h"
+#include "mixed.hpp"
 #include "op.hpp"
 
 using namespace mgic;
@@ -26,6 +27,9 @@ struct mgic_op_s {
 };
 struct mgic_mg_s {
   AMRMultiGrid amg;
+};
+struct mgic_mixed_s {
+  MixedMultiGrid mm;
 };
 struct mgic_plan_s {
   std::shared_ptr<Grid> src, dst;
@@ -797,6 +801,76 @@ MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs, m
     NEED(rhs);
     NEED(resid);
     const double v = mg->amg.initResidual(*phi->f, *rhs->f, *resid->f, norm_type, h != 0);
+    if (norm) *norm = v;
+  });
+}
+
+MGIC_API int mgic_mg_fmg(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
+                         int norm_type, int h, int ncycles, double *norm) {
+  return guard([&] {
+    NEED(mg);
+    NEED(phi);
+    NEED(rhs);
+    NEED(resid);
+    MGIC_CHECK(ncycles >= 1, "ncycles must be >= 1");
+    const double v = mg->amg.fmg(*phi->f, *rhs->f, *resid->f, norm_type, h != 0, ncycles);
+    if (norm) *norm = v;
+  });
+}
+
+// ---------------------------------------------------------------- mixed precision
+MGIC_API int mgic_mixed_create(mgic_factory f, const mgic_mg_params *p, mgic_mixed *out) {
+  return guard([&] {
+    NEED(f);
+    NEED(out);
+    auto *h = new mgic_mixed_s;
+    try {
+      h->mm.define(f->f, to_mg(p));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+MGIC_API int mgic_mixed_destroy(mgic_mixed m) {
+  return guard([&] { delete m; });
+}
+MGIC_API int mgic_mixed_num_depths(mgic_mixed m, int *n) {
+  return guard([&] {
+    NEED(m);
+    NEED(n);
+    *n = m->mm.depths();
+  });
+}
+MGIC_API int mgic_mixed_init_residual(mgic_mixed m, mgic_field phi, mgic_field rhs,
+                                      mgic_field resid, int norm_type, double *norm) {
+  return guard([&] {
+    NEED(m);
+    NEED(phi);
+    NEED(rhs);
+    const double v = m->mm.initResidual(*phi->f, *rhs->f, resid ? resid->f.get() : nullptr, norm_type);
+    if (norm) *norm = v;
+  });
+}
+MGIC_API int mgic_mixed_iteration(mgic_mixed m, mgic_field phi, mgic_field rhs, mgic_field resid,
+                                  int norm_type, double *norm) {
+  return guard([&] {
+    NEED(m);
+    NEED(phi);
+    NEED(rhs);
+    const double v = m->mm.iteration(*phi->f, *rhs->f, resid ? resid->f.get() : nullptr, norm_type);
+    if (norm) *norm = v;
+  });
+}
+MGIC_API int mgic_mixed_fmg(mgic_mixed m, mgic_field phi, mgic_field rhs, mgic_field resid,
+                            int norm_type, int ncycles, double *norm) {
+  return guard([&] {
+    NEED(m);
+    NEED(phi);
+    NEED(rhs);
+    MGIC_CHECK(ncycles >= 1, "ncycles must be >= 1");
+    const double v = m->mm.fmg(*phi->f, *rhs->f, resid ? resid->f.get() : nullptr, norm_type, ncycles);
     if (norm) *norm = v;
   });
 }

@@ -19,10 +19,25 @@ namespace {
 constexpr int TX = 64;  // one wavefront along x
 constexpr int TY = 4;   // 4 waves per block
 
-__device__ __forceinline__ double ghost_of(int mode, double c, double near) {
+template <class T>
+__device__ __forceinline__ T ghost_of(int mode, T c, T near) {
   // DiriBC order 1: 2*value - near (c = 2*value); NeumBC: near (+ isign*dx*value)
   return mode == kBcDirichlet ? (c - near) : (mode == kBcNeumannHom ? near : near + c);
 }
+
+// element type traits for the fp32 (mixed-precision) variants: a lane pair
+// is one 16-B (double) / 8-B (float) access; the stencil constants are
+// rounded to T once (identity for double)
+template <class T> struct Vec2;
+template <> struct Vec2<double> { using type = double2; };
+template <> struct Vec2<float> { using type = float2; };
+template <class T> using V2 = typename Vec2<T>::type;
+template <class T>
+struct SC {
+  T alpha, beta, dxinv, bval;
+  __device__ explicit SC(const StencilCoefs &s)
+      : alpha((T)s.alpha), beta((T)s.beta), dxinv((T)s.dxinv), bval((T)s.bval) {}
+};
 
 // 7-point Laplacian (.ChF:111-120) with the domain BC folded in: a ghost on
 // a domain face is the BC image of the adjacent valid cell, which is the
@@ -113,8 +128,8 @@ __global__ __launch_bounds__(256) void k_residual(double *__restrict__ r,
 // carries u(k-1), u(k) in registers; u(k+1) is the only new u load per cell
 // (the x/y neighbours come from L1/L2, loaded as centres by the neighbours).
 // Same expressions as k_residual.
-template <bool BC>
-__global__ __launch_bounds__(256) void k_residual_z(double *__restrict__ r,
+template <bool BC, class RT>
+__global__ __launch_bounds__(256) void k_residual_z(RT *__restrict__ r,
                                                     const double *__restrict__ u,
                                                     const double *__restrict__ rhs,
                                                     const double *__restrict__ a,
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(256) void k_residual_z(double *__restrict__ r,
     const double tz = (zp + zm) - 2.0 * uc;
     double ldpsi = (tx + ty) + tz;                                  // .ChF:320-329
     ldpsi = ldpsi * s.dxinv * s.beta * (BC ? s.bval : b[idx]);     // .ChF:331
-    r[idx] = res + ldpsi;                                           // .ChF:333
+    r[idx] = (RT)(res + ldpsi);  // .ChF:333 (RT = float: the fp64 residual rounded once)
     um = uc;
     uc = up;
   }
@@ -159,24 +174,26 @@ __global__ __launch_bounds__(256) void k_residual_z(double *__restrict__ r,
 // even cells and the valid-lo is 128-B aligned); all loads are issued
 // unconditionally (ghost addresses are always allocated) and the domain BC
 // is folded afterwards, as in lap7.
-__device__ __forceinline__ double2 ld2(const double *__restrict__ p) {
-  return *reinterpret_cast<const double2 *>(p);
+template <class T>
+__device__ __forceinline__ V2<T> ld2(const T *__restrict__ p) {
+  return *reinterpret_cast<const V2<T> *>(p);
 }
 
-template <bool BC>
-__global__ __launch_bounds__(256) void k_restrict(double *__restrict__ rc, const BoxArgs cg,
-                                                  const double *__restrict__ u,
-                                                  const double *__restrict__ rhs,
-                                                  const double *__restrict__ a,
-                                                  const double *__restrict__ b, const BoxArgs fg,
-                                                  const StencilCoefs s, int accumulate) {
+template <class T, bool BC>
+__global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxArgs cg,
+                                                  const T *__restrict__ u,
+                                                  const T *__restrict__ rhs,
+                                                  const T *__restrict__ a,
+                                                  const T *__restrict__ b, const BoxArgs fg,
+                                                  const StencilCoefs s64, int accumulate) {
+  const SC<T> s(s64);
   const int ci = blockIdx.x * TX + threadIdx.x;
   const int cj = blockIdx.y * TY + threadIdx.y;
   const int ck = blockIdx.z;
   if (ci >= cg.nx || cj >= cg.ny) return;
-  const double denom = 2 * 2 * 2;  // .ChF:402
+  const T denom = (T)(2 * 2 * 2);  // .ChF:402
   const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
-  double sum = accumulate ? rc[cidx] : 0.0;
+  T sum = accumulate ? rc[cidx] : (T)0;
   const int i0 = 2 * ci;
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
@@ -184,30 +201,32 @@ __global__ __launch_bounds__(256) void k_restrict(double *__restrict__ rc, const
     for (int jj = 0; jj < 2; ++jj) {
       const int j = 2 * cj + jj, k = 2 * ck + kk;
       const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
-      const double2 c = ld2(u + row);
-      const double2 ym = ld2(u + row - fg.sy), yp = ld2(u + row + fg.sy);
-      const double2 zm = ld2(u + row - fg.sz), zp = ld2(u + row + fg.sz);
-      const double xl = u[row - 1], xr = u[row + 2];
-      const double2 rv = ld2(rhs + row), av = ld2(a + row);
-      const double2 bv = BC ? make_double2(s.bval, s.bval) : ld2(b + row);
+      const V2<T> c = ld2(u + row);
+      const V2<T> ym = ld2(u + row - fg.sy), yp = ld2(u + row + fg.sy);
+      const V2<T> zm = ld2(u + row - fg.sz), zp = ld2(u + row + fg.sz);
+      const T xl = u[row - 1], xr = u[row + 2];
+      const V2<T> rv = ld2(rhs + row), av = ld2(a + row);
+      V2<T> bv;
+      if (BC) bv.x = bv.y = s.bval;
+      else bv = ld2(b + row);
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
         const int i = i0 + ii;
-        const double uc = ii ? c.y : c.x;
-        double vxm = ii ? c.x : xl, vxp = ii ? xr : c.y;
-        double vym = ii ? ym.y : ym.x, vyp = ii ? yp.y : yp.x;
-        double vzm = ii ? zm.y : zm.x, vzp = ii ? zp.y : zp.x;
-        if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], fg.bcc[0], uc);
-        if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], fg.bcc[1], uc);
-        if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], fg.bcc[2], uc);
-        if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], fg.bcc[3], uc);
-        if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], fg.bcc[4], uc);
-        if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], fg.bcc[5], uc);
-        const double tx = (vxp + vxm) - 2.0 * uc;
-        const double ty = (vyp + vym) - 2.0 * uc;
-        const double tz = (vzp + vzm) - 2.0 * uc;
-        double ldpsi = (tx + ty) + tz;                                  // .ChF:416-425
-        double lofdpsi = s.alpha * (ii ? av.y : av.x) * uc;            // .ChF:411-412
+        const T uc = ii ? c.y : c.x;
+        T vxm = ii ? c.x : xl, vxp = ii ? xr : c.y;
+        T vym = ii ? ym.y : ym.x, vyp = ii ? yp.y : yp.x;
+        T vzm = ii ? zm.y : zm.x, vzp = ii ? zp.y : zp.x;
+        if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], (T)fg.bcc[0], uc);
+        if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], (T)fg.bcc[1], uc);
+        if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], (T)fg.bcc[2], uc);
+        if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], (T)fg.bcc[3], uc);
+        if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], (T)fg.bcc[4], uc);
+        if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], (T)fg.bcc[5], uc);
+        const T tx = (vxp + vxm) - (T)2 * uc;
+        const T ty = (vyp + vym) - (T)2 * uc;
+        const T tz = (vzp + vzm) - (T)2 * uc;
+        T ldpsi = (tx + ty) + tz;                                  // .ChF:416-425
+        T lofdpsi = s.alpha * (ii ? av.y : av.x) * uc;            // .ChF:411-412
         ldpsi = ldpsi * s.dxinv * s.beta * (ii ? bv.y : bv.x);         // .ChF:427
         lofdpsi = lofdpsi - ldpsi;                                      // .ChF:429
         sum = sum + ((ii ? rv.y : rv.x) - lofdpsi) / denom;             // .ChF:431-432
@@ -226,17 +245,17 @@ struct ProlongArgs {
 // (interior, or an exchanged ghost across a box / periodic face), else on the
 // other side; e = c0 + dx-term + dy-term + dz-term in that order.  The six
 // neighbour loads are unconditional (coarse ghosts are always allocated).
-template <int TYPE>
-__global__ __launch_bounds__(256) void k_prolong(double *__restrict__ uf, const BoxArgs fg,
-                                                 const double *__restrict__ ec, const BoxArgs cg,
+template <class T, int TYPE>
+__global__ __launch_bounds__(256) void k_prolong(T *__restrict__ uf, const BoxArgs fg,
+                                                 const T *__restrict__ ec, const BoxArgs cg,
                                                  const ProlongArgs pa) {
   const int ci = blockIdx.x * TX + threadIdx.x;
   const int cj = blockIdx.y * TY + threadIdx.y;
   const int ck = blockIdx.z;
   if (ci >= cg.nx || cj >= cg.ny) return;
   const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
-  const double c0 = ec[cidx];
-  double dlo[3] = {0.0, 0.0, 0.0}, dhi[3] = {0.0, 0.0, 0.0};  // slope for lower / upper child
+  const T c0 = ec[cidx];
+  T dlo[3] = {(T)0, (T)0, (T)0}, dhi[3] = {(T)0, (T)0, (T)0};  // slope for lower / upper child
   bool ok[3] = {false, false, false};
   if (TYPE == 1) {
     const long cs[3] = {1, cg.sy, cg.sz};
@@ -244,13 +263,13 @@ __global__ __launch_bounds__(256) void k_prolong(double *__restrict__ uf, const 
     const int cn[3] = {cg.nx, cg.ny, cg.nz};
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-      const double lo = ec[cidx - cs[d]], hi = ec[cidx + cs[d]];
+      const T lo = ec[cidx - cs[d]], hi = ec[cidx + cs[d]];
       const bool has_lo = (ic[d] > 0) || pa.avail_lo[d];
       const bool has_hi = (ic[d] < cn[d] - 1) || pa.avail_hi[d];
       ok[d] = has_lo || has_hi;
-      const double sl_hi = hi - c0, sl_lo = c0 - lo;
-      dhi[d] = (has_hi ? sl_hi : sl_lo) * 0.25;    // upper child: +0.25 * slope
-      dlo[d] = (!has_lo ? sl_hi : sl_lo) * -0.25;  // lower child: -0.25 * slope
+      const T sl_hi = hi - c0, sl_lo = c0 - lo;
+      dhi[d] = (has_hi ? sl_hi : sl_lo) * (T)0.25;    // upper child: +0.25 * slope
+      dlo[d] = (!has_lo ? sl_hi : sl_lo) * (T)-0.25;  // lower child: -0.25 * slope
     }
   }
 #pragma unroll
@@ -258,27 +277,27 @@ __global__ __launch_bounds__(256) void k_prolong(double *__restrict__ uf, const 
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const long row = (long)(2 * ci) + (long)(2 * cj + jj) * fg.sy + (long)(2 * ck + kk) * fg.sz;
-      double2 v = ld2(uf + row);
-      double e0 = c0, e1 = c0;
+      V2<T> v = ld2(uf + row);
+      T e0 = c0, e1 = c0;
       if (TYPE == 1) {
         if (ok[0]) {
           e0 = e0 + dlo[0];
           e1 = e1 + dhi[0];
         }
         if (ok[1]) {
-          const double t = jj ? dhi[1] : dlo[1];
+          const T t = jj ? dhi[1] : dlo[1];
           e0 = e0 + t;
           e1 = e1 + t;
         }
         if (ok[2]) {
-          const double t = kk ? dhi[2] : dlo[2];
+          const T t = kk ? dhi[2] : dlo[2];
           e0 = e0 + t;
           e1 = e1 + t;
         }
       }
       v.x = v.x + e0;
       v.y = v.y + e1;
-      *reinterpret_cast<double2 *>(uf + row) = v;
+      *reinterpret_cast<V2<T> *>(uf + row) = v;
     }
 }
 
@@ -417,15 +436,16 @@ __global__ __launch_bounds__(RB) void k_reduce_final(const double *__restrict__ 
   if (threadIdx.x == 0) out[0] = sm[0];
 }
 
+template <class T>
 __global__ __launch_bounds__(256) void k_copy_items(const CopyItem *__restrict__ items,
-                                                    double *const *__restrict__ src_tab,
-                                                    const double *__restrict__ src_buf,
-                                                    double *const *__restrict__ dst_tab,
-                                                    double *__restrict__ dst_buf) {
+                                                    T *const *__restrict__ src_tab,
+                                                    const T *__restrict__ src_buf,
+                                                    T *const *__restrict__ dst_tab,
+                                                    T *__restrict__ dst_buf) {
   const CopyItem it = items[blockIdx.y];
   const long n = (long)it.nx * it.ny * it.nz;
-  const double *src = it.src >= 0 ? src_tab[it.src] : src_buf;
-  double *dst = it.dst >= 0 ? dst_tab[it.dst] : dst_buf;
+  const T *src = it.src >= 0 ? src_tab[it.src] : src_buf;
+  T *dst = it.dst >= 0 ? dst_tab[it.dst] : dst_buf;
   for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < n;
        t += (long)gridDim.x * blockDim.x) {
     const int i = (int)(t % it.nx);
@@ -581,6 +601,38 @@ inline void check_launch() {
   if (e != hipSuccess) throw Error(kHipErr, std::string("kernel launch: ") + hipGetErrorString(e));
 }
 
+// fp64 -> fp32 over the valid region grown by `grow` (coefficients of the
+// mixed-precision V-cycle); and a float box copy
+__global__ __launch_bounds__(256) void k_to_float(float *__restrict__ d, const double *__restrict__ s,
+                                                  const BoxArgs g, int grow) {
+  const int i = blockIdx.x * TX + threadIdx.x - grow;
+  const int j = blockIdx.y * TY + threadIdx.y - grow;
+  const int k = (int)blockIdx.z - grow;
+  if (i >= g.nx + grow || j >= g.ny + grow) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  d[idx] = (float)s[idx];
+}
+
+__global__ __launch_bounds__(256) void k_incr_f(double *__restrict__ x, const float *__restrict__ y,
+                                                const BoxArgs g) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  x[idx] = x[idx] + (double)y[idx];
+}
+
+__global__ __launch_bounds__(256) void k_copy_f(float *__restrict__ d, const float *__restrict__ s,
+                                                const BoxArgs g) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  d[idx] = s[idx];
+}
+
 }  // namespace
 
 void gsrb_pass(double *u, const double *rhs, const double *a, const double *b, const double *lam,
@@ -618,8 +670,8 @@ void residual(double *r, const double *u, const double *rhs, const double *a, co
     const int kc = mode < g.nz ? mode : g.nz;
     dim3 grid = grid_cells(g.nx, g.ny, g.nz);
     grid.z = (unsigned)((g.nz + kc - 1) / kc);
-    if (s.bconst) k_residual_z<true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
-    else k_residual_z<false><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+    if (s.bconst) k_residual_z<true, double><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+    else k_residual_z<false, double><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
   } else if (s.bconst) {
     k_residual<true><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
   } else {
@@ -633,11 +685,11 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
                        hipStream_t st, bool accumulate) {
   if (cg.nx <= 0 || cg.ny <= 0 || cg.nz <= 0) return;
   if (s.bconst)
-    k_restrict<true><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s,
-                                                                        accumulate ? 1 : 0);
+    k_restrict<double, true><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(
+        rc, cg, u, rhs, a, b, fg, s, accumulate ? 1 : 0);
   else
-    k_restrict<false><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg,
-                                                                         s, accumulate ? 1 : 0);
+    k_restrict<double, false><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(
+        rc, cg, u, rhs, a, b, fg, s, accumulate ? 1 : 0);
   check_launch();
 }
 
@@ -652,9 +704,9 @@ void prolong(double *uf, const BoxArgs &fg, const double *ec, const BoxArgs &cg,
   MGIC_CHECK(fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz,
              "prolong: fine box must be the coarse box refined by 2");
   if (type == 1)
-    k_prolong<1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
+    k_prolong<double, 1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
   else
-    k_prolong<0><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
+    k_prolong<double, 0><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
   check_launch();
 }
 
@@ -738,8 +790,8 @@ void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *con
   if (nitems <= 0 || max_cells <= 0) return;
   long bx = (max_cells + 255) / 256;
   if (bx > 1024) bx = 1024;
-  k_copy_items<<<dim3((unsigned)bx, (unsigned)nitems), dim3(256), 0, st>>>(d_items, src_tab, src_buf,
-                                                                            dst_tab, dst_buf);
+  k_copy_items<double><<<dim3((unsigned)bx, (unsigned)nitems), dim3(256), 0, st>>>(
+      d_items, src_tab, src_buf, dst_tab, dst_buf);
   check_launch();
 }
 
@@ -787,6 +839,78 @@ void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStrea
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
   k_incr_grown<<<grid_cells(g.nx + 2 * grow, g.ny + 2 * grow, g.nz + 2 * grow), kBlock, 0, st>>>(
       x, y, g, grow);
+  check_launch();
+}
+
+
+// ---- fp32 (mixed-precision V-cycle) variants -------------------------------
+void residual_to_f(float *r, const double *u, const double *rhs, const double *a, const double *b,
+                   const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  const int kc = 16 < g.nz ? 16 : g.nz;
+  dim3 grid = grid_cells(g.nx, g.ny, g.nz);
+  grid.z = (unsigned)((g.nz + kc - 1) / kc);
+  if (s.bconst) k_residual_z<true, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  else k_residual_z<false, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  check_launch();
+}
+
+void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const float *rhs,
+                         const float *a, const float *b, const BoxArgs &fg, const StencilCoefs &s,
+                         hipStream_t st) {
+  if (cg.nx <= 0 || cg.ny <= 0 || cg.nz <= 0) return;
+  if (s.bconst)
+    k_restrict<float, true><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b,
+                                                                               fg, s, 0);
+  else
+    k_restrict<float, false><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a,
+                                                                                b, fg, s, 0);
+  check_launch();
+}
+
+void prolong_f(float *uf, const BoxArgs &fg, const float *ec, const BoxArgs &cg,
+               const int avail_lo[3], const int avail_hi[3], int type, hipStream_t st) {
+  if (fg.nx <= 0 || fg.ny <= 0 || fg.nz <= 0) return;
+  ProlongArgs pa;
+  for (int d = 0; d < 3; ++d) {
+    pa.avail_lo[d] = avail_lo[d];
+    pa.avail_hi[d] = avail_hi[d];
+  }
+  MGIC_CHECK(fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz,
+             "prolong: fine box must be the coarse box refined by 2");
+  if (type == 1)
+    k_prolong<float, 1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
+  else
+    k_prolong<float, 0><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
+  check_launch();
+}
+
+void copy_items_f(const CopyItem *d_items, int nitems, long max_cells, float *const *src_tab,
+                  const float *src_buf, float *const *dst_tab, float *dst_buf, hipStream_t st) {
+  if (nitems <= 0 || max_cells <= 0) return;
+  long bx = (max_cells + 255) / 256;
+  if (bx > 1024) bx = 1024;
+  k_copy_items<float><<<dim3((unsigned)bx, (unsigned)nitems), dim3(256), 0, st>>>(
+      d_items, src_tab, src_buf, dst_tab, dst_buf);
+  check_launch();
+}
+
+void to_float(float *d, const double *s, const BoxArgs &g, int grow, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_to_float<<<grid_cells(g.nx + 2 * grow, g.ny + 2 * grow, g.nz + 2 * grow), kBlock, 0, st>>>(
+      d, s, g, grow);
+  check_launch();
+}
+
+void incr_f(double *x, const float *y, const BoxArgs &g, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_incr_f<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(x, y, g);
+  check_launch();
+}
+
+void copy_f(float *d, const float *s, const BoxArgs &g, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_copy_f<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(d, s, g);
   check_launch();
 }
 

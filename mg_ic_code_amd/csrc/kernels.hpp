@@ -29,6 +29,11 @@ void gsrb_pass(double *u, const double *rhs, const double *a, const double *b,
 void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       double *acc, int kind, hipStream_t st);
+// The same sweep on fp32 fields (the mixed-precision V-cycle); the stencil
+// constants are rounded to fp32 once; acc (phi += e) stays fp64.
+void gsrb_sweep_fused_f(float *u_out, float *u_in, const float *rhs, const float *a,
+                        const float *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                        double *acc, int kind, hipStream_t st);
 // The last pre-smoothing sweep fused with restrictResidual: u_out = sweep(
 // u_in) as gsrb_sweep_fused, and rc (the coarse box, coarsen(box, 2)) = the
 // restricted residual rhs - L(u_out) with the homogeneous BC of g (exactly
@@ -109,6 +114,22 @@ void lap_psi(double *l, const double *psi, const BoxArgs &g, double dx, hipStrea
 void rho_grad_phi(double *r, const double *phi, const BoxArgs &g, double dx, hipStream_t st);
 // x += y over the valid box grown by `grow` (<= kGhost) cells
 void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStream_t st);
+
+
+// ---- fp32 variants for the mixed-precision V-cycle (fp32 smoother / fp64
+// residual): the same expressions evaluated in float, constants rounded once
+void residual_to_f(float *r, const double *u, const double *rhs, const double *a, const double *b,
+                   const BoxArgs &g, const StencilCoefs &s, hipStream_t st);
+void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const float *rhs,
+                         const float *a, const float *b, const BoxArgs &fg, const StencilCoefs &s,
+                         hipStream_t st);
+void prolong_f(float *uf, const BoxArgs &fg, const float *ec, const BoxArgs &cg,
+               const int avail_lo[3], const int avail_hi[3], int type, hipStream_t st);
+void copy_items_f(const CopyItem *d_items, int nitems, long max_cells, float *const *src_tab,
+                  const float *src_buf, float *const *dst_tab, float *dst_buf, hipStream_t st);
+void to_float(float *d, const double *s, const BoxArgs &g, int grow, hipStream_t st);
+void copy_f(float *d, const float *s, const BoxArgs &g, hipStream_t st);
+void incr_f(double *x, const float *y, const BoxArgs &g, hipStream_t st);  // x += (double)y
 
 }  // namespace kern
 }  // namespace mgic

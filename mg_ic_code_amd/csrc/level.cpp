@@ -352,6 +352,29 @@ void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_ta
   }
 }
 
+void CopyPlan::execute_f(Comm &comm, float *const *src_tab, float *const *dst_tab,
+                         hipStream_t st) {
+  float *sb = reinterpret_cast<float *>(sendbuf_), *rb = reinterpret_cast<float *>(recvbuf_);
+  if (!local_.empty())
+    kern::copy_items_f(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
+  if (send_total_ || recv_total_) {
+    MGIC_CHECK(comm.uses_rccl(), "remote copies need an RCCL communicator");
+    if (!pack_.empty())
+      kern::copy_items_f(d_pack_, (int)pack_.size(), max_pack_, src_tab, nullptr, nullptr, sb, st);
+    MGIC_NCCL(ncclGroupStart());
+    for (auto &kv : send_cnt_)
+      MGIC_NCCL(ncclSend(sb + send_off_[kv.first], (size_t)kv.second, ncclFloat, kv.first,
+                         comm.nccl(), st));
+    for (auto &kv : recv_cnt_)
+      MGIC_NCCL(ncclRecv(rb + recv_off_[kv.first], (size_t)kv.second, ncclFloat, kv.first,
+                         comm.nccl(), st));
+    MGIC_NCCL(ncclGroupEnd());
+    if (!unpack_.empty())
+      kern::copy_items_f(d_unpack_, (int)unpack_.size(), max_unpack_, nullptr, rb, dst_tab,
+                         nullptr, st);
+  }
+}
+
 // ------------------------------------------------------------------ LevelData
 LevelData::LevelData(std::shared_ptr<Grid> g) : grid(std::move(g)) {
   const int n = grid->nlocal();
@@ -388,6 +411,39 @@ void LevelData::exchange_shell(hipStream_t st) {
   CopyPlan &pl = grid->shell_plan();
   if (pl.empty()) return;
   pl.execute(*grid->comm, d_tab, d_tab, st);
+}
+
+// ------------------------------------------------------------------ LevelDataF
+LevelDataF::LevelDataF(std::shared_ptr<Grid> g) : grid(std::move(g)) {
+  const int n = grid->nlocal();
+  base.resize(n, nullptr);
+  p.resize(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    const FabGeom &fg = grid->geom[i];
+    MGIC_HIP(hipMalloc(&base[i], sizeof(float) * (size_t)fg.total));
+    MGIC_HIP(hipMemset(base[i], 0, sizeof(float) * (size_t)fg.total));
+    p[i] = base[i] + fg.origin;
+  }
+  MGIC_HIP(hipMalloc(&d_tab, sizeof(float *) * (size_t)std::max(n, 1)));
+  if (n) MGIC_HIP(hipMemcpy(d_tab, p.data(), sizeof(float *) * (size_t)n, hipMemcpyHostToDevice));
+}
+
+LevelDataF::~LevelDataF() {
+  for (float *b : base)
+    if (b) (void)hipFree(b);
+  if (d_tab) (void)hipFree(d_tab);
+}
+
+void LevelDataF::exchange(hipStream_t st) {
+  CopyPlan &pl = grid->exchange_plan();
+  if (pl.empty()) return;
+  pl.execute_f(*grid->comm, d_tab, d_tab, st);
+}
+
+void LevelDataF::exchange_shell(hipStream_t st) {
+  CopyPlan &pl = grid->shell_plan();
+  if (pl.empty()) return;
+  pl.execute_f(*grid->comm, d_tab, d_tab, st);
 }
 
 }  // namespace mgic

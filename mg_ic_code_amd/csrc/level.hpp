@@ -79,6 +79,8 @@ class CopyPlan {
   void finalize();       // + upload item tables, allocate message buffers
   // src_tab / dst_tab: device tables of valid-lo pointers per local box
   void execute(Comm &comm, double *const *src_tab, double *const *dst_tab, hipStream_t st);
+  // the same copies on fp32 fields (same element offsets; messages in floats)
+  void execute_f(Comm &comm, float *const *src_tab, float *const *dst_tab, hipStream_t st);
   bool empty() const { return local_.empty() && pack_.empty() && unpack_.empty(); }
 
   std::vector<CopyItem> local_, pack_, unpack_;
@@ -152,6 +154,23 @@ class LevelData {
   void set_zero_all(hipStream_t st);  // valid + ghosts
   void exchange(hipStream_t st);
   void exchange_shell(hipStream_t st);  // 2-deep faces + edges + corners
+};
+
+// The same layout with fp32 elements (the mixed-precision V-cycle's
+// corrections, right-hand sides and coefficients): identical FabGeom in
+// elements, so every kernel offset and copy plan is shared with LevelData.
+class LevelDataF {
+ public:
+  explicit LevelDataF(std::shared_ptr<Grid> g);
+  ~LevelDataF();
+  LevelDataF(const LevelDataF &) = delete;
+  LevelDataF &operator=(const LevelDataF &) = delete;
+  std::shared_ptr<Grid> grid;
+  std::vector<float *> base;
+  std::vector<float *> p;
+  float **d_tab = nullptr;
+  void exchange(hipStream_t st);
+  void exchange_shell(hipStream_t st);
 };
 
 }  // namespace mgic

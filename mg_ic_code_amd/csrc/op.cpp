@@ -28,7 +28,7 @@ void prof_enable(bool on, long min_cells) {
   g_prof.passes = 0;
 }
 
-static void prof_mark(hipStream_t st, long ncells, bool begin, int passes) {
+void prof_mark(hipStream_t st, long ncells, bool begin, int passes) {
   if (!g_prof.on || ncells < g_prof.min_cells) return;
   if (begin) {
     if (g_prof.used + 2 > g_prof.ev.size()) {
@@ -804,6 +804,40 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
     op.relaxFlags(e, r, prm.n_post, rf | out);
 }
 
+void MultiGrid::fmg(LevelData &e0, LevelData &r0, LevelData &phi, int ncycles) {
+  const int D = depths();
+  for (int d = 1; d < D; ++d)
+    MGIC_CHECK(!levels_[d].agg, "FMG: agglomerated depths are not supported");
+  auto E = [&](int d) -> LevelData & { return d == 0 ? e0 : *levels_[d].e; };
+  auto Rr = [&](int d) -> LevelData & { return d == 0 ? r0 : *levels_[d].r; };
+  if (D == 1) {  // one depth: the bottom solve is the whole cycle
+    cycle(0, e0, r0, true, &phi);
+    return;
+  }
+  // right-hand sides: r_{d+1} = restrictResidual of a zero correction
+  for (int d = 0; d + 1 < D; ++d) {
+    levels_[d].op->setToZero(E(d));
+    levels_[d].op->restrictResidual(Rr(d + 1), E(d), Rr(d), true);
+  }
+  // coarsest depth from zero, then up with e_d = P e_{d+1} as the start
+  {
+    VariableCoeffPoissonOperator &op = *levels_[D - 1].op;
+    if (prm.bottom_solver == 1) {
+      op.setToZero(E(D - 1));
+      bottom.solve(op, E(D - 1), Rr(D - 1), true);
+    } else {
+      op.relaxFromZero(E(D - 1), Rr(D - 1), prm.n_bottom);
+    }
+  }
+  for (int d = D - 2; d >= 0; --d) {
+    VariableCoeffPoissonOperator &op = *levels_[d].op;
+    op.setToZero(E(d));
+    op.prolongIncrement(E(d), E(d + 1));
+    for (int c = 0; c < ncycles; ++c)
+      cycle(d, E(d), Rr(d), false, d == 0 && c == ncycles - 1 ? &phi : nullptr);
+  }
+}
+
 // --------------------------------------------------------------- AMRMultiGrid
 void AMRMultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &p) {
   mg.define(factory, p);
@@ -814,6 +848,14 @@ double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &
                                int normType, bool homogeneous) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
   mg.oneCycleFromZeroInto(*corr_, resid, phi);  // e = 0; oneCycle(e, r); phi += e
+  op0.residual(resid, phi, rhs, homogeneous);
+  return normType >= 0 ? op0.norm(resid, normType) : -1.0;
+}
+
+double AMRMultiGrid::fmg(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
+                         bool homogeneous, int ncycles) {
+  VariableCoeffPoissonOperator &op0 = mg.op(0);
+  mg.fmg(*corr_, resid, phi, ncycles);
   op0.residual(resid, phi, rhs, homogeneous);
   return normType >= 0 ? op0.norm(resid, normType) : -1.0;
 }

@@ -117,6 +117,9 @@ class VariableCoeffPoissonOperator {
 
  public:
   bool fusedSmootherApplies() const;
+  // kernel arguments for other drivers (the mixed-precision V-cycle)
+  const BoxArgs &boxArgs(int n, bool homogeneous) { return args(n, homogeneous); }
+  StencilCoefs stencil() { return coefs(); }
   // `n` levelGSRB sweeps with the fused out-of-place kernel (alternating
   // dpsi and the scratch buffer; the result always ends in dpsi).
   // zero_in: dpsi is taken as identically zero and not read (its memory
@@ -153,6 +156,8 @@ std::shared_ptr<LevelData> average_coef(const LevelData &fine, std::shared_ptr<G
 // at least min_cells cells is bracketed by hipEvents on its stream.
 void prof_enable(bool on, long min_cells);
 int prof_read(double *total_ms, long *passes);  // returns launches timed, total ms
+// bracket one smoother launch (no-op unless enabled and ncells >= min_cells)
+void prof_mark(hipStream_t st, long ncells, bool begin, int passes);
 
 // VariableCoeffPoissonOperatorFactory (single AMR level; the configs have one)
 class VariableCoeffPoissonOperatorFactory {
@@ -219,6 +224,10 @@ class MultiGrid {
   void oneCycleFromZeroInto(LevelData &e, const LevelData &r, LevelData &phi) {
     cycle(0, e, const_cast<LevelData &>(r), true, &phi);
   }
+  // full multigrid from the residual r at depth 0: r_{d+1} = R(r_d) at every
+  // depth, the bottom solve from zero, then per finer depth e_d = P e_{d+1}
+  // and `ncycles` V-cycles on it; phi += e_0 (folded into the last sweep)
+  void fmg(LevelData &e, LevelData &r, LevelData &phi, int ncycles);
   int depths() const { return (int)levels_.size(); }
   VariableCoeffPoissonOperator &op(int d) { return *levels_[d].op; }
   LevelData *corr(int d) { return levels_[d].e.get(); }
@@ -267,6 +276,10 @@ class AMRMultiGrid {
                    bool homogeneous);
   double initResidual(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
                       bool homogeneous);
+  // an FMG cycle on the current residual (resid as left by initResidual /
+  // iteration), phi += its correction, then resid = rhs - L(phi)
+  double fmg(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
+             bool homogeneous, int ncycles);
   MultiGrid mg;
 
  private:

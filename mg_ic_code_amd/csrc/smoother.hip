@@ -46,7 +46,8 @@ namespace kern {
 
 namespace {
 
-__device__ __forceinline__ double ghost_of(int mode, double c, double near) {
+template <class T>
+__device__ __forceinline__ T ghost_of(int mode, T c, T near) {
   return mode == kBcDirichlet ? (c - near) : (mode == kBcNeumannHom ? near : near + c);
 }
 
@@ -62,6 +63,33 @@ __device__ __forceinline__ double bsel(int q, double x, double y) {
   const unsigned hi = ((unsigned)(xb >> 32) & m) | ((unsigned)(yb >> 32) & ~m);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+__device__ __forceinline__ float bsel(int q, float x, float y) {
+  const unsigned m = 0u - (unsigned)(q & 1);
+  return __uint_as_float((__float_as_uint(x) & m) | (__float_as_uint(y) & ~m));
+}
+
+// element type traits: a lane pair is one 16-B (double) / 8-B (float) load
+template <class T> struct Vec2;
+template <> struct Vec2<double> { using type = double2; };
+template <> struct Vec2<float> { using type = float2; };
+template <class T> using V2 = typename Vec2<T>::type;
+template <class T>
+__device__ __forceinline__ V2<T> mk2(T x, T y) {
+  V2<T> v;
+  v.x = x;
+  v.y = y;
+  return v;
+}
+
+// the stencil constants in the element type (fp32 sweeps round each once;
+// for double this is the identity, so the fp64 kernels are unchanged)
+template <class T>
+struct SC {
+  T alpha, beta, dxinv, lamshift, bval;
+  __device__ explicit SC(const StencilCoefs &s)
+      : alpha((T)s.alpha), beta((T)s.beta), dxinv((T)s.dxinv), lamshift((T)s.lamshift),
+        bval((T)s.bval) {}
+};
 
 template <int TX, int TY, int NT>
 struct Fused6 {
@@ -76,17 +104,18 @@ struct Fused6 {
 
 // One tile (x0, y0) of the box, planes [z0, z1): R/B are the 5-plane LDS
 // rings (5 * CP doubles each) holding the red / black element of each pair.
-template <int TX, int TY, int NT, bool ZIN, bool BC, bool ACC>
-__device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *__restrict__ B,
-                                               double *__restrict__ uo,
+template <class T, int TX, int TY, int NT, bool ZIN, bool BC, bool ACC>
+__device__ __forceinline__ void fused6_segment(T *__restrict__ R, T *__restrict__ B,
+                                               T *__restrict__ uo,
                                                double *__restrict__ acc,
-                                               const double *__restrict__ ui,
-                                               const double *__restrict__ rhs,
-                                               const double *__restrict__ a,
-                                               const double *__restrict__ b, const BoxArgs &g,
-                                               const StencilCoefs &s, int x0, int y0, int z0,
+                                               const T *__restrict__ ui,
+                                               const T *__restrict__ rhs,
+                                               const T *__restrict__ a,
+                                               const T *__restrict__ b, const BoxArgs &g,
+                                               const StencilCoefs &s64, int x0, int y0, int z0,
                                                int z1) {
   using F = Fused6<TX, TY, NT>;
+  const SC<T> s(s64);
   constexpr int PW = F::PW, CP = F::CP, NRP = F::NRP, NL = F::NL, NP = F::NP;
   const int tid = threadIdx.x;
   const long sy = g.sy, sz = g.sz;
@@ -155,10 +184,10 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   }
   const int gxlo = max(x0 - 1, rxlo), gxhi = min(x0 + TX, rxhi);  // red ring extent
 
-  double pu0[NL], pu1[NL];
-  double cr0[NP], cr1[NP], ca0[NP], ca1[NP], cb0[NP], cb1[NP];
-  double nr0[NP], nr1[NP], na0[NP], na1[NP], nb0[NP], nb1[NP];
-  double kr[NP], ka[NP], kb[NP];
+  T pu0[NL], pu1[NL];
+  T cr0[NP], cr1[NP], ca0[NP], ca1[NP], cb0[NP], cb1[NP];
+  T nr0[NP], nr1[NP], na0[NP], na1[NP], nb0[NP], nb1[NP];
+  T kr[NP], ka[NP], kb[NP];
   double an0[NP], an1[NP], ak0[NP], ak1[NP];  // ACC: acc pairs of planes p and p-1
 
   auto fetch_u = [&](int p) {
@@ -168,36 +197,36 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (ZIN) {  // the input is identically +0 (a freshly zeroed correction)
-        pu0[i] = 0.0;
-        pu1[i] = 0.0;
+        pu0[i] = (T)0;
+        pu1[i] = (T)0;
       } else {
-        const double2 v = *reinterpret_cast<const double2 *>(ui + loff[i] + pz);
+        const V2<T> v = *reinterpret_cast<const V2<T> *>(ui + loff[i] + pz);
         pu0[i] = v.x;
         pu1[i] = v.y;
       }
     }
   };
   auto put_u = [&](int p) {
-    double *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
+    T *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
     const int zf = (g.bcm[4] && p == -1) ? 4 : (g.bcm[5] && p == nz) ? 5 : -1;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = tid + i * NT;
       if (NL * NT > CP && c >= CP) continue;
-      double u0 = pu0[i], u1 = pu1[i];
+      T u0 = pu0[i], u1 = pu1[i];
       if (!ZIN) {  // BC images (a zero input images to zero: homogeneous BC)
         const int bx = lbc[i] & 3, by = lbc[i] >> 2;
         if (by) {
           const int f = 1 + by;
-          u0 = ghost_of(g.bcm[f], g.bcc[f], u0);
-          u1 = ghost_of(g.bcm[f], g.bcc[f], u1);
+          u0 = ghost_of(g.bcm[f], (T)g.bcc[f], u0);
+          u1 = ghost_of(g.bcm[f], (T)g.bcc[f], u1);
         }
-        if (bx == 1) u1 = ghost_of(g.bcm[0], g.bcc[0], u0);
-        else if (bx == 2) u0 = ghost_of(g.bcm[1], g.bcc[1], u1);
-        else if (bx == 3) u1 = ghost_of(g.bcm[1], g.bcc[1], u0);
+        if (bx == 1) u1 = ghost_of(g.bcm[0], (T)g.bcc[0], u0);
+        else if (bx == 2) u0 = ghost_of(g.bcm[1], (T)g.bcc[1], u1);
+        else if (bx == 3) u1 = ghost_of(g.bcm[1], (T)g.bcc[1], u0);
         if (zf >= 0) {
-          u0 = ghost_of(g.bcm[zf], g.bcc[zf], u0);
-          u1 = ghost_of(g.bcm[zf], g.bcc[zf], u1);
+          u0 = ghost_of(g.bcm[zf], (T)g.bcc[zf], u0);
+          u1 = ghost_of(g.bcm[zf], (T)g.bcc[zf], u1);
         }
       }
       const int q = (q0 + lgy[i] + p) & 1;  // 1: the red element is the second
@@ -210,10 +239,10 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const long off = rcoff[i] + pz;
-      const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
-      const double2 va = *reinterpret_cast<const double2 *>(a + off);
-      const double2 vb = BC ? make_double2(s.bval, s.bval)
-                            : *reinterpret_cast<const double2 *>(b + off);
+      const V2<T> vr = *reinterpret_cast<const V2<T> *>(rhs + off);
+      const V2<T> va = *reinterpret_cast<const V2<T> *>(a + off);
+      const V2<T> vb = BC ? mk2<T>(s.bval, s.bval)
+                            : *reinterpret_cast<const V2<T> *>(b + off);
       nr0[i] = vr.x; nr1[i] = vr.y;
       na0[i] = va.x; na1[i] = va.y;
       nb0[i] = vb.x; nb1[i] = vb.y;
@@ -228,16 +257,16 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
       an1[i] = v.y;
     }
   };
-  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
-                 double rv, double av, double bv) -> double {
-    const double tx = (xp + xm) - 2.0 * uc;
-    const double ty = (yp + ym) - 2.0 * uc;
-    const double tz = (zp + zm) - 2.0 * uc;
-    const double lap = (tx + ty) + tz;                     // .ChF:111-120
-    double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
-    const double ldpsi = lap * s.dxinv * bv;               // .ChF:122
+  auto upd = [&](T uc, T xm, T xp, T ym, T yp, T zm, T zp,
+                 T rv, T av, T bv) -> T {
+    const T tx = (xp + xm) - (T)2 * uc;
+    const T ty = (yp + ym) - (T)2 * uc;
+    const T tz = (zp + zm) - (T)2 * uc;
+    const T lap = (tx + ty) + tz;                     // .ChF:111-120
+    T lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
+    const T ldpsi = lap * s.dxinv * bv;               // .ChF:122
     lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
-    const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
+    const T lam = (T)1 / (av * s.alpha + s.lamshift);  // .cpp:234-243
     return uc - lam * (lofdpsi - rv);                      // .ChF:127-128
   };
 
@@ -268,18 +297,18 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
     }
     __syncthreads();
     if (p >= rzlo && p <= rzhi) {  // RED cells of plane p on the ring
-      double *Rs = R + slot(p) * CP;
-      const double *Bs = B + slot(p) * CP;
-      const double *Bm = B + slot(p - 1) * CP;
-      const double *Bp = B + slot(p + 1) * CP;
+      T *Rs = R + slot(p) * CP;
+      const T *Bs = B + slot(p) * CP;
+      const T *Bm = B + slot(p - 1) * CP;
+      const T *Bp = B + slot(p + 1) * CP;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const int q = (q0 + rgy[i] + p) & 1;
         const int gx = rgx0[i] + q;
         if (!rrow[i] || gx < gxlo || gx > gxhi) continue;
         const int ci = rci[i];
-        const double xm = q ? Bs[ci] : Bs[ci - 1];
-        const double xp = q ? Bs[ci + 1] : Bs[ci];
+        const T xm = q ? Bs[ci] : Bs[ci - 1];
+        const T xp = q ? Bs[ci + 1] : Bs[ci];
         Rs[ci] = upd(Rs[ci], xm, xp, Bs[ci - PW], Bs[ci + PW], Bm[ci], Bp[ci],
                      bsel(q, cr1[i], cr0[i]), bsel(q, ca1[i], ca0[i]), bsel(q, cb1[i], cb0[i]));
       }
@@ -287,39 +316,39 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
     __syncthreads();
     const int k = p - 1;
     if (k >= z0 && k < z1) {  // BLACK cells of plane k on the tile + store
-      const double *Rs = R + slot(k) * CP;
-      const double *Bs = B + slot(k) * CP;
-      const double *Rm = R + slot(k - 1) * CP;
-      const double *Rp = R + slot(k + 1) * CP;
-      double *dst = uo + (long)k * sz;
+      const T *Rs = R + slot(k) * CP;
+      const T *Bs = B + slot(k) * CP;
+      const T *Rm = R + slot(k - 1) * CP;
+      const T *Rp = R + slot(k + 1) * CP;
+      T *dst = uo + (long)k * sz;
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         if (!rtile[i]) continue;
         const int qb = 1 - ((q0 + rgy[i] + k) & 1);  // 1: the black element is the second
         const int gx = rgx0[i] + qb;
         const int ci = rci[i];
-        const double red = Rs[ci];
-        double blk = Bs[ci];
+        const T red = Rs[ci];
+        T blk = Bs[ci];
         if (gx < nx) {
-          const double xm = qb ? Rs[ci] : Rs[ci - 1];
-          const double xp = qb ? Rs[ci + 1] : Rs[ci];
+          const T xm = qb ? Rs[ci] : Rs[ci - 1];
+          const T xp = qb ? Rs[ci + 1] : Rs[ci];
           blk = upd(blk, xm, xp, Rs[ci - PW], Rs[ci + PW], Rm[ci], Rp[ci], kr[i], ka[i], kb[i]);
         }
-        double2 w;
+        V2<T> w;
         w.x = bsel(qb, red, blk);
         w.y = bsel(qb, blk, red);
         if (ACC) {  // acc += the swept value (incr, scale 1), u_out not written
           double *ad = acc + (long)k * sz + roff[i];
           if (rgx0[i] + 1 < nx) {
             double2 t;
-            t.x = ak0[i] + w.x;
-            t.y = ak1[i] + w.y;
+            t.x = ak0[i] + (double)w.x;
+            t.y = ak1[i] + (double)w.y;
             *reinterpret_cast<double2 *>(ad) = t;
           } else {
-            ad[0] = ak0[i] + w.x;
+            ad[0] = ak0[i] + (double)w.x;
           }
         } else if (rgx0[i] + 1 < nx) {
-          *reinterpret_cast<double2 *>(dst + roff[i]) = w;
+          *reinterpret_cast<V2<T> *>(dst + roff[i]) = w;
         } else {
           dst[roff[i]] = w.x;
         }
@@ -338,25 +367,25 @@ __device__ __forceinline__ void fused6_segment(double *__restrict__ R, double *_
   }
 }
 
-template <int TX, int TY, int NT, bool ZIN, bool BC, bool ACC>
-__global__ __launch_bounds__(NT) void k_gsrb_fused6(double *__restrict__ uo,
+template <class T, int TX, int TY, int NT, bool ZIN, bool BC, bool ACC>
+__global__ __launch_bounds__(NT) void k_gsrb_fused6(T *__restrict__ uo,
                                                     double *__restrict__ acc,
-                                                    const double *__restrict__ ui,
-                                                    const double *__restrict__ rhs,
-                                                    const double *__restrict__ a,
-                                                    const double *__restrict__ b,
+                                                    const T *__restrict__ ui,
+                                                    const T *__restrict__ rhs,
+                                                    const T *__restrict__ a,
+                                                    const T *__restrict__ b,
                                                     const BoxArgs g, const StencilCoefs s, int kc,
                                                     int ntx, int nty, int nblocks) {
   using F = Fused6<TX, TY, NT>;
-  __shared__ double R[5 * F::CP];  // red element of every pair, 5-plane ring
-  __shared__ double B[5 * F::CP];  // black element
+  __shared__ T R[5 * F::CP];  // red element of every pair, 5-plane ring
+  __shared__ T B[5 * F::CP];  // black element
   const int bid = blockIdx.x;      // XCD-aware: consecutive tiles on one XCD
   const int q8 = nblocks / 8, r8 = nblocks % 8;
   const int xcd = bid % 8, i8 = bid / 8;
   const int L = xcd * q8 + min(xcd, r8) + i8;
   const int tx_ = L % ntx, ty_ = (L / ntx) % nty, tz_ = L / (ntx * nty);
   const int z0 = tz_ * kc;
-  fused6_segment<TX, TY, NT, ZIN, BC, ACC>(R, B, uo, acc, ui, rhs, a, b, g, s, tx_ * TX,
+  fused6_segment<T, TX, TY, NT, ZIN, BC, ACC>(R, B, uo, acc, ui, rhs, a, b, g, s, tx_ * TX,
                                            ty_ * TY, z0, min(z0 + kc, g.nz));
 }
 
@@ -385,19 +414,20 @@ struct Blk {
   static constexpr int NP = (NRP + NT - 1) / NT;
 };
 
-template <int TX, int TY, int TZ, int NT, bool ZIN, bool BC, bool ACC>
-__global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
+template <class T, int TX, int TY, int TZ, int NT, bool ZIN, bool BC, bool ACC>
+__global__ __launch_bounds__(NT) void k_gsrb_block(T *__restrict__ uo,
                                                    double *__restrict__ acc,
-                                                   const double *__restrict__ ui,
-                                                   const double *__restrict__ rhs,
-                                                   const double *__restrict__ a,
-                                                   const double *__restrict__ b,
-                                                   const BoxArgs g, const StencilCoefs s, int ntx,
+                                                   const T *__restrict__ ui,
+                                                   const T *__restrict__ rhs,
+                                                   const T *__restrict__ a,
+                                                   const T *__restrict__ b,
+                                                   const BoxArgs g, const StencilCoefs s64, int ntx,
                                                    int nty, int nblocks, int ox, int oy, int oz) {
   using F = Blk<TX, TY, TZ, NT>;
+  const SC<T> s(s64);
   constexpr int PW = F::PW, CP = F::CP, NREG = F::NREG, NRP = F::NRP, NL = F::NL, NP = F::NP;
-  __shared__ double R[NREG];  // red element of every region pair
-  __shared__ double B[NREG];  // black element
+  __shared__ T R[NREG];  // red element of every region pair
+  __shared__ T B[NREG];  // black element
   const int bid = blockIdx.x;  // XCD-aware: consecutive tiles on one XCD
   const int q8 = nblocks / 8, r8 = nblocks % 8;
   const int L = (bid % 8) * q8 + min(bid % 8, r8) + bid / 8;
@@ -415,7 +445,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
 
   // 1. issue every load: the u region (tile + 2) and the ring's rhs/a/b
-  double2 v[NL];
+  V2<T> v[NL];
   if (!ZIN) {
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
@@ -423,10 +453,11 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
       const int pz = c / CP, rem = c - pz * CP, r = rem / PW, m = rem - r * PW;
       const long off = (long)min(x0 - 2 + 2 * m, xpmax) + (long)clampi(y0 - 2 + r, -2, ny + 1) * sy +
                        (long)clampi(z0 - 2 + pz, -2, nz + 1) * sz;
-      v[i] = *reinterpret_cast<const double2 *>(ui + (c < NREG ? off : 0));
+      v[i] = *reinterpret_cast<const V2<T> *>(ui + (c < NREG ? off : 0));
     }
   }
-  double cr[NP][2], ca[NP][2], cb[NP][2], ac[NP][2];
+  T cr[NP][2], ca[NP][2], cb[NP][2];
+  double ac[NP][2];  // ACC: the sum field (fp64)
   int rgx0[NP], rgy[NP], rgz[NP], rci[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
@@ -439,9 +470,9 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
     const long off = c < NRP ? (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], -1, ny) * sy +
                                    (long)clampi(rgz[i], -1, nz) * sz
                              : 0;
-    const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
-    const double2 va = *reinterpret_cast<const double2 *>(a + off);
-    const double2 vb = BC ? make_double2(s.bval, s.bval) : *reinterpret_cast<const double2 *>(b + off);
+    const V2<T> vr = *reinterpret_cast<const V2<T> *>(rhs + off);
+    const V2<T> va = *reinterpret_cast<const V2<T> *>(a + off);
+    const V2<T> vb = BC ? mk2<T>(s.bval, s.bval) : *reinterpret_cast<const V2<T> *>(b + off);
     cr[i][0] = vr.x; cr[i][1] = vr.y;
     ca[i][0] = va.x; ca[i][1] = va.y;
     cb[i][0] = vb.x; cb[i][1] = vb.y;
@@ -459,7 +490,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
     if (NL * NT > NREG && c >= NREG) continue;
     const int pz = c / CP, rem = c - pz * CP, r = rem / PW;
     const int q = (q0 + y0 - 2 + r + z0 - 2 + pz) & 1;  // 1: the red element is the second
-    const double u0 = ZIN ? 0.0 : v[i].x, u1 = ZIN ? 0.0 : v[i].y;
+    const T u0 = ZIN ? (T)0 : v[i].x, u1 = ZIN ? (T)0 : v[i].y;
     R[c] = bsel(q, u1, u0);
     B[c] = bsel(q, u0, u1);
   }
@@ -474,7 +505,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
     __syncthreads();
     const int n3[3] = {nx, ny, nz}, o3[3] = {x0 - 2, y0 - 2, z0 - 2};
     constexpr int E3[3] = {TX + 4, TY + 4, TZ + 4};  // region extent per direction
-    auto lds = [&](int x, int y, int z) -> double * {  // the LDS slot of cell (x, y, z)
+    auto lds = [&](int x, int y, int z) -> T * {  // the LDS slot of cell (x, y, z)
       const int rx = x - o3[0];
       const int idx = ((z - o3[2]) * F::LH + (y - o3[1])) * PW + (rx >> 1);
       const int red = (rx & 1) == ((q0 + y + z) & 1);
@@ -497,22 +528,22 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
         c[dir] = gc;
         c[d0] = lo0 + t % w0;
         c[d1] = lo1 + t / w0;
-        double *gp = lds(c[0], c[1], c[2]);
+        T *gp = lds(c[0], c[1], c[2]);
         c[dir] = side == 0 ? 0 : n3[dir] - 1;
-        *gp = ghost_of(mode, g.bcc[face], *lds(c[0], c[1], c[2]));
+        *gp = ghost_of(mode, (T)g.bcc[face], *lds(c[0], c[1], c[2]));
       }
     }
   }
-  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
-                 double rv, double av, double bv) -> double {
-    const double tx = (xp + xm) - 2.0 * uc;
-    const double ty = (yp + ym) - 2.0 * uc;
-    const double tz = (zp + zm) - 2.0 * uc;
-    const double lap = (tx + ty) + tz;                     // .ChF:111-120
-    double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
-    const double ldpsi = lap * s.dxinv * bv;               // .ChF:122
+  auto upd = [&](T uc, T xm, T xp, T ym, T yp, T zm, T zp,
+                 T rv, T av, T bv) -> T {
+    const T tx = (xp + xm) - (T)2 * uc;
+    const T ty = (yp + ym) - (T)2 * uc;
+    const T tz = (zp + zm) - (T)2 * uc;
+    const T lap = (tx + ty) + tz;                     // .ChF:111-120
+    T lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
+    const T ldpsi = lap * s.dxinv * bv;               // .ChF:122
     lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
-    const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
+    const T lam = (T)1 / (av * s.alpha + s.lamshift);  // .cpp:234-243
     return uc - lam * (lofdpsi - rv);                      // .ChF:127-128
   };
   __syncthreads();
@@ -527,8 +558,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
     if (gx < gxlo || gx > gxhi || rgy[i] < gylo || rgy[i] > gyhi || rgz[i] < gzlo || rgz[i] > gzhi)
       continue;
     const int ci = rci[i];
-    const double xm = q ? B[ci] : B[ci - 1];
-    const double xp = q ? B[ci + 1] : B[ci];
+    const T xm = q ? B[ci] : B[ci - 1];
+    const T xp = q ? B[ci + 1] : B[ci];
     R[ci] = upd(R[ci], xm, xp, B[ci - PW], B[ci + PW], B[ci - CP], B[ci + CP],
                 bsel(q, cr[i][1], cr[i][0]), bsel(q, ca[i][1], ca[i][0]), bsel(q, cb[i][1], cb[i][0]));
   }
@@ -543,25 +574,26 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(double *__restrict__ uo,
     const int qb = 1 - ((q0 + gy + gz) & 1);  // 1: the black element is the second
     const int gx = rgx0[i] + qb;
     const int ci = rci[i];
-    const double red = R[ci];
-    double blk = B[ci];
+    const T red = R[ci];
+    T blk = B[ci];
     if (gx < nx) {
-      const double xm = qb ? R[ci] : R[ci - 1];
-      const double xp = qb ? R[ci + 1] : R[ci];
+      const T xm = qb ? R[ci] : R[ci - 1];
+      const T xp = qb ? R[ci + 1] : R[ci];
       blk = upd(blk, xm, xp, R[ci - PW], R[ci + PW], R[ci - CP], R[ci + CP], bsel(qb, cr[i][1], cr[i][0]),
                 bsel(qb, ca[i][1], ca[i][0]), bsel(qb, cb[i][1], cb[i][0]));
     }
-    double2 w;
+    V2<T> w;
     w.x = bsel(qb, red, blk);
     w.y = bsel(qb, blk, red);
     const long off = (long)rgx0[i] + (long)gy * sy + (long)gz * sz;
     if (ACC) {
-      w.x = ac[i][0] + w.x;
-      w.y = ac[i][1] + w.y;
-      if (rgx0[i] + 1 < nx) *reinterpret_cast<double2 *>(acc + off) = w;
-      else acc[off] = w.x;
+      double2 t;
+      t.x = ac[i][0] + (double)w.x;
+      t.y = ac[i][1] + (double)w.y;
+      if (rgx0[i] + 1 < nx) *reinterpret_cast<double2 *>(acc + off) = t;
+      else acc[off] = t.x;
     } else if (rgx0[i] + 1 < nx) {
-      *reinterpret_cast<double2 *>(uo + off) = w;
+      *reinterpret_cast<V2<T> *>(uo + off) = w;
     } else {
       uo[off] = w.x;
     }
@@ -1228,13 +1260,13 @@ static int choose_kc(int tiles, int nz, int slots, int overlap) {
   return best;
 }
 
-template <int TX, int TY, int NT>
-static void launch_fused6(double *u_out, double *u_in, const double *rhs, const double *a,
-                          const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                          double *acc, hipStream_t st) {
+template <class T, int TX, int TY, int NT>
+static void launch_fused6(T *u_out, T *u_in, const T *rhs, const T *a, const T *b,
+                          const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
+                          hipStream_t st) {
   // the domain BC is applied as the planes enter LDS (no fill launch)
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
-  static const int slots = resident_slots(k_gsrb_fused6<TX, TY, NT, false, false, false>, NT);
+  static const int slots = resident_slots(k_gsrb_fused6<T, TX, TY, NT, false, false, false>, NT);
   static const int kc_mode = [] {
     const char *e = getenv("MGIC_KC_MODE");
     return e ? atoi(e) : 0;
@@ -1251,8 +1283,8 @@ static void launch_fused6(double *u_out, double *u_in, const double *rhs, const 
   const int nblocks = ntx * nty * ntz;
   const dim3 grid((unsigned)nblocks), block(NT);
 #define MGIC_F6(Z, B, A)                                                                     \
-  k_gsrb_fused6<TX, TY, NT, Z, B, A><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, b, g, s, \
-                                                             kc, ntx, nty, nblocks)
+  k_gsrb_fused6<T, TX, TY, NT, Z, B, A><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, b, g, \
+                                                                s, kc, ntx, nty, nblocks)
   if (acc) {  // last sweep of a V-cycle at depth 0: phi += e in the same pass
     if (zero_in) throw Error(kBadArg, "fused sweep: accumulate on a zero input");
     if (s.bconst) MGIC_F6(false, true, true);
@@ -1317,8 +1349,9 @@ void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, co
 
 // tile shape, for measurement (MGIC_FUSED_VARIANT): 0 = 128x16 / 512 threads
 // (default: one 106 KB workgroup per CU, 1 KB contiguous rows, u halo 1.29x,
-// coefficient ring 1.16x), 1 = 60x8 / 256 (4 workgroups per CU), 2 = 256x8 / 512.
-// 512^3 sweep: 0.89 / 1.05 / 0.90 ms; 256^3: 0.142 / 0.168 / 0.145 ms.
+// coefficient ring 1.16x), 1 = 60x8 / 256 (4 workgroups per CU); a 256x8 /
+// 512 variant measured 0.90 ms.  512^3 sweep: 0.89 / 1.05 ms; 256^3: 0.142 /
+// 0.168 ms.
 static int fused_variant() {
   static int v = [] {
     const char *e = getenv("MGIC_FUSED_VARIANT");
@@ -1330,11 +1363,10 @@ static int fused_variant() {
 // the sweep on the tiles covering the region o + [0, e) of the box (the
 // whole box, or a slab along one face); cells of those tiles outside the
 // region are computed too (the same values)
-template <int TX, int TY, int TZ, int NT>
-static void launch_block(double *u_out, double *u_in, const double *rhs, const double *a,
-                         const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                         double *acc, hipStream_t st, const int *o = nullptr,
-                         const int *e = nullptr) {
+template <class T, int TX, int TY, int TZ, int NT>
+static void launch_block(T *u_out, T *u_in, const T *rhs, const T *a, const T *b,
+                         const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
+                         hipStream_t st, const int *o = nullptr, const int *e = nullptr) {
   const int ox = o ? o[0] : 0, oy = o ? o[1] : 0, oz = o ? o[2] : 0;
   const int ex = e ? e[0] : g.nx, ey = e ? e[1] : g.ny, ez = e ? e[2] : g.nz;
   if (ox & 1) throw Error(kBadArg, "block sweep: odd x origin");
@@ -1343,8 +1375,8 @@ static void launch_block(double *u_out, double *u_in, const double *rhs, const d
   if (nblocks <= 0) return;
   const dim3 grid((unsigned)nblocks), block(NT);
 #define MGIC_BK(Z, B, A)                                                                     \
-  k_gsrb_block<TX, TY, TZ, NT, Z, B, A><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, b, g, s, \
-                                                                ntx, nty, nblocks, ox, oy, oz)
+  k_gsrb_block<T, TX, TY, TZ, NT, Z, B, A><<<grid, block, 0, st>>>(                          \
+      u_out, acc, u_in, rhs, a, b, g, s, ntx, nty, nblocks, ox, oy, oz)
   if (acc) {
     if (zero_in) throw Error(kBadArg, "fused sweep: accumulate on a zero input");
     if (s.bconst) MGIC_BK(false, true, true);
@@ -1387,16 +1419,26 @@ void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const doub
     // 32x8x4 / 256 threads: 64^3 0.0094 ms, 128^3 0.026 ms per sweep; 32x8x8
     // 0.0116 / 0.0278; 16x8x8, 16x8x4, 32x4x4 (128 threads) were slower still
     if (block_variant() == 1)
-      launch_block<32, 8, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+      launch_block<double, 32, 8, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
     else
-      launch_block<32, 8, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+      launch_block<double, 32, 8, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
     return;
   }
-  switch (fused_variant()) {
-    case 1: launch_fused6<60, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
-    case 2: launch_fused6<256, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
-    default: launch_fused6<128, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st); break;
-  }
+  if (fused_variant() == 1)
+    launch_fused6<double, 60, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+  else
+    launch_fused6<double, 128, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+}
+
+// fp32 sweeps (the mixed-precision V-cycle): the same kernels with float
+// elements and 8-B pairs; acc (phi) stays fp64
+void gsrb_sweep_fused_f(float *u_out, float *u_in, const float *rhs, const float *a,
+                        const float *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
+                        double *acc, int kind, hipStream_t st) {
+  if (kind == 3 || (kind != 2 && (long)g.nx * g.ny * g.nz <= block_max_cells()))
+    launch_block<float, 32, 8, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+  else
+    launch_fused6<float, 128, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
 }
 
 template <int TX, int TY, int NT>
@@ -1456,11 +1498,11 @@ void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const doub
       const int x0 = o[0] & ~1;
       e[0] += o[0] - x0;
       o[0] = x0;
-      launch_block<4, 16, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
+      launch_block<double, 4, 16, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
     } else if (dir == 1) {
-      launch_block<32, 2, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
+      launch_block<double, 32, 2, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
     } else {
-      launch_block<32, 8, 2, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
+      launch_block<double, 32, 8, 2, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
     }
   }
 }

@@ -88,6 +88,7 @@ _sig = {
     "orc_mg_precond": [ctypes.c_void_p, c_int, c_int, c_int],
     "orc_mg_one_cycle": [ctypes.c_void_p, c_int],
     "orc_mg_iteration": [ctypes.c_void_p, c_int],
+    "orc_mg_fmg": [ctypes.c_void_p, c_int, c_int],
     "orc_mg_init_residual": [ctypes.c_void_p, c_int],
     "orc_mg_bicgstab": [ctypes.c_void_p, c_int, c_int, c_int, c_int],
     "orc_mg_amr_precond": [ctypes.c_void_p, c_int, c_int, c_int],
@@ -104,7 +105,7 @@ _sig = {
     "orc_set_threads": [c_int],
     "orc_get_threads": [],
 }
-_res = {"orc_mg_create": ctypes.c_void_p, "orc_mg_dx": c_double, "orc_mg_iteration": c_double,
+_res = {"orc_mg_create": ctypes.c_void_p, "orc_mg_dx": c_double, "orc_mg_iteration": c_double, "orc_mg_fmg": c_double,
         "orc_mg_init_residual": c_double, "orc_mg_norm": c_double, "orc_mg_dot": c_double}
 for _n, _a in _sig.items():
     _f = getattr(_lib, _n)
@@ -329,6 +330,9 @@ class OracleMG:
 
     def iteration(self, norm_type=0) -> float:
         return _lib.orc_mg_iteration(self._h, int(norm_type))
+
+    def fmg(self, ncycles=1, norm_type=0) -> float:
+        return _lib.orc_mg_fmg(self._h, int(ncycles), int(norm_type))
 
     def init_residual(self, norm_type=0) -> float:
         return _lib.orc_mg_init_residual(self._h, int(norm_type))

@@ -816,6 +816,38 @@ double orc_mg_iteration(orc_mg *mg, int norm_type) {
   return orc_mg_norm(mg, 0, ORC_RESID, norm_type);
 }
 
+/* Full multigrid (FMG) from RESID at level 0 (as left by init_residual /
+ * iteration), the schedule of mg_ic_code_amd/csrc/op.cpp MultiGrid::fmg:
+ * RESID(l+1) = restrictResidual of a zero CORR(l) at every depth, the bottom
+ * solve from zero, then per finer depth CORR = P CORR(l+1) and `ncycles`
+ * oneCycle(CORR, RESID); PHI += CORR(0); RESID = RHS - L(PHI).  Not a
+ * reference algorithm (BASELINE config C5 names FMG; Chombo's AMRMultiGrid
+ * has no FMG driver), so parity unpinned. */
+double orc_mg_fmg(orc_mg *mg, int ncycles, int norm_type) {
+  const orc_mg_params *p = &mg->prm;
+  const int D = mg->nlev;
+  if (D == 1) {
+    lv_zero_all(mg, 0, ORC_CORR);
+    orc_mg_one_cycle(mg, 0);
+  } else {
+    for (int l = 0; l + 1 < D; ++l) {
+      lv_zero_all(mg, l, ORC_CORR);
+      orc_mg_restrict_residual(mg, l, ORC_CORR, ORC_RESID);
+    }
+    lv_zero_all(mg, D - 1, ORC_CORR);
+    if (p->bottom_solver == 1) orc_mg_bicgstab(mg, D - 1, ORC_CORR, ORC_RESID, 1);
+    else orc_mg_relax(mg, D - 1, ORC_CORR, ORC_RESID, p->n_bottom);
+    for (int l = D - 2; l >= 0; --l) {
+      lv_zero_all(mg, l, ORC_CORR);
+      orc_mg_prolong_increment(mg, l, ORC_CORR);
+      for (int c = 0; c < ncycles; ++c) orc_mg_one_cycle(mg, l);
+    }
+  }
+  lv_op(mg, 0, ORC_PHI, ORC_CORR, 1.0, 1);
+  orc_mg_residual(mg, 0, ORC_RESID, ORC_PHI, ORC_RHS, 0);
+  return orc_mg_norm(mg, 0, ORC_RESID, norm_type);
+}
+
 /* ------------------------------------------------------------------ */
 /* Input generator at psi = 1                                          */
 /* ------------------------------------------------------------------ */

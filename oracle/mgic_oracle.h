@@ -139,6 +139,8 @@ void orc_mg_one_cycle(orc_mg *mg, int level);
 /* one AMRMultiGrid iteration at level 0: CORR=0, oneCycle, PHI+=CORR,
  * RESID = RHS - L(PHI); returns norm(RESID, norm_type) */
 double orc_mg_iteration(orc_mg *mg, int norm_type);
+/* full multigrid from RESID at level 0: PHI += FMG correction (see .c) */
+double orc_mg_fmg(orc_mg *mg, int ncycles, int norm_type);
 /* RESID = RHS - L(PHI) on level 0, returns its norm */
 double orc_mg_init_residual(orc_mg *mg, int norm_type);
 /* BiCGStab (homogeneous) on a level: solves L e = r for fields fe, fr */

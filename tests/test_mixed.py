@@ -1,0 +1,216 @@
+"""Mixed precision (fp32 smoother / fp64 residual) and FMG -- BASELINE config C5.
+
+GPU tests compare the MixedMultiGrid with the float32 restatement in
+oracle/mixed.py bit for bit (single box), multi-box layouts with the single
+box, and the fp64 FMG with the C oracle's orc_mg_fmg.  CPU tests check the
+restatement itself (iterative refinement around an fp32 V-cycle reaches
+the fp64 residual floor, FMG's first cycle lands near the V-cycle's).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from oracle.mixed import MixedOracle
+
+
+def _problem(rng, shape, bvar):
+    nx, ny, nz = shape
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    b = rng.uniform(0.5, 2.0, (nz, ny, nx)) if bvar else np.ones((nz, ny, nx))
+    rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    return a, b, rhs
+
+
+def _oracle(dom, dx, a, b, rhs, nlevels, bc_lo=(0, 0, 0), bc_hi=(0, 0, 0), bcv=0.0,
+            bottom=0):
+    o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi,
+                        bc_value=bcv, nlevels=nlevels, avg_type=1, prolong_type=1,
+                        bottom_solver=bottom)
+    for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs)):
+        o.set(0, f, 0, arr)
+    o.setup()
+    return o
+
+
+# ------------------------------------------------------------------ CPU
+def test_mixed_oracle_refinement_reaches_fp64_floor():
+    rng = np.random.default_rng(4)
+    n = 16
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    a, b, rhs = _problem(rng, (n, n, n), True)
+    m = MixedOracle(_oracle(dom, 100.0 / n, a, b, rhs, 3), 1.0, -1.0)
+    hist = [np.abs(m.init_residual(np.zeros((n, n, n)))).max()]
+    for _ in range(5):
+        hist.append(np.abs(m.iteration()).max())
+    o = _oracle(dom, 100.0 / n, a, b, rhs, 3)
+    ref = [o.init_residual(0)] + [o.iteration(0) for _ in range(5)]
+    # the fp32 cycle contracts like the fp64 one until fp32 roundoff, and the
+    # fp64 residual keeps the refinement going to the fp64 floor
+    assert hist[1] < 2 * ref[1] and hist[2] < 2 * ref[2]
+    assert hist[-1] < 1e-13 * hist[0]
+
+
+def test_fmg_oracles_first_cycle():
+    rng = np.random.default_rng(5)
+    n = 32
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    a, b, rhs = _problem(rng, (n, n, n), False)
+    o = _oracle(dom, 100.0 / n, a, b, rhs, 3)
+    r0 = o.init_residual(0)
+    r1 = o.fmg(1, 0)
+    o2 = _oracle(dom, 100.0 / n, a, b, rhs, 3)
+    o2.init_residual(0)
+    v1 = o2.iteration(0)
+    assert r1 < 1e-3 * r0 and r1 < 3 * v1
+    m = MixedOracle(_oracle(dom, 100.0 / n, a, b, rhs, 3), 1.0, -1.0)
+    m.init_residual(np.zeros((n, n, n)))
+    assert np.abs(m.fmg(1)).max() < 1.01 * r1 + 1e-12
+
+
+# ------------------------------------------------------------------ GPU
+@pytest.fixture(scope="module")
+def comm():
+    import mg_ic_code_amd as mg
+    return mg.Comm()
+
+
+def _gpu(comm, dom, boxes, dx, a, b, rhs, nlevels, fused, bc_lo=(0, 0, 0), bc_hi=(0, 0, 0),
+         bcv=0.0, periodic=(0, 0, 0)):
+    import mg_ic_code_amd as mg
+    grid = mg.Grid(comm, dom, boxes, dx, periodic=periodic)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    shape = tuple(dom[3 + d] - dom[d] + 1 for d in range(3))[::-1]
+    off = dom[:3]
+    for f, arr in ((fa, a), (fb, b), (frhs, rhs)):
+        for k in range(grid.num_local):
+            bx = grid.local_box(k)
+            f.upload(k, arr[bx[2] - off[2]:bx[5] - off[2] + 1, bx[1] - off[1]:bx[4] - off[1] + 1,
+                            bx[0] - off[0]:bx[3] - off[0] + 1])
+    fphi.set_zero()
+    prm = mg.OperatorParams(alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bcv,
+                            coefficient_average_type=1, prolong_type=1, fused_smoother=fused)
+    fac = mg.defineOperatorFactory(grid, fa, fb, prm)
+    sp = mg.SolverParams(max_depth=nlevels - 1, bottom_solver=0)
+    return dict(grid=grid, fphi=fphi, frhs=frhs, fres=fres, fac=fac, sp=sp, shape=shape, off=off)
+
+
+def _phi(S):
+    out = np.zeros(S["shape"])
+    off = S["off"]
+    for k in range(S["grid"].num_local):
+        bx = S["grid"].local_box(k)
+        out[bx[2] - off[2]:bx[5] - off[2] + 1, bx[1] - off[1]:bx[4] - off[1] + 1,
+            bx[0] - off[0]:bx[3] - off[0] + 1] = S["fphi"].download(k)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [2, 3])
+@pytest.mark.parametrize("bvar", [False, True])
+@pytest.mark.parametrize("use_fmg", [False, True])
+def test_mixed_vcycle_matches_fp32_oracle_bitwise(comm, fused, bvar, use_fmg):
+    import mg_ic_code_amd as mg
+    rng = np.random.default_rng(9)
+    shape = (48, 40, 56)
+    lo = (-16, 8, 32)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    dx = 0.37
+    bc_lo, bc_hi, bcv = (0, 1, 0), (1, 0, 1), 0.25
+    a, b, rhs = _problem(rng, shape, bvar)
+    S = _gpu(comm, dom, [dom], dx, a, b, rhs, 3, fused, bc_lo, bc_hi, bcv)
+    mm = mg.MixedMultiGrid(S["fac"], S["sp"])
+    assert mm.num_depths == 3
+    m = MixedOracle(_oracle(dom, dx, a, b, rhs, 3, bc_lo, bc_hi, bcv), 1.0, -1.0, bc_lo, bc_hi)
+    g0 = mm.init_residual(S["fphi"], S["frhs"], S["fres"], 0)
+    o0 = np.abs(m.init_residual(np.zeros(shape[::-1]))).max()
+    assert g0 == o0
+    steps = [("fmg" if use_fmg else "it")] + ["it"] * 2
+    for st in steps:
+        if st == "fmg":
+            g = mm.fmg(S["fphi"], S["frhs"], S["fres"], 0, ncycles=1)
+            r = m.fmg(1)
+        else:
+            g = mm.iteration(S["fphi"], S["frhs"], S["fres"], 0)
+            r = m.iteration()
+        assert g == np.abs(r).max()
+    assert np.array_equal(_phi(S), m.phi)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rccl", [False, True])
+def test_mixed_multibox_matches_single_box(rccl):
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.decomposition import split_domain
+    rng = np.random.default_rng(10)
+    n = 64
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    a, b, rhs = _problem(rng, (n, n, n), True)
+    out = []
+    for parts in ((1, 1, 1), (2, 2, 2)):
+        if rccl and parts != (1, 1, 1):
+            comm = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+            comm.set_self_messages(True)
+        else:
+            comm = mg.Comm()
+        S = _gpu(comm, dom, split_domain(dom, parts), 100.0 / n, a, b, rhs, 3, 1,
+                 periodic=(1, 0, 1))
+        mm = mg.MixedMultiGrid(S["fac"], S["sp"])
+        hist = [mm.init_residual(S["fphi"], S["frhs"], S["fres"], 0),
+                mm.fmg(S["fphi"], S["frhs"], S["fres"], 0)]
+        hist += [mm.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
+        out.append((hist, _phi(S)))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [(1, 1, 1), (2, 1, 2)])
+@pytest.mark.parametrize("ncycles", [1, 2])
+def test_fmg_fp64_matches_oracle(comm, parts, ncycles):
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.decomposition import split_domain
+    rng = np.random.default_rng(11)
+    n = 32
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    a, b, rhs = _problem(rng, (n, n, n), True)
+    S = _gpu(comm, dom, split_domain(dom, parts), 100.0 / n, a, b, rhs, 3, 1)
+    amg = mg.AMRMultiGrid(S["fac"], S["sp"])
+    o = _oracle(dom, 100.0 / n, a, b, rhs, 3)
+    assert amg.init_residual(S["fphi"], S["frhs"], S["fres"], 0) == o.init_residual(0)
+    assert amg.fmg(S["fphi"], S["frhs"], S["fres"], 0, ncycles=ncycles) == o.fmg(ncycles, 0)
+    assert amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) == o.iteration(0)
+    assert np.array_equal(_phi(S), o.get(0, oracle.PHI, 0))
+
+
+@pytest.mark.gpu
+def test_mixed_vcycle_at_scale_converges_like_fp64(comm):
+    # 256^3 (C2-sized) SetBinaryBH inputs: the mixed cycle's residual history
+    # tracks the fp64 cycle's until fp32 roundoff and keeps falling after
+    import os
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.params import read_params_file
+    prm = read_params_file(os.path.join(os.path.dirname(__file__), "golden", "params.txt"))
+    n = 256
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    grid = mg.Grid(comm, dom, [dom], prm.L / n)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    bh = prm.bh()
+    bh["domain_length"] = prm.L
+    mg.set_binary_bh_coefs(fa, frhs, bh)
+    fb.set_val(1.0)
+    op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, coefficient_average_type=1,
+                           prolong_type=1)
+    fac = mg.defineOperatorFactory(grid, fa, fb, op)
+    sp = mg.SolverParams(max_depth=3, bottom_solver=0)
+    hists = []
+    for kind in ("fp64", "mixed"):
+        fphi.set_zero()
+        solver = mg.AMRMultiGrid(fac, sp) if kind == "fp64" else mg.MixedMultiGrid(fac, sp)
+        h = [solver.init_residual(fphi, frhs, fres, 0)]
+        h += [solver.iteration(fphi, frhs, fres, 0) for _ in range(6)]
+        hists.append(h)
+    f64, mix = hists
+    assert mix[0] == f64[0]
+    for i in (1, 2, 3):
+        assert mix[i] < 1.5 * f64[i]
+    assert mix[-1] < mix[-2] or mix[-1] < 1e-12 * mix[0]
