@@ -324,7 +324,9 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     // first exchange, rhs/coefficient ghosts) is what the side step reads
     if (overlap) MGIC_HIP(hipEventRecord(evM, st));
     for (int b = 0; b < grid->nlocal(); ++b) {
-      const long nc = grid->geom[b].valid.ncells();
+      // the roofline instrumentation times the sweep kernels only (the
+      // sweep+restriction launch moves other bytes)
+      const long nc = last && restrict_last ? 0 : grid->geom[b].valid.ncells();
       prof_mark(st, nc, true, 2 * k);
       if (k == 2)  // two sweeps in one launch (temporal blocking)
         kern::gsrb_sweep_fused2x(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
