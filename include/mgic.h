@@ -48,6 +48,7 @@ typedef struct mgic_op_s *mgic_op;           /* VariableCoeffPoissonOperator */
 typedef struct mgic_mg_s *mgic_mg;           /* AMRMultiGrid on one AMR level */
 typedef struct mgic_plan_s *mgic_plan;       /* host-side view of a Copier plan */
 typedef struct mgic_mixed_s *mgic_mixed;     /* fp32-smoother / fp64-residual V-cycle */
+typedef struct mgic_amr_s *mgic_amr;         /* AMR hierarchy (levels > 0, ratio 2) */
 
 /* Operator constants and ParseBC state (params.txt keys alpha, beta, bc_lo,
  * bc_hi, bc_value, coefficient_average_type; [Chombo] statics). */
@@ -247,6 +248,42 @@ MGIC_API int mgic_mixed_iteration(mgic_mixed m, mgic_field phi, mgic_field rhs, 
                                   int norm_type, double *norm);
 MGIC_API int mgic_mixed_fmg(mgic_mixed m, mgic_field phi, mgic_field rhs, mgic_field resid,
                             int norm_type, int ncycles, double *norm);
+
+/* ---- AMR levels > 0 ([Chombo] AMRPoissonOp multi-level
+ * operators restated: QuadCFInterp, AMROperator / AMRResidual (reflux a
+ * no-op as in the reference), AMRRestrict, AMRProlong, AMRUpdateResidual,
+ * AMRMultiGrid's multi-level V-cycle).  grids[0] tiles its domain; level
+ * l+1's domain is level l's refined by 2 and its boxes are properly nested
+ * (mgic_grid_create_patches).  Level 0 is solved by its MultiGrid (base). */
+MGIC_API int mgic_grid_create_patches(mgic_comm c, const int domain[6], const int periodic[3],
+                                      double dx, int nbox, const int *boxes, const int *owners,
+                                      mgic_grid *out); /* disjoint boxes inside the domain */
+MGIC_API int mgic_amr_create(int nlevels, const mgic_grid *grids, const mgic_field *acoef,
+                             const mgic_field *bcoef, const mgic_op_params *op,
+                             const mgic_mg_params *base, mgic_amr *out);
+MGIC_API int mgic_amr_destroy(mgic_amr a);
+MGIC_API int mgic_amr_num_levels(mgic_amr a, int *n);
+MGIC_API int mgic_amr_level_op(mgic_amr a, int level, mgic_op *out); /* borrowed */
+/* coarse == NULL: homogeneousCFInterp (zero coarse field) */
+MGIC_API int mgic_amr_cf_interp(mgic_amr a, int level, mgic_field u, mgic_field coarse);
+MGIC_API int mgic_amr_average_down(mgic_amr a, int level, mgic_field coarse, mgic_field fine);
+MGIC_API int mgic_amr_operator(mgic_amr a, int level, mgic_field lphi, mgic_field phi,
+                               mgic_field phi_coarse, int homogeneous);
+MGIC_API int mgic_amr_residual(mgic_amr a, int level, mgic_field r, mgic_field phi,
+                               mgic_field phi_coarse, mgic_field rhs, int homogeneous);
+MGIC_API int mgic_amr_restrict(mgic_amr a, int level, mgic_field res_coarse, mgic_field res,
+                               mgic_field corr, mgic_field corr_coarse);
+MGIC_API int mgic_amr_prolong(mgic_amr a, int level, mgic_field corr, mgic_field corr_coarse);
+MGIC_API int mgic_amr_update_residual(mgic_amr a, int level, mgic_field res, mgic_field corr,
+                                      mgic_field corr_coarse);
+/* composite residuals rhs - L(phi) on every level (covered coarse cells
+ * zeroed); *norm = max over levels (norm_type >= 0) */
+MGIC_API int mgic_amr_init_residual(mgic_amr a, const mgic_field *phi, const mgic_field *rhs,
+                                    int norm_type, double *norm);
+/* one AMR V-cycle, phi += e on every level, average down, new residuals */
+MGIC_API int mgic_amr_iteration(mgic_amr a, const mgic_field *phi, const mgic_field *rhs,
+                                int norm_type, double *norm);
+MGIC_API int mgic_amr_residual_field(mgic_amr a, int level, mgic_field *out); /* borrowed */
 
 /* MultilevelLinearOp::preCond: e = 0, then `iters` AMRMultiGrid iterations
  * on (e, r), homogeneous BC (Main_PoissonSolver.cpp:107-117) */

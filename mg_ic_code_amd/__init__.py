@@ -7,6 +7,7 @@ reference's operator / factory / solver interface (see core.py).
 """
 from .core import (  # noqa: F401
     AMRMultiGrid,
+    AMRSolver,
     BiCGStabSolver,
     Comm,
     Grid,

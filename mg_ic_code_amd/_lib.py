@@ -159,6 +159,22 @@ SIGNATURES = {
     "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_precondition": [H, H, H, c_int],
     "mgic_mg_fmg": [H, H, H, H, c_int, c_int, c_int, PD],
+    "mgic_grid_create_patches": [H, PI, PI, c_double, c_int, PI, PI, PH],
+    "mgic_amr_create": [c_int, POINTER(H), POINTER(H), POINTER(H), POINTER(OpParams),
+                        POINTER(MGParams), PH],
+    "mgic_amr_destroy": [H],
+    "mgic_amr_num_levels": [H, PI],
+    "mgic_amr_level_op": [H, c_int, PH],
+    "mgic_amr_cf_interp": [H, c_int, H, H],
+    "mgic_amr_average_down": [H, c_int, H, H],
+    "mgic_amr_operator": [H, c_int, H, H, H, c_int],
+    "mgic_amr_residual": [H, c_int, H, H, H, H, c_int],
+    "mgic_amr_restrict": [H, c_int, H, H, H, H],
+    "mgic_amr_prolong": [H, c_int, H, H],
+    "mgic_amr_update_residual": [H, c_int, H, H, H],
+    "mgic_amr_init_residual": [H, POINTER(H), POINTER(H), c_int, PD],
+    "mgic_amr_iteration": [H, POINTER(H), POINTER(H), c_int, PD],
+    "mgic_amr_residual_field": [H, c_int, PH],
     "mgic_mixed_create": [H, POINTER(MGParams), PH],
     "mgic_mixed_destroy": [H],
     "mgic_mixed_num_depths": [H, PI],

@@ -125,7 +125,9 @@ class Grid:
 
     def __init__(self, comm: Comm, domain: Box6, boxes: Sequence[Box6], dx: float,
                  periodic: Sequence[int] = (0, 0, 0), owners: Optional[Sequence[int]] = None,
-                 _handle=None):
+                 _handle=None, patches: bool = False):
+        """patches: an AMR level > 0 (disjoint boxes inside the domain, not
+        tiling it)"""
         self.comm = comm
         self.domain = tuple(int(v) for v in domain)
         self.boxes = [tuple(int(v) for v in b) for b in boxes]
@@ -137,9 +139,9 @@ class Grid:
         else:
             h = ctypes.c_void_p()
             flat = [v for b in self.boxes for v in b]
-            call("mgic_grid_create", comm.handle, _ints(self.domain), _ints(self.periodic),
-                 ctypes.c_double(self.dx), len(self.boxes), _ints(flat), _ints(self.owners),
-                 ctypes.byref(h))
+            call("mgic_grid_create_patches" if patches else "mgic_grid_create", comm.handle,
+                 _ints(self.domain), _ints(self.periodic), ctypes.c_double(self.dx),
+                 len(self.boxes), _ints(flat), _ints(self.owners), ctypes.byref(h))
             self._h = h
 
     @property
@@ -606,6 +608,86 @@ class MixedMultiGrid:
         h = getattr(self, "_h", None)
         if h:
             lib.mgic_mixed_destroy(h)
+            self._h = None
+
+
+class AMRSolver:
+    """AMR levels > 0: levels = [(grid, aCoef, bCoef), ...]
+    from the coarsest; each finer grid is Grid(..., patches=True) on the
+    coarser domain refined by 2, properly nested.  The [Chombo] AMRPoissonOp
+    multi-level operators (QuadCFInterp, AMROperator/AMRResidual with reflux a
+    no-op, AMRRestrict, AMRProlong, AMRUpdateResidual) and AMRMultiGrid's
+    multi-level V-cycle; level 0 is solved by its own MultiGrid (params)."""
+
+    def __init__(self, levels, op_params: OperatorParams, params: Optional[SolverParams] = None):
+        self.levels = list(levels)
+        n = len(self.levels)
+        grids = (ctypes.c_void_p * n)(*[g.handle.value for g, _, _ in self.levels])
+        acs = (ctypes.c_void_p * n)(*[a.handle.value for _, a, _ in self.levels])
+        bcs = (ctypes.c_void_p * n)(*[b.handle.value for _, _, b in self.levels])
+        op = op_params.to_c()
+        self.params = params or SolverParams()
+        mp = self.params.to_c()
+        h = ctypes.c_void_p()
+        call("mgic_amr_create", n, grids, acs, bcs, ctypes.byref(op), ctypes.byref(mp),
+             ctypes.byref(h))
+        self._h = h
+        self.num_levels = n
+
+    @staticmethod
+    def _f(x):
+        return x.handle if x is not None else None
+
+    def cf_interp(self, level: int, u: LevelData, coarse: Optional[LevelData] = None) -> None:
+        call("mgic_amr_cf_interp", self._h, int(level), u.handle, self._f(coarse))
+
+    def average_down(self, level: int, coarse: LevelData, fine: LevelData) -> None:
+        call("mgic_amr_average_down", self._h, int(level), coarse.handle, fine.handle)
+
+    def AMROperator(self, level, lphi, phi, phi_coarse=None, homogeneous=False) -> None:
+        call("mgic_amr_operator", self._h, int(level), lphi.handle, phi.handle,
+             self._f(phi_coarse), int(bool(homogeneous)))
+
+    def AMRResidual(self, level, r, phi, phi_coarse, rhs, homogeneous=False) -> None:
+        call("mgic_amr_residual", self._h, int(level), r.handle, phi.handle,
+             self._f(phi_coarse), rhs.handle, int(bool(homogeneous)))
+
+    def AMRRestrict(self, level, res_coarse, res, corr, corr_coarse=None) -> None:
+        call("mgic_amr_restrict", self._h, int(level), res_coarse.handle, res.handle,
+             corr.handle, self._f(corr_coarse))
+
+    def AMRProlong(self, level, corr, corr_coarse) -> None:
+        call("mgic_amr_prolong", self._h, int(level), corr.handle, corr_coarse.handle)
+
+    def AMRUpdateResidual(self, level, res, corr, corr_coarse=None) -> None:
+        call("mgic_amr_update_residual", self._h, int(level), res.handle, corr.handle,
+             self._f(corr_coarse))
+
+    def _fields(self, fs):
+        assert len(fs) == self.num_levels
+        return (ctypes.c_void_p * self.num_levels)(*[f.handle.value for f in fs])
+
+    def init_residual(self, phis, rhss, norm_type: int = 0) -> float:
+        out = ctypes.c_double()
+        call("mgic_amr_init_residual", self._h, self._fields(phis), self._fields(rhss),
+             int(norm_type), ctypes.byref(out))
+        return out.value
+
+    def iteration(self, phis, rhss, norm_type: int = 0) -> float:
+        out = ctypes.c_double()
+        call("mgic_amr_iteration", self._h, self._fields(phis), self._fields(rhss),
+             int(norm_type), ctypes.byref(out))
+        return out.value
+
+    def residual_field(self, level: int) -> LevelData:
+        h = ctypes.c_void_p()
+        call("mgic_amr_residual_field", self._h, int(level), ctypes.byref(h))
+        return LevelData(self.levels[level][0], _handle=h, _owner=self)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.mgic_amr_destroy(h)
             self._h = None
 
 

@@ -4,6 +4,7 @@
 #include <string>
 
 #include "../../include/mgic.h"
+#include "amr.hpp"
 #include "mixed.hpp"
 #include "op.hpp"
 
@@ -27,6 +28,9 @@ struct mgic_op_s {
 };
 struct mgic_mg_s {
   AMRMultiGrid amg;
+};
+struct mgic_amr_s {
+  AMRSolver amr;
 };
 struct mgic_mixed_s {
   MixedMultiGrid mm;
@@ -872,6 +876,196 @@ MGIC_API int mgic_mixed_fmg(mgic_mixed m, mgic_field phi, mgic_field rhs, mgic_f
     MGIC_CHECK(ncycles >= 1, "ncycles must be >= 1");
     const double v = m->mm.fmg(*phi->f, *rhs->f, resid ? resid->f.get() : nullptr, norm_type, ncycles);
     if (norm) *norm = v;
+  });
+}
+
+// ---------------------------------------------------------------- AMR levels
+MGIC_API int mgic_grid_create_patches(mgic_comm c, const int domain[6], const int periodic[3],
+                                      double dx, int nbox, const int *boxes, const int *owners,
+                                      mgic_grid *out) {
+  return guard([&] {
+    NEED(c);
+    NEED(domain);
+    NEED(boxes);
+    NEED(out);
+    MGIC_CHECK(nbox >= 1, "nbox must be >= 1");
+    MGIC_CHECK(dx > 0.0, "dx must be positive");
+    bool per[3] = {false, false, false};
+    if (periodic)
+      for (int d = 0; d < 3; ++d) per[d] = periodic[d] != 0;
+    const Box dom = Box::make(domain);
+    std::vector<Box> bx;
+    std::vector<int> own;
+    long vol = 0;
+    for (int b = 0; b < nbox; ++b) {
+      bx.push_back(Box::make(boxes + 6 * b));
+      MGIC_CHECK(!bx.back().empty() && dom.contains(bx.back()), "patch boxes must lie in the domain");
+      vol += bx.back().ncells();
+      own.push_back(owners ? owners[b] : 0);
+    }
+    for (int a = 0; a < nbox; ++a)
+      for (int b = a + 1; b < nbox; ++b)
+        MGIC_CHECK(bx[a].intersect(bx[b]).empty(), "patch boxes must be disjoint");
+    *out = new mgic_grid_s{std::make_shared<Grid>(c->c, dom, per, dx, bx, own)};
+  });
+}
+
+MGIC_API int mgic_amr_create(int nlevels, const mgic_grid *grids, const mgic_field *acoef,
+                             const mgic_field *bcoef, const mgic_op_params *op,
+                             const mgic_mg_params *base, mgic_amr *out) {
+  return guard([&] {
+    NEED(grids);
+    NEED(acoef);
+    NEED(bcoef);
+    NEED(out);
+    MGIC_CHECK(nlevels >= 1, "nlevels must be >= 1");
+    std::vector<AMRLevelSpec> lv;
+    for (int l = 0; l < nlevels; ++l) {
+      NEED(grids[l]);
+      NEED(acoef[l]);
+      NEED(bcoef[l]);
+      lv.push_back({grids[l]->g, acoef[l]->f, bcoef[l]->f});
+    }
+    auto *h = new mgic_amr_s;
+    try {
+      h->amr.define(lv, to_op(op), to_mg(base));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+MGIC_API int mgic_amr_destroy(mgic_amr a) {
+  return guard([&] { delete a; });
+}
+MGIC_API int mgic_amr_num_levels(mgic_amr a, int *n) {
+  return guard([&] {
+    NEED(a);
+    NEED(n);
+    *n = a->amr.numLevels();
+  });
+}
+static void amr_level(mgic_amr a, int l, int lo) {
+  MGIC_CHECK(l >= lo && l < a->amr.numLevels(), "bad AMR level");
+}
+MGIC_API int mgic_amr_level_op(mgic_amr a, int level, mgic_op *out) {
+  return guard([&] {
+    NEED(a);
+    NEED(out);
+    amr_level(a, level, 0);
+    auto *h = new mgic_op_s;
+    h->op = &a->amr.op(level);
+    *out = h;
+  });
+}
+MGIC_API int mgic_amr_cf_interp(mgic_amr a, int level, mgic_field u, mgic_field coarse) {
+  return guard([&] {
+    NEED(a);
+    NEED(u);
+    amr_level(a, level, 1);
+    a->amr.cf(level).interp(*u->f, coarse ? coarse->f.get() : nullptr, a->amr.op(level).stream());
+  });
+}
+MGIC_API int mgic_amr_average_down(mgic_amr a, int level, mgic_field coarse, mgic_field fine) {
+  return guard([&] {
+    NEED(a);
+    NEED(coarse);
+    NEED(fine);
+    amr_level(a, level, 1);
+    a->amr.cf(level).averageDown(*coarse->f, *fine->f, a->amr.op(level).stream());
+  });
+}
+MGIC_API int mgic_amr_operator(mgic_amr a, int level, mgic_field lphi, mgic_field phi,
+                               mgic_field phi_coarse, int h) {
+  return guard([&] {
+    NEED(a);
+    NEED(lphi);
+    NEED(phi);
+    amr_level(a, level, 0);
+    a->amr.AMROperator(level, *lphi->f, *phi->f, phi_coarse ? phi_coarse->f.get() : nullptr, h != 0);
+  });
+}
+MGIC_API int mgic_amr_residual(mgic_amr a, int level, mgic_field r, mgic_field phi,
+                               mgic_field phi_coarse, mgic_field rhs, int h) {
+  return guard([&] {
+    NEED(a);
+    NEED(r);
+    NEED(phi);
+    NEED(rhs);
+    amr_level(a, level, 0);
+    a->amr.AMRResidual(level, *r->f, *phi->f, phi_coarse ? phi_coarse->f.get() : nullptr, *rhs->f,
+                       h != 0);
+  });
+}
+MGIC_API int mgic_amr_restrict(mgic_amr a, int level, mgic_field res_coarse, mgic_field res,
+                               mgic_field corr, mgic_field corr_coarse) {
+  return guard([&] {
+    NEED(a);
+    NEED(res_coarse);
+    NEED(res);
+    NEED(corr);
+    amr_level(a, level, 1);
+    a->amr.AMRRestrict(level, *res_coarse->f, *res->f, *corr->f,
+                       corr_coarse ? corr_coarse->f.get() : nullptr);
+  });
+}
+MGIC_API int mgic_amr_prolong(mgic_amr a, int level, mgic_field corr, mgic_field corr_coarse) {
+  return guard([&] {
+    NEED(a);
+    NEED(corr);
+    NEED(corr_coarse);
+    amr_level(a, level, 1);
+    a->amr.AMRProlong(level, *corr->f, *corr_coarse->f);
+  });
+}
+MGIC_API int mgic_amr_update_residual(mgic_amr a, int level, mgic_field res, mgic_field corr,
+                                      mgic_field corr_coarse) {
+  return guard([&] {
+    NEED(a);
+    NEED(res);
+    NEED(corr);
+    amr_level(a, level, 1);
+    a->amr.AMRUpdateResidual(level, *res->f, *corr->f, corr_coarse ? corr_coarse->f.get() : nullptr);
+  });
+}
+static std::vector<LevelData *> amr_fields(mgic_amr a, const mgic_field *f) {
+  std::vector<LevelData *> v;
+  for (int l = 0; l < a->amr.numLevels(); ++l) {
+    MGIC_CHECK(f[l] != nullptr, "null field");
+    check_same_layout(*a->amr.op(l).grid, *f[l]->f, "AMR field");
+    v.push_back(f[l]->f.get());
+  }
+  return v;
+}
+MGIC_API int mgic_amr_init_residual(mgic_amr a, const mgic_field *phi, const mgic_field *rhs,
+                                    int norm_type, double *norm) {
+  return guard([&] {
+    NEED(a);
+    NEED(phi);
+    NEED(rhs);
+    auto p = amr_fields(a, phi);
+    const double v = a->amr.initResidual(p, amr_fields(a, rhs), norm_type);
+    if (norm) *norm = v;
+  });
+}
+MGIC_API int mgic_amr_iteration(mgic_amr a, const mgic_field *phi, const mgic_field *rhs,
+                                int norm_type, double *norm) {
+  return guard([&] {
+    NEED(a);
+    NEED(phi);
+    NEED(rhs);
+    auto p = amr_fields(a, phi);
+    const double v = a->amr.iteration(p, amr_fields(a, rhs), norm_type);
+    if (norm) *norm = v;
+  });
+}
+MGIC_API int mgic_amr_residual_field(mgic_amr a, int level, mgic_field *out) {
+  return guard([&] {
+    NEED(a);
+    NEED(out);
+    amr_level(a, level, 0);
+    *out = borrowed_field(&a->amr.residual(level));
   });
 }
 

@@ -633,6 +633,118 @@ __global__ __launch_bounds__(256) void k_copy_f(float *__restrict__ d, const flo
   d[idx] = s[idx];
 }
 
+// ---- coarse-fine interpolation ([Chombo] QuadCFInterp, restated) ---------
+// A ghost cell g of a fine box face that is not a domain face takes the
+// quadratic through (normal coordinate, fine cells h from the face = 0):
+//   phi* at -h (the centre of the coarse cell that holds g, tangentially
+//           interpolated to g's position), f1 at h/2, f2 at 3h/2,
+// evaluated at -h/2:  g = 8/15 phi* + 2/3 f1 - 1/5 f2   (ratio 2).
+// phi* = c0 + sum_t (x_t d1_t + x_t^2/2 d2_t) + x_1 x_2 d12 with x_t = +-1/4
+// (the fine cell's offset in coarse cells), centred differences where both
+// tangential coarse neighbours are usable (inside the domain or periodic, not
+// covered by the fine level), one-sided first differences (d2 = 0) where one
+// is, nothing where none is; the mixed term needs all four diagonals.
+// Homogeneous (HOM): phi* = 0 (a zero coarse correction).
+__device__ __forceinline__ bool cf_covered(int x, int y, int z, const CFArgs &c) {
+  for (int n = 0; n < c.ncov; ++n) {
+    const int *b = c.cov + 6 * n;
+    if (x >= b[0] && x <= b[3] && y >= b[1] && y <= b[4] && z >= b[2] && z <= b[5]) return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ bool cf_usable(int p[3], const CFArgs &c) {
+  int q[3];
+  for (int d = 0; d < 3; ++d) {
+    q[d] = p[d];
+    const int n = c.cdom_hi[d] - c.cdom_lo[d] + 1;
+    if (q[d] < c.cdom_lo[d] || q[d] > c.cdom_hi[d]) {
+      if (!c.periodic[d]) return false;
+      q[d] = c.cdom_lo[d] + ((q[d] - c.cdom_lo[d]) % n + n) % n;
+    }
+  }
+  return !cf_covered(q[0], q[1], q[2], c);
+}
+
+template <bool HOM>
+__global__ __launch_bounds__(256) void k_cf_interp(double *__restrict__ u,
+                                                   const double *__restrict__ cs, const BoxArgs g,
+                                                   const CFArgs c) {
+  const int dir = c.face >> 1, side = c.face & 1;
+  const int d0 = dir == 0 ? 1 : 0, d1 = dir == 2 ? 1 : 2;
+  const int n[3] = {g.nx, g.ny, g.nz};
+  const int a0 = (int)(blockIdx.x * blockDim.x + threadIdx.x), a1 = (int)blockIdx.y;
+  if (a0 >= n[d0] || a1 >= n[d1]) return;
+  int l[3];  // local fine index of the ghost
+  l[dir] = side ? n[dir] : -1;
+  l[d0] = a0;
+  l[d1] = a1;
+  const long st[3] = {1, g.sy, g.sz};
+  const long gi = (long)l[0] + (long)l[1] * g.sy + (long)l[2] * g.sz;
+  const long in = side ? -st[dir] : st[dir];  // one cell into the box
+  const double f1 = u[gi + in], f2 = u[gi + 2 * in];
+  double ps = 0.0;
+  if (!HOM) {
+    int gf[3], gc[3];
+    for (int d = 0; d < 3; ++d) {
+      gf[d] = c.flo[d] + l[d];
+      gc[d] = gf[d] >= 0 ? gf[d] / 2 : -((-gf[d] + 1) / 2);  // floor(gf / 2)
+    }
+    auto at = [&](int x, int y, int z) {
+      return cs[(long)(x - c.clo[0]) + (long)(y - c.clo[1]) * c.csy + (long)(z - c.clo[2]) * c.csz];
+    };
+    const double c0 = at(gc[0], gc[1], gc[2]);
+    const int td[2] = {d0, d1};
+    double d1v[2], d2v[2], xt[2];
+    bool okp[2], okm[2];
+    for (int t = 0; t < 2; ++t) {
+      const int d = td[t];
+      xt[t] = (gf[d] - 2 * gc[d]) ? 0.25 : -0.25;
+      int pp[3] = {gc[0], gc[1], gc[2]}, pm[3] = {gc[0], gc[1], gc[2]};
+      pp[d] += 1;
+      pm[d] -= 1;
+      okp[t] = cf_usable(pp, c);
+      okm[t] = cf_usable(pm, c);
+      const double vp = okp[t] ? at(pp[0], pp[1], pp[2]) : 0.0;
+      const double vm = okm[t] ? at(pm[0], pm[1], pm[2]) : 0.0;
+      if (okp[t] && okm[t]) {
+        d1v[t] = (vp - vm) * 0.5;
+        d2v[t] = (vp - 2.0 * c0) + vm;
+      } else if (okp[t]) {
+        d1v[t] = vp - c0;
+        d2v[t] = 0.0;
+      } else if (okm[t]) {
+        d1v[t] = c0 - vm;
+        d2v[t] = 0.0;
+      } else {
+        d1v[t] = 0.0;
+        d2v[t] = 0.0;
+      }
+    }
+    double d12 = 0.0;
+    {
+      bool all = true;
+      double v[4];
+      int q = 0;
+      for (int s1 = -1; s1 <= 1; s1 += 2)
+        for (int s0 = -1; s0 <= 1; s0 += 2) {
+          int p[3] = {gc[0], gc[1], gc[2]};
+          p[d0] += s0;
+          p[d1] += s1;
+          const bool ok = cf_usable(p, c);
+          all = all && ok;
+          v[q++] = ok ? at(p[0], p[1], p[2]) : 0.0;
+        }
+      // v: (-,-), (+,-), (-,+), (+,+) in (d0, d1)
+      if (all) d12 = (((v[3] - v[2]) - v[1]) + v[0]) * 0.25;
+    }
+    ps = c0;
+    for (int t = 0; t < 2; ++t) ps = ps + (xt[t] * d1v[t] + 0.5 * (xt[t] * xt[t]) * d2v[t]);
+    ps = ps + (xt[0] * xt[1]) * d12;
+  }
+  u[gi] = ((8.0 / 15.0) * ps + (2.0 / 3.0) * f1) + (-0.2) * f2;
+}
+
 }  // namespace
 
 void gsrb_pass(double *u, const double *rhs, const double *a, const double *b, const double *lam,
@@ -899,6 +1011,18 @@ void to_float(float *d, const double *s, const BoxArgs &g, int grow, hipStream_t
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
   k_to_float<<<grid_cells(g.nx + 2 * grow, g.ny + 2 * grow, g.nz + 2 * grow), kBlock, 0, st>>>(
       d, s, g, grow);
+  check_launch();
+}
+
+void cf_interp(double *u, const double *coarse_stage, const BoxArgs &g, const CFArgs &c,
+               bool homogeneous, hipStream_t st) {
+  const int dir = c.face >> 1;
+  const int n[3] = {g.nx, g.ny, g.nz};
+  const int d0 = dir == 0 ? 1 : 0, d1 = dir == 2 ? 1 : 2;
+  if (n[dir] < 2) throw Error(kBadArg, "cf_interp: a box needs 2 cells normal to a CF face");
+  const dim3 grid((unsigned)((n[d0] + 255) / 256), (unsigned)n[d1]);
+  if (homogeneous) k_cf_interp<true><<<grid, 256, 0, st>>>(u, coarse_stage, g, c);
+  else k_cf_interp<false><<<grid, 256, 0, st>>>(u, coarse_stage, g, c);
   check_launch();
 }
 

@@ -131,5 +131,19 @@ void to_float(float *d, const double *s, const BoxArgs &g, int grow, hipStream_t
 void copy_f(float *d, const float *s, const BoxArgs &g, hipStream_t st);
 void incr_f(double *x, const float *y, const BoxArgs &g, hipStream_t st);  // x += (double)y
 
+// ---- coarse-fine interpolation on one face of one fine box (AMR levels)
+struct CFArgs {
+  int face;                      // 0..5 (dir * 2 + side)
+  int flo[3];                    // fine box valid lo (global fine index)
+  int clo[3];                    // staged coarse box valid lo (global coarse index)
+  long csy, csz;                 // its strides (valid-lo based pointer)
+  int cdom_lo[3], cdom_hi[3];    // coarse problem domain
+  int periodic[3];
+  int ncov;                      // coarsened fine boxes of the level (covered test)
+  const int *cov;                // device, 6 ints each (global coarse index)
+};
+void cf_interp(double *u, const double *coarse_stage, const BoxArgs &g, const CFArgs &c,
+               bool homogeneous, hipStream_t st);
+
 }  // namespace kern
 }  // namespace mgic

@@ -163,7 +163,8 @@ void VariableCoeffPoissonOperator::restrictResidual(LevelData &resC, LevelData &
                "restrictResidual: coarse box is not coarsen(fine box, 2)");
   }
   const hipStream_t st = stream();
-  if (exchange) dpsiF.exchange(st);  // .cpp:163 (BC of :158-161 folded, homogeneous)
+  if (cf) cf_homogeneous(*cf, dpsiF, st);  // .cpp:156
+  if (exchange || cf) dpsiF.exchange(st);  // .cpp:163 (BC of :158-161 folded, homogeneous)
   const StencilCoefs s = coefs();
   for (int n = 0; n < grid->nlocal(); ++n)
     kern::restrict_residual(resC.p[n], cg.box_args_plain(n), dpsiF.p[n], rhsF.p[n], m_aCoef->p[n],
@@ -236,6 +237,7 @@ void VariableCoeffPoissonOperator::setTime(double t) {
 }
 
 bool VariableCoeffPoissonOperator::fusedSmootherApplies() const {
+  if (cf) return false;  // CF ghosts are refilled before every colour pass
   // Both colour passes of a sweep in one launch per box.  Faces on the
   // domain boundary fold the BC; exchanged faces (box or periodic
   // neighbours) get a 2-deep ghost shell before the sweep, from which the
@@ -437,6 +439,7 @@ void VariableCoeffPoissonOperator::levelGSRB(LevelData &dpsi, const LevelData &r
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
   for (int pass = 0; pass <= 1; ++pass) {  // .cpp:290
+    if (cf) cf_homogeneous(*cf, dpsi, st);  // .cpp:296
     dpsi.exchange(st);                      // .cpp:301 (BC of :307-310 folded)
     for (int n = 0; n < grid->nlocal(); ++n) {
       const long nc = grid->geom[n].valid.ncells();

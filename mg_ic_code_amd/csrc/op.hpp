@@ -16,6 +16,10 @@
 
 namespace mgic {
 
+struct CFLevel;  // amr.hpp: the coarse-fine interface of an AMR level > 0
+// homogeneousCFInterp: the CF ghosts of u from a zero coarse field
+void cf_homogeneous(CFLevel &cf, LevelData &u, hipStream_t st);
+
 // ParseBC state (SetBCs.cpp GlobalBCRS + ParmParse bc_value) and the
 // operator constants/options of params.txt.
 struct OpParams {
@@ -102,6 +106,10 @@ class VariableCoeffPoissonOperator {
   std::unique_ptr<LevelData> m_lambda;
   bool m_lambdaNeedsResetting = true;
   bool coef_ghosts_ = false;  // aCoef/bCoef face ghosts exchanged (fused sweep)
+  // AMR level > 0 (AMRnewOp with a coarser level): levelGSRB and
+  // restrictResidual fill the CF ghosts by homogeneousCFInterp first
+  // (.cpp:156, :296); the per-colour kernels are used on such levels
+  std::shared_ptr<CFLevel> cf;
   bool b_const_ = false;      // bCoef holds one value everywhere (all ranks)
   double b_val_ = 1.0;
 

@@ -1,0 +1,311 @@
+"""numpy restatement of the AMR multi-level operators -- TEST INFRASTRUCTURE ONLY.
+
+The checker for mg_ic_code_amd/csrc/amr.cpp on
+hierarchies with one box per level.  fp64, every expression in the GPU
+kernels' order, so results are bit-identical:
+
+* coarse-fine interpolation ([Chombo] QuadCFInterp, restated; the
+  reference calls homogeneousCFInterp at
+  Source/VariableCoeffPoissonOperator.cpp:156,296): ghost of a non-domain
+  face = ((8/15) phi* + (2/3) f1) + (-0.2) f2, phi* the coarse value
+  tangentially interpolated (centred / one-sided / none by usable
+  neighbours, plus the mixed term), 0 when homogeneous;
+* GSRB colour passes (GSRBHELMHOLTZVC3D, .ChF:91-136), residual
+  (VCCOMPUTERES3D, .ChF:283-339) with the physical BC folded in;
+* CoarseAverage (sum of 8 children * 1/8), piecewise-constant prolongation;
+* the AMR V-cycle of amr.cpp: l_base = 0 solved by the C oracle's
+  MultiGrid one_cycle, finer levels smoothed with homogeneous CF ghosts,
+  AMRRestrict / AMRProlong / AMRUpdateResidual, reflux a no-op
+  (.cpp:264-271).
+Parity unpinned against Chombo (its AMR code is not in the reference tree).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle
+
+W0, W1, W2 = 8.0 / 15.0, 2.0 / 3.0, -0.2
+
+
+class Level:
+    def __init__(self, box, dx, a, b, domain, bc_lo, bc_hi, bc_value, alpha, beta):
+        self.box = tuple(box)  # lo0 lo1 lo2 hi0 hi1 hi2
+        self.dx = dx
+        self.a, self.b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        self.domain = tuple(domain)
+        self.bc_lo, self.bc_hi, self.bc_value = tuple(bc_lo), tuple(bc_hi), bc_value
+        self.alpha, self.beta = alpha, beta
+        self.dxinv = 1.0 / (dx * dx)
+        self.lamshift = 2.0 * 3 * beta / (dx * dx)
+
+    @property
+    def shape(self):
+        b = self.box
+        return (b[5] - b[2] + 1, b[4] - b[1] + 1, b[3] - b[0] + 1)
+
+    def full(self, v=None):
+        out = np.zeros(tuple(s + 2 for s in self.shape))
+        if v is not None:
+            out[1:-1, 1:-1, 1:-1] = v
+        return out
+
+    def domain_face(self, dir, side):
+        b, d = self.box, self.domain
+        return b[3 + dir] == d[3 + dir] if side else b[dir] == d[dir]
+
+    # -------------------------------------------------------------- ghosts
+    def fill_bc(self, u, hom):
+        """physical BC images on domain faces (DiriBC: c - near with c =
+        2 value; NeumBC: near (+ isign dx value)); faces only"""
+        for dir in range(3):
+            ax = 2 - dir
+            for side in (0, 1):
+                if not self.domain_face(dir, side):
+                    continue
+                flag = self.bc_hi[dir] if side else self.bc_lo[dir]
+                g, n = [slice(1, -1)] * 3, [slice(1, -1)] * 3
+                g[ax], n[ax] = (-1, -2) if side else (0, 1)
+                near = u[tuple(n)]
+                if flag == 0:  # Dirichlet
+                    c = 0.0 if hom else 2.0 * self.bc_value
+                    u[tuple(g)] = c - near
+                elif hom:
+                    u[tuple(g)] = near
+                else:
+                    c = (1.0 if side else -1.0) * self.dx * self.bc_value
+                    u[tuple(g)] = near + c
+
+    def cf_interp(self, u, coarse=None, cov=(), cdomain=None):
+        """ghosts of the non-domain faces from the coarse level (lv, full
+        array) or zero; cov: coarsened fine boxes (covered test)"""
+        b = self.box
+        for dir in range(3):
+            ax = 2 - dir
+            for side in (0, 1):
+                if self.domain_face(dir, side):
+                    continue
+                d0, d1 = (1, 2) if dir == 0 else ((0, 2) if dir == 1 else (0, 1))
+                n = [b[3 + d] - b[d] + 1 for d in range(3)]
+                A0, A1 = np.meshgrid(np.arange(n[d0]), np.arange(n[d1]), indexing="ij")
+                loc = [None] * 3
+                loc[dir] = np.full(A0.shape, n[dir] if side else -1)
+                loc[d0], loc[d1] = A0, A1
+                gi = tuple(loc[2 - a] + 1 for a in range(3))  # (z, y, x) in the full array
+                step = -1 if side else 1
+                i1 = list(gi)
+                i1[ax] = i1[ax] + step
+                i2 = list(gi)
+                i2[ax] = i2[ax] + 2 * step
+                f1, f2 = u[tuple(i1)], u[tuple(i2)]
+                if coarse is None:
+                    ps = np.zeros(A0.shape)
+                else:
+                    ps = self._phistar(loc, dir, d0, d1, coarse, cov, cdomain)
+                u[gi] = (W0 * ps + W1 * f1) + W2 * f2
+
+    def _phistar(self, loc, dir, d0, d1, cl, cov, cdom):
+        b = self.box
+        gf = [loc[d] + b[d] for d in range(3)]
+        gc = [np.floor_divide(g, 2) for g in gf]
+        cb = cl.box
+        cu = cl.u_full  # coarse full array (ghost 1)
+
+        def at(p):
+            return cu[p[2] - cb[2] + 1, p[1] - cb[1] + 1, p[0] - cb[0] + 1]
+
+        def usable(p):
+            ok = np.ones(p[0].shape, bool)
+            for d in range(3):
+                ok &= (p[d] >= cdom[d]) & (p[d] <= cdom[3 + d])
+            for c in cov:
+                inside = np.ones(p[0].shape, bool)
+                for d in range(3):
+                    inside &= (p[d] >= c[d]) & (p[d] <= c[3 + d])
+                ok &= ~inside
+            return ok
+
+        c0 = at(gc)
+        d1v, d2v, xt = [], [], []
+        for d in (d0, d1):
+            xt.append(np.where(gf[d] - 2 * gc[d] != 0, 0.25, -0.25))
+            pp = list(gc)
+            pp[d] = gc[d] + 1
+            pm = list(gc)
+            pm[d] = gc[d] - 1
+            okp, okm = usable(pp), usable(pm)
+            vp = np.where(okp, at([np.clip(pp[k], cb[k] - 1, cb[3 + k] + 1) for k in range(3)]), 0.0)
+            vm = np.where(okm, at([np.clip(pm[k], cb[k] - 1, cb[3 + k] + 1) for k in range(3)]), 0.0)
+            both = okp & okm
+            g1 = np.where(both, (vp - vm) * 0.5, np.where(okp, vp - c0, np.where(okm, c0 - vm, 0.0)))
+            g2 = np.where(both, (vp - 2.0 * c0) + vm, 0.0)
+            d1v.append(g1)
+            d2v.append(g2)
+        v, allok = [], np.ones(c0.shape, bool)
+        for s1 in (-1, 1):
+            for s0 in (-1, 1):
+                p = list(gc)
+                p[d0] = gc[d0] + s0
+                p[d1] = gc[d1] + s1
+                ok = usable(p)
+                allok &= ok
+                v.append(np.where(ok, at([np.clip(p[k], cb[k] - 1, cb[3 + k] + 1) for k in range(3)]), 0.0))
+        d12 = np.where(allok, (((v[3] - v[2]) - v[1]) + v[0]) * 0.25, 0.0)
+        ps = c0
+        for t in range(2):
+            ps = ps + (xt[t] * d1v[t] + 0.5 * (xt[t] * xt[t]) * d2v[t])
+        return ps + (xt[0] * xt[1]) * d12
+
+    # -------------------------------------------------------------- kernels
+    def _colour(self, shape):
+        b = self.box
+        k, j, i = np.meshgrid(np.arange(shape[0]) + b[2], np.arange(shape[1]) + b[1],
+                              np.arange(shape[2]) + b[0], indexing="ij")
+        return (i + j + k) % 2
+
+    def _lap(self, u):
+        c = u[1:-1, 1:-1, 1:-1]
+        tx = (u[1:-1, 1:-1, 2:] + u[1:-1, 1:-1, :-2]) - 2.0 * c
+        ty = (u[1:-1, 2:, 1:-1] + u[1:-1, :-2, 1:-1]) - 2.0 * c
+        tz = (u[2:, 1:-1, 1:-1] + u[:-2, 1:-1, 1:-1]) - 2.0 * c
+        return (tx + ty) + tz
+
+    def gsrb_pass(self, u, rhs, colour):
+        c = u[1:-1, 1:-1, 1:-1]
+        lof = self.alpha * self.a * c
+        ldpsi = self._lap(u) * self.dxinv * self.b
+        lof = lof - self.beta * ldpsi
+        lam = 1.0 / (self.a * self.alpha + self.lamshift)
+        new = c - lam * (lof - rhs)
+        m = self._colour(c.shape) == colour
+        c[m] = new[m]
+
+    def residual(self, u, rhs):
+        c = u[1:-1, 1:-1, 1:-1]
+        res = rhs - self.alpha * self.a * c
+        ldpsi = self._lap(u) * self.dxinv * self.beta * self.b
+        return res + ldpsi
+
+
+def average_down(fine: np.ndarray) -> np.ndarray:
+    s = np.zeros(tuple(v // 2 for v in fine.shape))
+    for kk in range(2):
+        for jj in range(2):
+            for ii in range(2):
+                s = s + fine[kk::2, jj::2, ii::2]
+    return s * (1.0 / 8)
+
+
+class AMROracle:
+    """levels: list of dict(box, a, b) from coarsest; level 0's box is the
+    domain.  base: the C oracle's MultiGrid parameters for level 0."""
+
+    def __init__(self, levels, dx0, domain0, alpha=1.0, beta=-1.0, bc_lo=(0, 0, 0),
+                 bc_hi=(0, 0, 0), bc_value=0.0, n_pre=4, n_post=4, base=None):
+        self.L = []
+        dom = tuple(domain0)
+        dx = dx0
+        for lv in levels:
+            self.L.append(Level(lv["box"], dx, lv["a"], lv["b"], dom, bc_lo, bc_hi, bc_value,
+                                alpha, beta))
+            dom = tuple(2 * v if i < 3 else 2 * v + 1 for i, v in enumerate(dom))
+            dx = dx / 2
+        self.n_pre, self.n_post = n_pre, n_post
+        base = dict(base or {})
+        self.o = oracle.OracleMG([self.L[0].box], self.L[0].box, dx0, alpha=alpha, beta=beta,
+                                 bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bc_value, **base)
+        self.o.set(0, oracle.ACOEF, 0, self.L[0].a)
+        self.o.set(0, oracle.BCOEF, 0, self.L[0].b)
+        self.o.setup()
+
+    def cov(self, l):
+        b = self.L[l].box
+        return [tuple([v // 2 for v in b[:3]] + [(v + 1) // 2 - 1 for v in b[3:]])]
+
+    def fill(self, l, u, coarse_full, hom_phys):
+        """CF ghosts (coarse_full None: homogeneous), then the physical BC"""
+        lv = self.L[l]
+        if l > 0:
+            cl = None
+            if coarse_full is not None:
+                cl = self.L[l - 1]
+                cl.u_full = coarse_full
+            lv.cf_interp(u, cl, self.cov(l), self.L[l - 1].domain)
+        lv.fill_bc(u, hom_phys)
+
+    def relax(self, l, e, r, n):
+        lv = self.L[l]
+        for _ in range(n):
+            for colour in (0, 1):
+                self.fill(l, e, None, True)
+                lv.gsrb_pass(e, r, colour)
+
+    def amr_residual(self, l, phi, phi_coarse, rhs, hom=False):
+        self.fill(l, phi, phi_coarse, hom)
+        return self.L[l].residual(phi, rhs)
+
+    def put_covered(self, l, coarse_valid, fine_valid_avg):
+        """write the averaged fine data onto the covered coarse cells"""
+        cb, fb = self.L[l - 1].box, self.L[l].box
+        lo = [fb[d] // 2 - cb[d] for d in range(3)]
+        n = fine_valid_avg.shape
+        coarse_valid[lo[2]:lo[2] + n[0], lo[1]:lo[1] + n[1], lo[0]:lo[0] + n[2]] = fine_valid_avg
+
+    def prolong_const(self, l, e_full, ec_full):
+        cb, fb = self.L[l - 1].box, self.L[l].box
+        lo = [fb[d] // 2 - cb[d] + 1 for d in range(3)]
+        n = [s // 2 for s in self.L[l].shape]
+        c = ec_full[lo[2]:lo[2] + n[0], lo[1]:lo[1] + n[1], lo[0]:lo[0] + n[2]]
+        f = e_full[1:-1, 1:-1, 1:-1]
+        for kk in range(2):
+            for jj in range(2):
+                for ii in range(2):
+                    f[kk::2, jj::2, ii::2] = f[kk::2, jj::2, ii::2] + c
+
+    # ---------------------------------------------------------------- driver
+    def init_residual(self, phis, rhss):
+        """phis: full arrays per level (modified: ghosts); returns residuals"""
+        self.phis, self.rhss = phis, rhss
+        res = []
+        for l in range(len(self.L)):
+            res.append(self.amr_residual(l, phis[l], phis[l - 1] if l else None, rhss[l]))
+        for l in range(1, len(self.L)):
+            self.put_covered(l, res[l - 1], np.zeros(tuple(s // 2 for s in self.L[l].shape)))
+        self.res = res
+        return res
+
+    def cycle(self, l):
+        if l == 0:
+            o = self.o
+            o.set(0, oracle.RESID, 0, self.res[0])
+            o.set(0, oracle.CORR, 0, self.L[0].full(), full=True)
+            o.one_cycle(0)
+            self.corr[0] = self.L[0].full(o.get(0, oracle.CORR, 0))
+            return
+        lv = self.L[l]
+        e = lv.full()
+        self.relax(l, e, self.res[l], self.n_pre)
+        self.corr[l] = e
+        # AMRRestrict: residual of e (homogeneous CF, homogeneous physical BC)
+        r = self.amr_residual(l, e, None, self.res[l], True)
+        self.put_covered(l, self.res[l - 1], average_down(r))
+        self.cycle(l - 1)
+        e = self.corr[l]
+        self.prolong_const(l, e, self.corr[l - 1])
+        # AMRUpdateResidual: CF ghosts of e from e_c
+        self.res[l] = self.amr_residual(l, e, self.corr[l - 1], self.res[l], True)
+        de = lv.full()
+        self.relax(l, de, self.res[l], self.n_post)
+        e[1:-1, 1:-1, 1:-1] = e[1:-1, 1:-1, 1:-1] + de[1:-1, 1:-1, 1:-1]
+
+    def iteration(self):
+        n = len(self.L)
+        self.corr = [None] * n
+        self.cycle(n - 1)
+        for l in range(n):
+            self.phis[l][1:-1, 1:-1, 1:-1] = (self.phis[l][1:-1, 1:-1, 1:-1]
+                                              + self.corr[l][1:-1, 1:-1, 1:-1])
+        for l in range(n - 1, 0, -1):
+            cv = self.phis[l - 1][1:-1, 1:-1, 1:-1]
+            self.put_covered(l, cv, average_down(self.phis[l][1:-1, 1:-1, 1:-1]))
+        return self.init_residual(self.phis, self.rhss)
