@@ -285,6 +285,28 @@ MGIC_API int mgic_amr_iteration(mgic_amr a, const mgic_field *phi, const mgic_fi
                                 int norm_type, double *norm);
 MGIC_API int mgic_amr_residual_field(mgic_amr a, int level, mgic_field *out); /* borrowed */
 
+/* ---- output (WriteOutput.H).  For local box n, planes
+ * [k0, k0+nk) of its valid box: the components the reference writes,
+ * component-major and i fastest (the FArrayBox order of that box's chunk of
+ * "data:datatype=0"), into out (host memory, or device memory if
+ * out_on_device).
+ * grchombo_vars: set_output_data (SetLevelData.cpp:343-396), the 31
+ *   GRChombo variables (GRChomboUserVariables.hpp order) from psi, with
+ *   constant_K = bh[12];
+ * solver_vars: output_solver_data's 10 components (WriteOutput.H:74-100):
+ *   dpsi, rhs, psi, A11_0, A12_0, A13_0, A22_0, A23_0, A33_0, phi_0. */
+MGIC_API int mgic_field_grchombo_vars(mgic_field psi, int n, int k0, int nk, const double bh[13],
+                                      double *out, int out_on_device);
+MGIC_API int mgic_field_solver_vars(mgic_field dpsi, mgic_field rhs, mgic_field psi, int n, int k0,
+                                    int nk, const double bh[13], double *out, int out_on_device);
+/* the field's layout: domain, periodicity, dx, number of boxes (all ranks),
+ * this rank and the job size; box i's extent, owner rank and local index
+ * (-1 if not local); a barrier over the field's communicator */
+MGIC_API int mgic_field_layout(mgic_field f, int domain[6], int periodic[3], double *dx, int *nbox,
+                               int *rank, int *size);
+MGIC_API int mgic_field_box(mgic_field f, int i, int lohi[6], int *owner, int *local_index);
+MGIC_API int mgic_field_barrier(mgic_field f);
+
 /* MultilevelLinearOp::preCond: e = 0, then `iters` AMRMultiGrid iterations
  * on (e, r), homogeneous BC (Main_PoissonSolver.cpp:107-117) */
 MGIC_API int mgic_mg_precondition(mgic_mg mg, mgic_field e, mgic_field r, int iters);

@@ -28,6 +28,7 @@ from .core import (  # noqa: F401
     set_nl_coefs,
     set_device,
 )
-from ._lib import LIB_PATH, lib  # noqa: F401
+from ._lib import IO_LIB_PATH, LIB_PATH, lib  # noqa: F401
+from .output import output_final_data, output_solver_data  # noqa: F401
 
 __version__ = "0.1.0"

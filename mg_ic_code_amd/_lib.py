@@ -183,6 +183,11 @@ SIGNATURES = {
     "mgic_mixed_fmg": [H, H, H, H, c_int, c_int, PD],
     "mgic_solve_params_default": [POINTER(SolveParams)],
     "mgic_mg_solve": [H, H, H, POINTER(SolveParams), PI, PD],
+    "mgic_field_grchombo_vars": [H, c_int, c_int, c_int, PD, c_void_p, c_int],
+    "mgic_field_solver_vars": [H, H, H, c_int, c_int, c_int, PD, c_void_p, c_int],
+    "mgic_field_layout": [H, PI, PI, PD, PI, PI, PI],
+    "mgic_field_box": [H, c_int, PI, PI, PI],
+    "mgic_field_barrier": [H],
     "mgic_prof_smoother": [c_int, c_long],
     "mgic_prof_smoother_read": [PI, POINTER(c_long), PD],
     # ChomboFortran drop-ins (include/mgic_chf.h); argtypes left open
@@ -224,6 +229,41 @@ def _load() -> ctypes.CDLL:
 
 
 lib = _load()
+
+
+# ---- libmgic_io.so (include/mgic_io.h): the HDF5 writers, loaded on first
+# use (it links libhdf5); missing or unloadable = an ImportError, no fallback
+IO_LIB_PATH = os.path.join(_HERE, "libmgic_io.so")
+IO_SIGNATURES = {
+    "mgic_io_last_error": [],
+    "mgic_io_write_final_data": [c_char_p, c_int, PH, PD, c_int, PI],
+    "mgic_io_write_solver_data": [c_char_p, c_int, PH, PH, PH, PD, PI, c_int],
+    "mgic_io_write_host": [c_char_p, c_int, c_int, PI, PI, PI, PD, PI, PD, c_int, c_int],
+}
+_io = None
+
+
+def io_lib() -> ctypes.CDLL:
+    global _io
+    if _io is None:
+        if not os.path.exists(IO_LIB_PATH):
+            raise ImportError(f"{IO_LIB_PATH} not found: build it with __graft_entry__.build()")
+        L = ctypes.CDLL(IO_LIB_PATH)
+        for name, argtypes in IO_SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = argtypes
+            fn.restype = c_char_p if name == "mgic_io_last_error" else c_int
+        _io = L
+    return _io
+
+
+def io_call(name: str, *args) -> int:
+    L = io_lib()
+    st = getattr(L, name)(*args)
+    if st < 0:
+        msg = L.mgic_io_last_error()
+        raise MgicError(name, st, msg.decode() if msg else "")
+    return st
 
 
 def last_error() -> str:

@@ -552,6 +552,110 @@ MGIC_API int mgic_field_nl_integrand(mgic_field psi, mgic_field out, const doubl
                                  g.dx, p, g.comm->stream());
   });
 }
+// ---- output: WriteOutput.H's per-box components, and
+// the layout queries the HDF5 writer (libmgic_io) needs
+// a device staging buffer for results the caller wants on the host (grown on
+// demand, freed at exit)
+static void *scratch_device(size_t bytes) {
+  struct Buf {
+    void *p = nullptr;
+    size_t n = 0;
+    ~Buf() {
+      if (p) (void)hipFree(p);
+    }
+  };
+  static Buf b;
+  if (bytes > b.n) {
+    if (b.p) MGIC_HIP(hipFree(b.p));
+    b.p = nullptr;
+    b.n = 0;
+    MGIC_HIP(hipMalloc(&b.p, bytes));
+    b.n = bytes;
+  }
+  return b.p;
+}
+static void output_vars_capi(int kind, mgic_field psi, mgic_field dpsi, mgic_field rhs, int n,
+                             int k0, int nk, const double bh[13], double *out, int on_device) {
+  NEED(psi);
+  NEED(bh);
+  NEED(out);
+  const LevelData &u = *psi->f;
+  const Grid &g = *u.grid;
+  if (kind == 1) {
+    NEED(dpsi);
+    NEED(rhs);
+    check_same_layout(g, *dpsi->f, "dpsi");
+    check_same_layout(g, *rhs->f, "rhs");
+  }
+  MGIC_CHECK(n >= 0 && n < g.nlocal(), "bad local box index");
+  const FabGeom &fg = g.geom[n];
+  MGIC_CHECK(k0 >= 0 && nk >= 1 && k0 + nk <= fg.nz, "plane range outside the box");
+  const int nc = kind == 0 ? kern::kNumGRChomboVars : kern::kNumSolverVars;
+  const size_t bytes = sizeof(double) * (size_t)nc * fg.nx * fg.ny * nk;
+  const hipStream_t st = g.comm->stream();
+  const BoxArgs a = g.box_args_plain(n);
+  const kern::BhParams p = bh_params(bh);
+  double *d = out;
+  if (!on_device) d = static_cast<double *>(scratch_device(bytes));
+  kern::output_vars(kind, d, u.p[n], kind ? dpsi->f->p[n] : nullptr, kind ? rhs->f->p[n] : nullptr,
+                    a, k0, nk, g.dx, p, st);
+  if (!on_device) {
+    MGIC_HIP(hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, st));
+    MGIC_HIP(hipStreamSynchronize(st));
+  }
+}
+MGIC_API int mgic_field_grchombo_vars(mgic_field psi, int n, int k0, int nk, const double bh[13],
+                                      double *out, int out_on_device) {
+  return guard([&] { output_vars_capi(0, psi, nullptr, nullptr, n, k0, nk, bh, out, out_on_device); });
+}
+MGIC_API int mgic_field_solver_vars(mgic_field dpsi, mgic_field rhs, mgic_field psi, int n, int k0,
+                                    int nk, const double bh[13], double *out, int out_on_device) {
+  return guard([&] { output_vars_capi(1, psi, dpsi, rhs, n, k0, nk, bh, out, out_on_device); });
+}
+MGIC_API int mgic_field_layout(mgic_field f, int domain[6], int periodic[3], double *dx, int *nbox,
+                               int *rank, int *size) {
+  return guard([&] {
+    NEED(f);
+    const Grid &g = *f->f->grid;
+    for (int d = 0; d < 3; ++d) {
+      if (domain) {
+        domain[d] = g.domain.lo[d];
+        domain[3 + d] = g.domain.hi[d];
+      }
+      if (periodic) periodic[d] = g.periodic[d] ? 1 : 0;
+    }
+    if (dx) *dx = g.dx;
+    if (nbox) *nbox = (int)g.boxes.size();
+    if (rank) *rank = g.comm->rank();
+    if (size) *size = g.comm->size();
+  });
+}
+MGIC_API int mgic_field_box(mgic_field f, int i, int lohi[6], int *owner, int *local_index) {
+  return guard([&] {
+    NEED(f);
+    NEED(lohi);
+    const Grid &g = *f->f->grid;
+    MGIC_CHECK(i >= 0 && i < (int)g.boxes.size(), "bad box index");
+    for (int d = 0; d < 3; ++d) {
+      lohi[d] = g.boxes[i].lo[d];
+      lohi[3 + d] = g.boxes[i].hi[d];
+    }
+    if (owner) *owner = g.owners[i];
+    if (local_index) {
+      *local_index = -1;
+      for (int n = 0; n < g.nlocal(); ++n)
+        if (g.local[n] == i) *local_index = n;
+    }
+  });
+}
+MGIC_API int mgic_field_barrier(mgic_field f) {
+  return guard([&] {
+    NEED(f);
+    Comm &c = *f->f->grid->comm;
+    c.allreduce(c.d_result(), 0);  // any collective orders the ranks
+    MGIC_HIP(hipStreamSynchronize(c.stream()));
+  });
+}
 MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]) {
   return mgic_field_nl_coefs(nullptr, acoef, rhs, bh);
 }

@@ -591,6 +591,73 @@ __global__ __launch_bounds__(256) void k_rho_grad_phi(double *__restrict__ r,
   r[idx] = acc;
 }
 
+// ---- output: the components WriteOutput.H writes, for
+// planes [k0, k0 + nk) of a valid box, component-major and i fastest (the
+// FArrayBox order of the HDF5 "data:datatype=0" chunk of that box)
+// KIND 0: set_output_data (SetLevelData.cpp:343-396), the 31 GRChombo
+//         variables (GRChomboUserVariables.hpp order) from psi
+// KIND 1: output_solver_data's tempData (WriteOutput.H:84-100): dpsi, rhs and
+//         the 8 multigrid_vars (psi, A11_0 .. A33_0, phi_0; the A_ij_0 and
+//         phi_0 of set_initial_conditions, SetLevelData.cpp:31-72)
+template <int KIND>
+__global__ __launch_bounds__(256) void k_output_vars(double *__restrict__ out,
+                                                     const double *__restrict__ psi,
+                                                     const double *__restrict__ dpsi,
+                                                     const double *__restrict__ rhs,
+                                                     const BoxArgs g, int k0, int nk, double dx,
+                                                     const BhParams p) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const int iv[3] = {g.glo[0] + i, g.glo[1] + j, g.glo[2] + k0 + k};
+  double loc[3];
+  for (int d = 0; d < 3; ++d) loc[d] = bh_loc(iv[d], dx, p.domlen[d]);
+  double l1[3] = {loc[0] - p.off1, loc[1], loc[2]}, l2[3] = {loc[0] - p.off2, loc[1], loc[2]};
+  const double r1 = sqrt(l1[0] * l1[0] + l1[1] * l1[1] + l1[2] * l1[2]);
+  const double r2 = sqrt(l2[0] * l2[0] + l2[1] * l2[1] + l2[2] * l2[2]);
+  const double n1[3] = {l1[0] / r1, l1[1] / r1, l1[2] / r1};
+  const double n2[3] = {l2[0] / r2, l2[1] / r2, l2[2] / r2};
+  const double J1[3] = {0.0, 0.0, p.spin1}, J2[3] = {0.0, 0.0, p.spin2};
+  const double P1[3] = {0.0, p.mom1, 0.0}, P2[3] = {0.0, p.mom2, 0.0};
+  const double A11 = bh_Aij(0, 0, r1, r2, n1, n2, J1, J2, P1, P2);  // SetBinaryBH.H:77-82
+  const double A22 = bh_Aij(1, 1, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A33 = bh_Aij(2, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A12 = bh_Aij(0, 1, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A13 = bh_Aij(0, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double A23 = bh_Aij(1, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+  const double phi0 = bh_phi(p, loc[0], loc[1], loc[2]);  // MyPhiFunction.H
+  const long idx = (long)i + (long)j * g.sy + (long)(k0 + k) * g.sz;
+  const double psi_c = psi[idx];
+  const long V = (long)g.nx * g.ny * nk;
+  double *o = out + (long)i + (long)g.nx * (j + (long)g.ny * k);
+  if (KIND == 1) {
+    const double v[10] = {dpsi[idx], rhs[idx], psi_c, A11, A12, A13, A22, A23, A33, phi0};
+#pragma unroll
+    for (int c = 0; c < 10; ++c) o[c * V] = v[c];
+    return;
+  }
+  const double psi_bh = p.m1 / r1 + p.m2 / r2;      // SetBinaryBH.H:85-99
+  const double chi = pow(psi_c + psi_bh, -4.0);      // SetLevelData.cpp:381-383
+  const double factor = pow(chi, 1.5);               // :384
+  double v[31];
+#pragma unroll
+  for (int c = 0; c < 31; ++c) v[c] = 0.0;           // :358-361
+  v[1] = v[4] = v[6] = 1.0;                          // h11, h22, h33 (:365-367)
+  v[18] = 1.0;                                       // lapse (:368)
+  v[7] = p.constant_K;                               // K (:371)
+  v[0] = chi;
+  v[25] = phi0;                                      // phi (:387)
+  v[8] = A11 * factor;                               // A11 .. A33 (:388-393)
+  v[9] = A12 * factor;
+  v[10] = A13 * factor;
+  v[11] = A22 * factor;
+  v[12] = A23 * factor;
+  v[13] = A33 * factor;
+#pragma unroll
+  for (int c = 0; c < 31; ++c) o[c * V] = v[c];
+}
+
 inline dim3 grid_cells(int nx, int ny, int nz) {
   return dim3((unsigned)((nx + TX - 1) / TX), (unsigned)((ny + TY - 1) / TY), (unsigned)nz);
 }
@@ -930,6 +997,18 @@ void lap_psi(double *l, const double *psi, const BoxArgs &g, double dx, hipStrea
 void rho_grad_phi(double *r, const double *phi, const BoxArgs &g, double dx, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
   k_rho_grad_phi<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, phi, g, dx);
+  check_launch();
+}
+
+void output_vars(int kind, double *out, const double *psi, const double *dpsi, const double *rhs,
+                 const BoxArgs &g, int k0, int nk, double dx, const BhParams &p, hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || nk <= 0) return;
+  if (kind == 0)
+    k_output_vars<0><<<grid_cells(g.nx, g.ny, nk), kBlock, 0, st>>>(out, psi, dpsi, rhs, g, k0, nk,
+                                                                    dx, p);
+  else
+    k_output_vars<1><<<grid_cells(g.nx, g.ny, nk), kBlock, 0, st>>>(out, psi, dpsi, rhs, g, k0, nk,
+                                                                    dx, p);
   check_launch();
 }
 

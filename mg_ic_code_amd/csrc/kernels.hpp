@@ -112,6 +112,13 @@ void constant_k_integrand(double *out, const double *psi, const BoxArgs &g, doub
 // GETLAPLACIANPSIF / GETRHOGRADPHIF (SetLevelDataF.ChF), operand ghosts as is
 void lap_psi(double *l, const double *psi, const BoxArgs &g, double dx, hipStream_t st);
 void rho_grad_phi(double *r, const double *phi, const BoxArgs &g, double dx, hipStream_t st);
+// WriteOutput.H's components for planes [k0, k0+nk) of a valid box,
+// component-major, i fastest.  kind 0: the 31 GRChombo variables of
+// set_output_data (psi); kind 1: output_solver_data's dpsi, rhs, psi, A_ij_0,
+// phi_0
+constexpr int kNumGRChomboVars = 31, kNumSolverVars = 10;
+void output_vars(int kind, double *out, const double *psi, const double *dpsi, const double *rhs,
+                 const BoxArgs &g, int k0, int nk, double dx, const BhParams &p, hipStream_t st);
 // x += y over the valid box grown by `grow` (<= kGhost) cells
 void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStream_t st);
 

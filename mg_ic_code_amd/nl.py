@@ -15,8 +15,10 @@ max_level = 0:
 On a periodic domain each NL iteration first sets K from the integrability
 condition: K = -sqrt(|sum(integrand) dV| / volume), with the integrand of
 set_constant_K_integrand (:133-147).  Every field stays in HBM, and each step
-is a libmgic kernel.  Not covered: AMR levels (max_level > 0) and the HDF5
-output.
+is a libmgic kernel.  With output_dir set, the reference's HDF5 files are
+written as it writes them: output_solver_data before every solve (:181) and
+output_final_data after the loop (:229), through libmgic_io (output.py).
+Not covered: AMR levels (max_level > 0).
 """
 from __future__ import annotations
 
@@ -25,10 +27,12 @@ from typing import List, Optional
 
 import ctypes
 import math
+import os
 
 from .core import (AMRMultiGrid, BiCGStabSolver, Grid, LevelData, MultilevelLinearOp,
                    OperatorParams, SolverParams, defineOperatorFactory, set_nl_coefs, BH_KEYS)
 from ._lib import call
+from .output import output_final_data, output_solver_data
 from .params import PoissonParameters
 
 
@@ -50,7 +54,8 @@ def set_nl_integrand(psi: LevelData, out: LevelData, bh: dict) -> None:
 
 def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
                   prolong_type: int = 1, bottom_solver: int = 1,
-                  max_NL_iterations: Optional[int] = None) -> NLResult:
+                  max_NL_iterations: Optional[int] = None,
+                  output_dir: Optional[str] = None) -> NLResult:
     periodic = bool(prm.is_periodic)
     if periodic != all(grid.periodic):
         raise ValueError("grid periodicity must match params is_periodic")
@@ -71,7 +76,7 @@ def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
     dx = grid.dx
     ones = integrand = None
     volume = prm.domainLength[0] * prm.domainLength[1] * prm.domainLength[2]
-    for _ in range(n_nl):
+    for it in range(n_nl):
         if periodic:  # integrability condition for K (:133-147)
             if integrand is None:
                 integrand, ones = LevelData(grid), LevelData(grid)
@@ -90,6 +95,9 @@ def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
         solver = BiCGStabSolver(MultilevelLinearOp(amg, prm.numMGIterations),
                                 tolerance=prm.tolerance, max_iterations=prm.max_iterations,
                                 norm_type=0)
+        if output_dir is not None:  # :180-181
+            output_solver_data([dpsi], [rhs], [psi], bh, it, [2],
+                               os.path.join(output_dir, f"vcPoissonOut.3d_{it}.hdf5"))
         res.linear_iterations.append(solver.solve(dpsi, rhs))
         op0 = amg.op(0)
         op0.update_psi(psi, dpsi)
@@ -99,4 +107,7 @@ def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
         if nrm < prm.tolerance or nrm > 1e5:
             res.converged = nrm < prm.tolerance
             break
+    if output_dir is not None:  # :227-230
+        output_final_data([psi], bh, prm.max_level, [2], os.path.join(output_dir,
+                                                                      "vcPoissonFinal.3d.hdf5"))
     return res

@@ -102,6 +102,8 @@ _sig = {
     "orc_nl_integrand": [POINTER(BHParams), PI, PI, c_double, POINTER(c_double),
                          POINTER(c_double)],
     "orc_getlaplacianpsif": [POINTER(c_double), POINTER(c_double), PI, PI, c_double, c_int],
+    "orc_output_vars": [c_int, POINTER(BHParams), PI, PI, c_double, POINTER(c_double),
+                        POINTER(c_double), POINTER(c_double), POINTER(c_double)],
     "orc_set_threads": [c_int],
     "orc_get_threads": [],
 }
@@ -209,6 +211,21 @@ def nl_integrand(bh: dict, lo, hi, dx, psi):
     out = np.empty((hi[2] - lo[2] + 1, hi[1] - lo[1] + 1, hi[0] - lo[0] + 1))
     assert g.shape == tuple(n + 2 for n in out.shape)
     _lib.orc_nl_integrand(ctypes.byref(p), _i3(lo), _i3(hi), dx, _dp(g), _dp(out))
+    return out
+
+
+def output_vars(kind: int, bh: dict, lo, hi, dx, psi, dpsi=None, rhs=None):
+    """WriteOutput.H's components over [lo, hi]: kind 0 the 31 GRChombo
+    variables of set_output_data, kind 1 output_solver_data's 10; arrays
+    (nz, ny, nx), result (ncomp, nz, ny, nx)."""
+    p = _bh_params(bh)
+    shape = (hi[2] - lo[2] + 1, hi[1] - lo[1] + 1, hi[0] - lo[0] + 1)
+    f = lambda a: np.ascontiguousarray(a if a is not None else np.zeros(shape), dtype=np.float64)
+    u, d, r = f(psi), f(dpsi), f(rhs)
+    assert u.shape == d.shape == r.shape == shape
+    out = np.empty((31 if kind == 0 else 10,) + shape)
+    _lib.orc_output_vars(int(kind), ctypes.byref(p), _i3(lo), _i3(hi), float(dx), _dp(u), _dp(d),
+                         _dp(r), _dp(out))
     return out
 
 

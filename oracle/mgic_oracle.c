@@ -1006,6 +1006,63 @@ void orc_binary_bh_coefs(const orc_bh_params *p, const int *lo, const int *hi, d
   orc_nl_coefs(p, lo, hi, dx, NULL, acoef, rhs);
 }
 
+void orc_output_vars(int kind, const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                     const double *psi, const double *dpsi, const double *rhs, double *out) {
+  const double domlen[3] = {p->L, p->L, p->L};
+  const size_t nx = (size_t)(hi[0] - lo[0] + 1), ny = (size_t)(hi[1] - lo[1] + 1),
+               nz = (size_t)(hi[2] - lo[2] + 1);
+  const size_t V = nx * ny * nz;
+  for (int k = lo[2]; k <= hi[2]; ++k)
+    for (int j = lo[1]; j <= hi[1]; ++j)
+      for (int i = lo[0]; i <= hi[0]; ++i) {
+        const int iv[3] = {i, j, k};
+        const size_t n = (size_t)(i - lo[0]) + nx * ((size_t)(j - lo[1]) + ny * (size_t)(k - lo[2]));
+        double loc[3];
+        cell_loc(iv, dx, domlen, loc); /* SetLevelData.cpp:375-378 */
+        /* multigrid_vars A_ij_0, phi_0 as set_initial_conditions left them
+         * (SetLevelData.cpp:60-69, SetBinaryBH.H:55-83) */
+        double l1[3] = {loc[0], loc[1], loc[2]}, l2[3] = {loc[0], loc[1], loc[2]};
+        const double r1 = bh_radius(l1, p->bh1_offset);
+        const double r2 = bh_radius(l2, p->bh2_offset);
+        const double n1[3] = {l1[0] / r1, l1[1] / r1, l1[2] / r1};
+        const double n2[3] = {l2[0] / r2, l2[1] / r2, l2[2] / r2};
+        const double J1[3] = {0.0, 0.0, p->bh1_spin}, J2[3] = {0.0, 0.0, p->bh2_spin};
+        const double P1[3] = {0.0, p->bh1_momentum, 0.0}, P2[3] = {0.0, p->bh2_momentum, 0.0};
+        const double A11 = get_Aij(0, 0, r1, r2, n1, n2, J1, J2, P1, P2);
+        const double A22 = get_Aij(1, 1, r1, r2, n1, n2, J1, J2, P1, P2);
+        const double A33 = get_Aij(2, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+        const double A12 = get_Aij(0, 1, r1, r2, n1, n2, J1, J2, P1, P2);
+        const double A13 = get_Aij(0, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+        const double A23 = get_Aij(1, 2, r1, r2, n1, n2, J1, J2, P1, P2);
+        const double phi0 = phi_fn(p, loc);
+        if (kind == 1) { /* WriteOutput.H:74-100: dpsi, rhs, then multigrid_vars */
+          const double v[10] = {dpsi[n], rhs[n], psi[n], A11, A12, A13, A22, A23, A33, phi0};
+          for (int c = 0; c < 10; ++c) out[c * V + n] = v[c];
+          continue;
+        }
+        /* set_output_data, SetLevelData.cpp:357-394 */
+        double v[31];
+        for (int c = 0; c < 31; ++c) v[c] = 0.0;
+        v[1] = v[4] = v[6] = 1.0; /* h11, h22, h33 */
+        v[18] = 1.0;              /* lapse */
+        v[7] = p->constant_K;     /* K */
+        double b1[3] = {loc[0], loc[1], loc[2]}, b2[3] = {loc[0], loc[1], loc[2]};
+        const double psi_bh = p->bh1_bare_mass / bh_radius(b1, p->bh1_offset) +
+                              p->bh2_bare_mass / bh_radius(b2, p->bh2_offset);
+        const double chi = pow(psi[n] + psi_bh, -4.0);
+        const double factor = pow(chi, 1.5);
+        v[0] = chi;
+        v[25] = phi0; /* phi */
+        v[8] = A11 * factor;
+        v[9] = A12 * factor;
+        v[10] = A13 * factor;
+        v[11] = A22 * factor;
+        v[12] = A23 * factor;
+        v[13] = A33 * factor;
+        for (int c = 0; c < 31; ++c) out[c * V + n] = v[c];
+      }
+}
+
 void orc_set_threads(int n) {
 #ifdef _OPENMP
   if (n > 0) omp_set_num_threads(n);

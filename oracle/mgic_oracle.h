@@ -184,6 +184,15 @@ void orc_nl_integrand(const orc_bh_params *p, const int *lo, const int *hi, doub
 void orc_getlaplacianpsif(double *out, const double *in, const int *lo, const int *hi, double dx,
                           int laplacian);
 
+/* WriteOutput.H's components over the cell box [lo, hi] (component-major,
+ * i fastest).  kind 0: set_output_data (SetLevelData.cpp:343-396), the 31
+ * GRChombo variables from psi (constant_K from p); kind 1: output_solver_data's
+ * tempData (WriteOutput.H:84-100): dpsi, rhs, psi, A11_0, A12_0, A13_0, A22_0,
+ * A23_0, A33_0, phi_0 (set_initial_conditions, SetLevelData.cpp:31-72).
+ * psi / dpsi / rhs over the box (i fastest); dpsi, rhs unused for kind 0. */
+void orc_output_vars(int kind, const orc_bh_params *p, const int *lo, const int *hi, double dx,
+                     const double *psi, const double *dpsi, const double *rhs, double *out);
+
 void orc_set_threads(int n);
 int orc_get_threads(void);
 
