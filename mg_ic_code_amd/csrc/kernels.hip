@@ -389,36 +389,151 @@ __device__ __forceinline__ double red_init() {
 }
 
 template <int KIND>
+__device__ __forceinline__ double red_term(const double *__restrict__ x,
+                                           const double *__restrict__ y, long idx) {
+  const double v = x[idx];
+  if constexpr (KIND == 0) return v * y[idx];
+  else if constexpr (KIND == 2) return v * v;
+  else if constexpr (KIND == 4) return v;
+  else if constexpr (KIND == 5) return -v;
+  else return fabs(v);
+}
+
+// one wave per (j, k) row, lanes along i (coalesced 512-B rows, four
+// independent accumulators per lane), block partials through LDS.  Rows are
+// dealt round-robin to the waves of the grid; no per-element index division.
+template <int KIND>
 __global__ __launch_bounds__(RB) void k_reduce_partial(const double *__restrict__ x,
                                                        const double *__restrict__ y,
                                                        const BoxArgs g,
                                                        double *__restrict__ partials) {
   __shared__ double sm[RB];
-  const long ncell = (long)g.nx * g.ny * g.nz;
-  const long plane = (long)g.nx * g.ny;
-  double acc = red_init<KIND>();
-  for (long t = (long)blockIdx.x * RB + threadIdx.x; t < ncell; t += (long)gridDim.x * RB) {
-    const int k = (int)(t / plane);
-    const int rem = (int)(t - (long)k * plane);
-    const int j = rem / g.nx;
-    const int i = rem - j * g.nx;
-    const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
-    const double v = x[idx];
-    double term;
-    if constexpr (KIND == 0) term = v * y[idx];
-    else if constexpr (KIND == 2) term = v * v;
-    else if constexpr (KIND == 4) term = v;
-    else if constexpr (KIND == 5) term = -v;
-    else term = fabs(v);
-    acc = red_op<KIND>(acc, term);
+  constexpr int W = RB / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrows = g.ny * g.nz;
+  double a0 = red_init<KIND>(), a1 = a0, a2 = a0, a3 = a0;
+  for (int r = blockIdx.x * W + wave; r < nrows; r += gridDim.x * W) {
+    const int k = r / g.ny, j = r - k * g.ny;
+    const long base = (long)j * g.sy + (long)k * g.sz;
+    int i = lane;
+    for (; i + 192 < g.nx; i += 256) {
+      a0 = red_op<KIND>(a0, red_term<KIND>(x, y, base + i));
+      a1 = red_op<KIND>(a1, red_term<KIND>(x, y, base + i + 64));
+      a2 = red_op<KIND>(a2, red_term<KIND>(x, y, base + i + 128));
+      a3 = red_op<KIND>(a3, red_term<KIND>(x, y, base + i + 192));
+    }
+    for (; i < g.nx; i += 64) a0 = red_op<KIND>(a0, red_term<KIND>(x, y, base + i));
   }
-  sm[threadIdx.x] = acc;
+  sm[threadIdx.x] = red_op<KIND>(red_op<KIND>(a0, a1), red_op<KIND>(a2, a3));
   __syncthreads();
   for (int w = RB / 2; w > 0; w >>= 1) {
     if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
     __syncthreads();
   }
   if (threadIdx.x == 0) partials[blockIdx.x] = sm[0];
+}
+
+// ---- BiCGStab's vector updates fused with the reductions that follow them
+// (BiCGStabSolver, restated in op.cpp).  Each element is computed with the
+// same expressions as the separate assign / scale / incr passes (bit-identical
+// results), and the partial sums use k_reduce_partial's row-to-wave deal and
+// accumulators, so a fused norm equals the separate one bit for bit.
+// s = r + ca*v; e = e + cb*pt; partials of the norm kind KIND of s
+template <int KIND>
+__global__ __launch_bounds__(RB) void k_axpy2_reduce(double *__restrict__ s,
+                                                     const double *__restrict__ r,
+                                                     const double *__restrict__ v, double ca,
+                                                     double *__restrict__ e,
+                                                     const double *__restrict__ pt, double cb,
+                                                     const BoxArgs g,
+                                                     double *__restrict__ partials) {
+  __shared__ double sm[RB];
+  constexpr int W = RB / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrows = g.ny * g.nz;
+  double acc[4] = {red_init<KIND>(), red_init<KIND>(), red_init<KIND>(), red_init<KIND>()};
+  auto one = [&](long idx, int q) {
+    const double sv = r[idx] + ca * v[idx];  // S = R; S += ca V
+    s[idx] = sv;
+    e[idx] = e[idx] + cb * pt[idx];          // E += cb PT
+    acc[q] = red_op<KIND>(acc[q], red_term<KIND>(s, nullptr, idx));
+  };
+  for (int row = blockIdx.x * W + wave; row < nrows; row += gridDim.x * W) {
+    const int k = row / g.ny, j = row - k * g.ny;
+    const long base = (long)j * g.sy + (long)k * g.sz;
+    int i = lane;
+    for (; i + 192 < g.nx; i += 256) {
+      one(base + i, 0);
+      one(base + i + 64, 1);
+      one(base + i + 128, 2);
+      one(base + i + 192, 3);
+    }
+    for (; i < g.nx; i += 64) one(base + i, 0);
+  }
+  sm[threadIdx.x] = red_op<KIND>(red_op<KIND>(acc[0], acc[1]), red_op<KIND>(acc[2], acc[3]));
+  __syncthreads();
+  for (int w = RB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = sm[0];
+}
+
+// the partials of dot(t, s) and dot(t, t) in one pass
+__global__ __launch_bounds__(RB) void k_dot2(const double *__restrict__ t,
+                                             const double *__restrict__ s, const BoxArgs g,
+                                             double *__restrict__ pts, double *__restrict__ ptt) {
+  __shared__ double sm[2][RB];
+  constexpr int W = RB / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrows = g.ny * g.nz;
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
+  auto one = [&](long idx, int q) {
+    const double tv = t[idx];
+    a[q] = a[q] + tv * s[idx];
+    b[q] = b[q] + tv * tv;
+  };
+  for (int row = blockIdx.x * W + wave; row < nrows; row += gridDim.x * W) {
+    const int k = row / g.ny, j = row - k * g.ny;
+    const long base = (long)j * g.sy + (long)k * g.sz;
+    int i = lane;
+    for (; i + 192 < g.nx; i += 256) {
+      one(base + i, 0);
+      one(base + i + 64, 1);
+      one(base + i + 128, 2);
+      one(base + i + 192, 3);
+    }
+    for (; i < g.nx; i += 64) one(base + i, 0);
+  }
+  sm[0][threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
+  sm[1][threadIdx.x] = (b[0] + b[1]) + (b[2] + b[3]);
+  __syncthreads();
+  for (int w = RB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      sm[0][threadIdx.x] = sm[0][threadIdx.x] + sm[0][threadIdx.x + w];
+      sm[1][threadIdx.x] = sm[1][threadIdx.x] + sm[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    pts[blockIdx.x] = sm[0][0];
+    ptt[blockIdx.x] = sm[1][0];
+  }
+}
+
+// p = ((p * beta) + c * v) + 1.0 * r  (scale(P, beta); incr(P, V, c); incr(P, R, 1))
+__global__ __launch_bounds__(256) void k_bicg_p(double *__restrict__ p,
+                                                const double *__restrict__ v,
+                                                const double *__restrict__ r, double beta,
+                                                double c, const BoxArgs g) {
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  double t = p[idx] * beta;
+  t = t + c * v[idx];
+  p[idx] = t + 1.0 * r[idx];
 }
 
 template <int KIND>
@@ -915,6 +1030,11 @@ void fill_bc(double *u, const BoxArgs &g, hipStream_t st) {
   }
 }
 
+static long reduce_blocks(const BoxArgs &g) {
+  long nb = ((long)g.ny * g.nz + RB / 64 - 1) / (RB / 64);  // one wave per row at most
+  return nb > kMaxPartsPerBox ? kMaxPartsPerBox : nb;
+}
+
 void blas(int kind, double *x, const double *y, const double *z, double s, double t,
           const BoxArgs &g, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
@@ -935,8 +1055,7 @@ int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
                    double *partials, hipStream_t st) {
   const long ncell = (long)g.nx * g.ny * g.nz;
   if (ncell <= 0) return 0;
-  long nb = (ncell + RB - 1) / RB;
-  if (nb > kMaxPartsPerBox) nb = kMaxPartsPerBox;
+  const long nb = reduce_blocks(g);
   const dim3 grid((unsigned)nb), block(RB);
   switch (kind) {
     case 0: k_reduce_partial<0><<<grid, block, 0, st>>>(x, y, g, partials); break;
@@ -961,6 +1080,38 @@ void reduce_final(int kind, const double *partials, int n, double *out, hipStrea
     case 5: k_reduce_final<5><<<1, RB, 0, st>>>(partials, n, out); break;
     default: throw Error(kBadArg, "reduce: bad kind");
   }
+  check_launch();
+}
+
+int axpy2_reduce(int kind, double *s, const double *r, const double *v, double ca, double *e,
+                 const double *pt, double cb, const BoxArgs &g, double *partials,
+                 hipStream_t st) {
+  if ((long)g.nx * g.ny * g.nz <= 0) return 0;
+  const long nb = reduce_blocks(g);
+  const dim3 grid((unsigned)nb), block(RB);
+  switch (kind) {
+    case 1: k_axpy2_reduce<1><<<grid, block, 0, st>>>(s, r, v, ca, e, pt, cb, g, partials); break;
+    case 2: k_axpy2_reduce<2><<<grid, block, 0, st>>>(s, r, v, ca, e, pt, cb, g, partials); break;
+    case 3: k_axpy2_reduce<3><<<grid, block, 0, st>>>(s, r, v, ca, e, pt, cb, g, partials); break;
+    default: throw Error(kBadArg, "axpy2_reduce: bad kind");
+  }
+  check_launch();
+  return (int)nb;
+}
+
+int dot2_partial(const double *t, const double *s, const BoxArgs &g, double *pts, double *ptt,
+                 hipStream_t st) {
+  if ((long)g.nx * g.ny * g.nz <= 0) return 0;
+  const long nb = reduce_blocks(g);
+  k_dot2<<<dim3((unsigned)nb), dim3(RB), 0, st>>>(t, s, g, pts, ptt);
+  check_launch();
+  return (int)nb;
+}
+
+void bicg_p(double *p, const double *v, const double *r, double beta, double c, const BoxArgs &g,
+            hipStream_t st) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
+  k_bicg_p<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(p, v, r, beta, c, g);
   check_launch();
 }
 

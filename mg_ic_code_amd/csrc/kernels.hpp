@@ -89,9 +89,19 @@ void blas(int kind, double *x, const double *y, const double *z, double s, doubl
 // Writes nparts partials at partials[0..nparts); returns nparts.
 int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
                    double *partials, hipStream_t st);
-constexpr int kMaxPartsPerBox = 256;
+constexpr int kMaxPartsPerBox = 2048;
 void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st);
 
+// BiCGStab's fused vector updates (bit-identical to the separate passes):
+// s = r + ca*v, e = e + cb*pt and the partials of reduction `kind` (1 sum|s|,
+// 2 sum s^2, 3 max|s|) of s; the partials of dot(t,s) and dot(t,t); and
+// p = ((p*beta) + c*v) + r.  Return the number of partials written.
+int axpy2_reduce(int kind, double *s, const double *r, const double *v, double ca, double *e,
+                 const double *pt, double cb, const BoxArgs &g, double *partials, hipStream_t st);
+int dot2_partial(const double *t, const double *s, const BoxArgs &g, double *pts, double *ptt,
+                 hipStream_t st);
+void bicg_p(double *p, const double *v, const double *r, double beta, double c, const BoxArgs &g,
+            hipStream_t st);
 // batched rectangular copies (exchange / copyTo / pack / unpack)
 void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *const *src_tab,
                 const double *src_buf, double *const *dst_tab, double *dst_buf,

@@ -508,6 +508,21 @@ void VariableCoeffPoissonOperator::setVal(LevelData &lhs, double v) {
     kern::blas(5, lhs.p[n], nullptr, nullptr, v, 0.0, args_plain_[n], stream());
 }
 
+double VariableCoeffPoissonOperator::finish_reduce(int kind, double *parts, int total, int slot) {
+  Comm &c = *grid->comm;
+  const hipStream_t st = stream();
+  double *res = c.d_result() + slot;
+  if (total == 0) {  // no local cells: the identity of the reduction
+    c.h_result()[1] = kind >= 4 ? -HUGE_VAL : 0.0;  // pinned: safe for an async copy
+    MGIC_HIP(hipMemcpyAsync(res, c.h_result() + 1, sizeof(double), hipMemcpyHostToDevice, st));
+    MGIC_HIP(hipStreamSynchronize(st));
+  } else {
+    kern::reduce_final(kind, parts, total, res, st);
+  }
+  c.allreduce(res, kind >= 3 ? 1 : 0);
+  return 0.0;
+}
+
 double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const LevelData *y) {
   Comm &c = *grid->comm;
   const hipStream_t st = stream();
@@ -515,16 +530,56 @@ double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const 
   int total = 0;
   for (int n = 0; n < grid->nlocal(); ++n)
     total += kern::reduce_partial(kind, x.p[n], y ? y->p[n] : nullptr, args_plain_[n], parts + total, st);
-  if (total == 0) {  // no local cells: the identity of the reduction
-    c.h_result()[1] = kind >= 4 ? -HUGE_VAL : 0.0;  // pinned: safe for an async copy
-    MGIC_HIP(hipMemcpyAsync(c.d_result(), c.h_result() + 1, sizeof(double), hipMemcpyHostToDevice,
-                            st));
-  }
-  else kern::reduce_final(kind, parts, total, c.d_result(), st);
-  c.allreduce(c.d_result(), kind >= 3 ? 1 : 0);
+  finish_reduce(kind, parts, total, 0);
   MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
   MGIC_HIP(hipStreamSynchronize(st));
   return c.h_result()[0];
+}
+
+static int norm_kind(int ord) { return ord == 0 ? 3 : ord == 1 ? 1 : 2; }
+
+double VariableCoeffPoissonOperator::axpy2Norm(LevelData &s, const LevelData &r, const LevelData &v,
+                                               double ca, LevelData &e, const LevelData &pt,
+                                               double cb, int ord) {
+  Comm &c = *grid->comm;
+  const hipStream_t st = stream();
+  const int kind = norm_kind(ord);
+  double *parts = c.d_partials(std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox);
+  int total = 0;
+  for (int n = 0; n < grid->nlocal(); ++n)
+    total += kern::axpy2_reduce(kind, s.p[n], r.p[n], v.p[n], ca, e.p[n], pt.p[n], cb,
+                                args_plain_[n], parts + total, st);
+  finish_reduce(kind, parts, total, 0);
+  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
+  MGIC_HIP(hipStreamSynchronize(st));
+  const double x = c.h_result()[0];
+  return kind == 2 ? std::sqrt(x) : x;
+}
+
+void VariableCoeffPoissonOperator::bicgP(LevelData &p, const LevelData &v, const LevelData &r,
+                                         double beta, double cc) {
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::bicg_p(p.p[n], v.p[n], r.p[n], beta, cc, args_plain_[n], stream());
+}
+
+void VariableCoeffPoissonOperator::dot2(const LevelData &t, const LevelData &s, double &ts,
+                                        double &tt) {
+  Comm &c = *grid->comm;
+  const hipStream_t st = stream();
+  const int cap = std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox;
+  double *parts = c.d_partials(2 * cap);
+  int total = 0;
+  for (int n = 0; n < grid->nlocal(); ++n) {
+    const int k = kern::dot2_partial(t.p[n], s.p[n], args_plain_[n], parts + total,
+                                     parts + cap + total, st);
+    total += k;
+  }
+  finish_reduce(0, parts, total, 0);
+  finish_reduce(0, parts + cap, total, 1);
+  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+  MGIC_HIP(hipStreamSynchronize(st));
+  ts = c.h_result()[0];
+  tt = c.h_result()[1];
 }
 
 double VariableCoeffPoissonOperator::dotProduct(const LevelData &x, const LevelData &y) {
@@ -624,34 +679,24 @@ int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, cons
       init = false;
     } else {
       beta = (rho1 / rho2) * (alpha / omega);
-      op.scale(P, beta);
-      op.incr(P, V, -beta * omega);
-      op.incr(P, R, 1.0);
+      op.bicgP(P, V, R, beta, -beta * omega);  // scale(P, beta); incr(P, V, -beta omega); incr(P, R, 1)
     }
     if (precond) precond(PT, P);
     else op.preCond(PT, P);
-    op.setToZero(V);
-    op.applyOp(V, PT, true);
+    op.applyOp(V, PT, true);  // writes every valid cell of V
     const double m = op.dotProduct(RT, V);
     if (std::fabs(m) > prm.small * std::fabs(rho1)) {
       alpha = rho1 / m;
-      op.assignLocal(S, R);
-      op.incr(S, V, -alpha);
-      op.incr(E, PT, alpha);
-      nrm = op.norm(S, nt);
+      nrm = op.axpy2Norm(S, R, V, -alpha, E, PT, alpha, nt);  // S = R - alpha V; E += alpha PT
       if (nrm <= prm.eps * init_norm || nrm <= prm.reps) break;
       if (precond) precond(ST, S);
       else op.preCond(ST, S);
-      op.setToZero(T);
       op.applyOp(T, ST, true);
-      const double ts = op.dotProduct(T, S);
-      const double tt = op.dotProduct(T, T);
+      double ts = 0.0, tt = 0.0;
+      op.dot2(T, S, ts, tt);
       if (tt == 0.0) break;
       omega = ts / tt;
-      op.assignLocal(R, S);
-      op.incr(R, T, -omega);
-      op.incr(E, ST, omega);
-      nrm = op.norm(R, nt);
+      nrm = op.axpy2Norm(R, S, T, -omega, E, ST, omega, nt);  // R = S - omega T; E += omega ST
       if (omega == 0.0) break;
     } else {
       if (restarts >= prm.numRestarts) break;
@@ -869,8 +914,14 @@ void AMRMultiGrid::precondition(LevelData &e, const LevelData &r, int iters) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
   if (!pre_resid_) pre_resid_ = op0.create();
   op0.setToZero(e);
-  initResidual(e, r, *pre_resid_, -1, true);
-  for (int i = 0; i < iters; ++i) iteration(e, r, *pre_resid_, -1, true);
+  // e = 0, so the first residual r - L(0) (homogeneous BC) is r itself: the
+  // first cycle runs on r (its ghosts are the only cells it writes); the
+  // residual after the last cycle is not needed
+  LevelData &r0 = const_cast<LevelData &>(r);
+  for (int i = 0; i < iters; ++i) {
+    if (i > 0) op0.residual(*pre_resid_, e, r, true);
+    mg.oneCycleFromZeroInto(*corr_, i == 0 ? r0 : *pre_resid_, e);
+  }
 }
 
 int AMRMultiGrid::solve(LevelData &phi, const LevelData &rhs, const SolveParams &p,

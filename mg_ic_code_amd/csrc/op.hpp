@@ -97,6 +97,14 @@ class VariableCoeffPoissonOperator {
   void setVal(LevelData &lhs, double v);
   double dotProduct(const LevelData &x, const LevelData &y);
   double norm(const LevelData &x, int ord);
+  // BiCGStab's fused updates (bit-identical to the separate passes):
+  // s = r + ca v; e += cb pt; returns norm(s, ord)
+  double axpy2Norm(LevelData &s, const LevelData &r, const LevelData &v, double ca, LevelData &e,
+                   const LevelData &pt, double cb, int ord);
+  // p = p beta + c v + r (scale(P, beta); incr(P, V, c); incr(P, R, 1))
+  void bicgP(LevelData &p, const LevelData &v, const LevelData &r, double beta, double c);
+  // dot(t, s) and dot(t, t) in one pass
+  void dot2(const LevelData &t, const LevelData &s, double &ts, double &tt);
 
   // state (public as in the reference: m_aCoef, m_bCoef, m_lambda)
   std::shared_ptr<Grid> grid;
@@ -119,6 +127,8 @@ class VariableCoeffPoissonOperator {
   const BoxArgs &args(int n, bool homogeneous);
   void build_args();
   double reduce(int kind, const LevelData &x, const LevelData *y);
+  // partials (count `total`, per-box blocks) -> final -> allreduce -> host
+  double finish_reduce(int kind, double *parts, int total, int slot);
   std::vector<BoxArgs> args_hom_, args_inhom_, args_plain_;
   std::unique_ptr<LevelData> jac_tmp_;
   std::unique_ptr<LevelData> sweep_tmp_;  // out-of-place buffer of the fused sweep
