@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--overlap", type=int, default=0,
                     help="halo exchange overlapped with the sweep: 0 off, 1 auto (boxes >= 96^3), "
                          "2 always")
+    ap.add_argument("--deep-halo", type=int, default=-1,
+                    help="4-deep ghost shells, two sweeps per exchange: 0 off, 1 every level, "
+                         "2 levels of boxes <= 128^3; default 1 for N > 1 (RCCL exchanges: "
+                         "fewer, larger messages), 0 on one GPU (local copies are cheap)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -102,7 +106,9 @@ def main():
                                   bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
                                   coefficient_average_type=1, prolong_type=1, relax_mode=1,
                                   fused_smoother=0 if args.no_fused else 1,
-                                  overlap_exchange=args.overlap)
+                                  overlap_exchange=args.overlap,
+                                  deep_halo=(1 if world > 1 else 0) if args.deep_halo < 0
+                                  else args.deep_halo)
     fac = mg.defineOperatorFactory(grid, fa, fb, op_params)
     sp = mg.SolverParams(max_depth=args.levels - 1, n_pre=args.nsmooth, n_post=args.nsmooth,
                          n_bottom=args.nsmooth, bottom_solver=0)
@@ -186,6 +192,9 @@ def main():
                             "harmonic coef averaging, linear prolongation, Dirichlet-0",
                 "n": n, "levels": args.levels, "numMGsmooth": args.nsmooth,
                 "decomposition": f"{len(boxes)} box(es), {world} rank(s)",
+                "halo": ("none (one box)" if len(boxes) == 1 else
+                         "4-deep ghost shell per 2 fused sweeps (deep halo)" if op_params.deep_halo
+                         else "2-deep ghost shell per fused sweep"),
                 "parallelism": f"domain-decomposition x{world} (RCCL halo exchange)" if world > 1
                 else "single GPU",
             },

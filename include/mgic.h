@@ -64,7 +64,13 @@ typedef struct {
   int overlap_exchange;         /* fused sweeps on exchanged layouts: boundary slabs +
                                    ghost-shell exchange on a second stream, overlapping
                                    the sweep.  0 off (default), 1 if every box >= 96^3,
-                                   2 always */
+                                   2 always; boundary-first split (slabs swept first,
+                                   their exchange overlaps the interior sweep): 3 if
+                                   every box >= 64^3, 4 always */
+  int deep_halo;                /* fused sweeps on exchanged layouts: 4-deep ghost shells,
+                                   two sweeps per exchange (the first on the box grown by
+                                   2 across exchanged faces).  0 off (default), 1 every
+                                   level, 2 levels of boxes <= 128^3 cells */
 } mgic_op_params;
 
 /* MultiGrid / bottom-solver configuration (MultilevelLinearOp knobs:

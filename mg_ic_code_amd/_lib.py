@@ -37,6 +37,7 @@ class OpParams(ctypes.Structure):
         ("relax_mode", c_int),
         ("fused_smoother", c_int),
         ("overlap_exchange", c_int),
+        ("deep_halo", c_int),
     ]
 
 

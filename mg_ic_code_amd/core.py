@@ -259,6 +259,9 @@ class OperatorParams:
     relax_mode: int = 1                 # 1 GSRB, 4 Jacobi
     fused_smoother: int = 1             # 0 per-colour passes, 1 by size, 2 z-streaming, 3 3D blocks
     overlap_exchange: int = 0           # halo exchange overlapped with the sweep: 0, 1 auto, 2 always
+    #                                     (redundant slabs); 3 auto, 4 always (boundary-first split)
+    deep_halo: int = 0                  # 4-deep ghost shells, two sweeps per exchange: 0 off,
+    #                                     1 every level, 2 levels of boxes <= 128^3
 
     def to_c(self) -> OpParams:
         p = OpParams()
@@ -271,6 +274,7 @@ class OperatorParams:
         p.relax_mode = self.relax_mode
         p.fused_smoother = self.fused_smoother
         p.overlap_exchange = self.overlap_exchange
+        p.deep_halo = self.deep_halo
         return p
 
 

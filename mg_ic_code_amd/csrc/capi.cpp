@@ -77,6 +77,7 @@ OpParams to_op(const mgic_op_params *p) {
   o.relax_mode = p->relax_mode;
   o.fused_smoother = p->fused_smoother;
   o.overlap_exchange = p->overlap_exchange;
+  o.deep_halo = p->deep_halo;
   return o;
 }
 
@@ -200,6 +201,7 @@ MGIC_API void mgic_op_params_default(mgic_op_params *p) {
   p->relax_mode = o.relax_mode;
   p->fused_smoother = o.fused_smoother;
   p->overlap_exchange = o.overlap_exchange;
+  p->deep_halo = o.deep_halo;
 }
 
 MGIC_API void mgic_mg_params_default(mgic_mg_params *p) {

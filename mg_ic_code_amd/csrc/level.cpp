@@ -113,9 +113,11 @@ CopyPlan &Grid::exchange_plan() {
   return *exchange_;
 }
 
-CopyPlan &Grid::shell_plan() {
-  if (!shell_) shell_ = build_copy_plan(*this, *this, false, false, true, 2);
-  return *shell_;
+CopyPlan &Grid::shell_plan(int depth) {
+  MGIC_CHECK(depth >= 1 && depth <= kGhost, "shell depth exceeds the allocated ghosts");
+  auto &p = shell_[depth];
+  if (!p) p = build_copy_plan(*this, *this, false, false, true, depth);
+  return *p;
 }
 
 bool Grid::has_memory_faces() const {
@@ -407,8 +409,8 @@ void LevelData::exchange(hipStream_t st) {
   pl.execute(*grid->comm, d_tab, d_tab, st);
 }
 
-void LevelData::exchange_shell(hipStream_t st) {
-  CopyPlan &pl = grid->shell_plan();
+void LevelData::exchange_shell(hipStream_t st, int depth) {
+  CopyPlan &pl = grid->shell_plan(depth);
   if (pl.empty()) return;
   pl.execute(*grid->comm, d_tab, d_tab, st);
 }
@@ -440,8 +442,8 @@ void LevelDataF::exchange(hipStream_t st) {
   pl.execute_f(*grid->comm, d_tab, d_tab, st);
 }
 
-void LevelDataF::exchange_shell(hipStream_t st) {
-  CopyPlan &pl = grid->shell_plan();
+void LevelDataF::exchange_shell(hipStream_t st, int depth) {
+  CopyPlan &pl = grid->shell_plan(depth);
   if (pl.empty()) return;
   pl.execute_f(*grid->comm, d_tab, d_tab, st);
 }

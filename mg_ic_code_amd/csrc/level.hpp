@@ -117,7 +117,7 @@ class Grid {
   CopyPlan &exchange_plan();
   // full 2-deep ghost shell (faces, edges, corners): what a fused sweep
   // needs to recompute the neighbours' red values on its own ghost layer
-  CopyPlan &shell_plan();
+  CopyPlan &shell_plan(int depth = 2);
   bool has_memory_faces() const;  // some local box face is exchanged
   // BoxArgs of local box n with the face BC modes for (bc flags, value,
   // homogeneous); faces that are not domain faces (or are periodic) get
@@ -127,7 +127,8 @@ class Grid {
   BoxArgs box_args_plain(int n) const;  // all faces kBcMemory
 
  private:
-  std::unique_ptr<CopyPlan> exchange_, shell_;
+  std::unique_ptr<CopyPlan> exchange_;
+  std::map<int, std::unique_ptr<CopyPlan>> shell_;  // per depth
 };
 
 // Build a copy plan from src layout to dst layout.  dst regions: the valid
@@ -153,7 +154,7 @@ class LevelData {
   double *ptr(int n) const { return p[n]; }
   void set_zero_all(hipStream_t st);  // valid + ghosts
   void exchange(hipStream_t st);
-  void exchange_shell(hipStream_t st);  // 2-deep faces + edges + corners
+  void exchange_shell(hipStream_t st, int depth = 2);  // faces + edges + corners
 };
 
 // The same layout with fp32 elements (the mixed-precision V-cycle's
@@ -170,7 +171,7 @@ class LevelDataF {
   std::vector<float *> p;
   float **d_tab = nullptr;
   void exchange(hipStream_t st);
-  void exchange_shell(hipStream_t st);
+  void exchange_shell(hipStream_t st, int depth = 2);
 };
 
 }  // namespace mgic

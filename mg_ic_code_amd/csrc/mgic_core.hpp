@@ -21,8 +21,9 @@
 
 namespace mgic {
 
-constexpr int kGhost = 2;     // ghost depth allocated: 1 for the stencils (CH_assert(ghostVect >=
+constexpr int kGhost = 4;     // ghost depth allocated: 1 for the stencils (CH_assert(ghostVect >=
                               // Unit), .cpp:279) + 1 for the fused sweep's halo (shell exchange)
+                              // + 2 for the deep halo (two sweeps per 4-deep shell exchange)
 constexpr int kRowAlign = 16; // doubles: 128-byte rows
 
 struct Error : std::runtime_error {

@@ -255,7 +255,7 @@ static int sweeps_per_launch() {
 }
 
 bool VariableCoeffPoissonOperator::overlapApplies() const {
-  if (prm.overlap_exchange == 0) return false;
+  if (prm.overlap_exchange != 1 && prm.overlap_exchange != 2) return false;
   if (prm.overlap_exchange == 2) return true;
   static const long min_cells = [] {
     const char *e = getenv("MGIC_OVERLAP_MIN_CELLS");
@@ -268,6 +268,98 @@ bool VariableCoeffPoissonOperator::overlapApplies() const {
   return true;
 }
 
+// Boundary-first split of a sweep (overlap_exchange 3 / 4): the cells
+// within kSplitDepth of every exchanged face are swept first (one small
+// launch), the ghost-shell exchange of that result then runs on the side
+// stream while the main stream sweeps the rest of the box.  Every cell is
+// computed once, from the same old values as the whole-box sweep (the
+// interior sweep reads the slab cells of u_in as its shell), so results are
+// bit-identical.  Decided on the global layout (same RCCL sequence on every
+// rank): every box must leave a non-empty interior.
+static constexpr int kSplitDepth = 2;
+
+bool VariableCoeffPoissonOperator::splitApplies() const {
+  if (prm.overlap_exchange != 3 && prm.overlap_exchange != 4) return false;
+  static const long min_cells = [] {
+    const char *e = getenv("MGIC_SPLIT_MIN_CELLS");
+    return e ? atol(e) : 64L * 64 * 64;
+  }();
+  for (const Box &b : grid->boxes) {
+    if (prm.overlap_exchange == 3 && b.ncells() < min_cells) return false;
+    for (int d = 0; d < 3; ++d)
+      if (b.size(d) < 4 * kSplitDepth + 2) return false;
+  }
+  return true;
+}
+
+// the box minus kSplitDepth cells along every exchanged face: BoxArgs of
+// the interior and its element offset from the valid-lo corner
+static BoxArgs split_interior(const BoxArgs &g, long *off) {
+  BoxArgs a = g;
+  long o = 0;
+  const long st[3] = {1, g.sy, g.sz};
+  int *n[3] = {&a.nx, &a.ny, &a.nz};
+  for (int d = 0; d < 3; ++d) {
+    if (!g.bcm[2 * d]) {
+      *n[d] -= kSplitDepth;
+      a.glo[d] += kSplitDepth;
+      o += kSplitDepth * st[d];
+    }
+    if (!g.bcm[2 * d + 1]) *n[d] -= kSplitDepth;
+  }
+  *off = o;
+  return a;
+}
+
+// Deep halo (deep_halo = 1): a 4-deep ghost shell feeds two sweeps.  The
+// first sweeps the box grown by 2 across every exchanged face -- the
+// neighbours' cells within 2 of the face, recomputed from the shell with the
+// same expressions and inputs, so bit-identical to their own -- which leaves
+// the result's 2-deep shell valid for the second sweep without an exchange.
+// Half the exchanges of the 2-deep scheme for the same bytes (latency bound
+// halos on coarse levels and small per-rank boxes).  rhs / aCoef / bCoef need
+// the 4-deep shell too (the grown sweep's red ring reaches depth 3).
+static constexpr int kDeepDepth = 4, kDeepGrow = 2;
+
+bool VariableCoeffPoissonOperator::deepApplies() const {
+  if (!prm.deep_halo || !grid->has_memory_faces() || !grid->tiles_domain()) return false;
+  static const long max_cells = [] {  // deep_halo 2: only levels of boxes up to this size
+    const char *e = getenv("MGIC_DEEP_MAX_CELLS");
+    return e ? atol(e) : 128L * 128 * 128;
+  }();
+  // every shell cell must be some box's valid cell within one period
+  for (const Box &b : grid->boxes) {
+    if (prm.deep_halo == 2 && b.ncells() > max_cells) return false;
+    for (int d = 0; d < 3; ++d)
+      if (b.size(d) < kDeepDepth) return false;
+  }
+  return true;
+}
+
+void VariableCoeffPoissonOperator::rhsHalo(LevelData &r, hipStream_t st) const {
+  if (deepApplies()) r.exchange_shell(st, kDeepDepth);
+  else r.exchange(st);
+}
+
+// the box grown by `d` cells across every exchanged face (element offset of
+// its lo corner from the valid-lo corner: negative)
+static BoxArgs grow_exchanged(const BoxArgs &g, int d, long *off) {
+  BoxArgs a = g;
+  long o = 0;
+  const long st[3] = {1, g.sy, g.sz};
+  int *n[3] = {&a.nx, &a.ny, &a.nz};
+  for (int k = 0; k < 3; ++k) {
+    if (!g.bcm[2 * k]) {
+      *n[k] += d;
+      a.glo[k] -= d;
+      o -= d * st[k];
+    }
+    if (!g.bcm[2 * k + 1]) *n[k] += d;
+  }
+  *off = o;
+  return a;
+}
+
 bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
                                               bool zero_in, LevelData *acc, int flags,
                                               LevelData *rst) {
@@ -276,11 +368,17 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   const StencilCoefs s = coefs();
   if (!sweep_tmp_) sweep_tmp_ = create();
   const bool halo = grid->has_memory_faces();
+  const bool deep_ok = halo && deepApplies();
   if (halo) {  // ghost layer 1 of rhs / aCoef / bCoef for the red ring on the halo
-    if (!(flags & kRhsHaloReady)) const_cast<LevelData &>(rhs).exchange(st);
+    if (!(flags & kRhsHaloReady)) rhsHalo(const_cast<LevelData &>(rhs), st);
     if (!coef_ghosts_) {
-      m_aCoef->exchange(st);
-      m_bCoef->exchange(st);
+      if (deep_ok) {
+        m_aCoef->exchange_shell(st, kDeepDepth);
+        m_bCoef->exchange_shell(st, kDeepDepth);
+      } else {
+        m_aCoef->exchange(st);
+        m_bCoef->exchange(st);
+      }
       coef_ghosts_ = true;
     }
   }
@@ -288,6 +386,10 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   const int per = acc ? 1 : sweeps_per_launch();
   const bool want_out = halo && (flags & kHaloOut) && !acc;
   const bool overlap = halo && per == 1 && overlapApplies();
+  const bool split = halo && per == 1 && !overlap && splitApplies();
+  const bool deep = deep_ok && per == 1 && !overlap && !split;
+  int vd = zero_in ? (1 << 20) : 0;  // deep: valid ghost-shell depth of src
+  bool out_ready = false;            // deep: the last sweep left its face ghosts valid
   // Overlapped halo: sweep i runs on the main stream over the whole box;
   // meanwhile the side stream recomputes the cells within 2 of every
   // exchanged face (the same values) and exchanges that ghost shell, so the
@@ -297,7 +399,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   // side step i done reading the buffer sweep i+1 overwrites).
   hipStream_t side = nullptr;
   hipEvent_t evM = nullptr, evE = nullptr;
-  if (overlap) {
+  if (overlap || split) {
     side = grid->comm->side_stream();
     evM = grid->comm->event(0);
     evE = grid->comm->event(1);
@@ -317,7 +419,21 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     const bool zin = zero_in && it == 0;
     const int k = (per == 2 && !halo && n - it >= 2) ? 2 : 1;
     const bool last = it + k == n;
-    if (halo && !zin && (!overlap || it == 0)) src->exchange_shell(st);
+    if (deep) {
+      if (vd < 2) {
+        src->exchange_shell(st, kDeepDepth);
+        vd = kDeepDepth;
+      }
+    } else if (halo && !zin && (!(overlap || split) || it == 0)) {
+      src->exchange_shell(st);
+    }
+    // deep: sweep the grown box when the shell allows it and the result's
+    // ghosts are wanted (a later sweep, or the caller's face ghosts)
+    const int grow = deep && vd >= kDeepDepth && !(last && acc) && (!last || want_out) ? kDeepGrow : 0;
+    if (deep) {
+      vd = grow;
+      if (last) out_ready = grow > 0;
+    }
     if (side_pending) {
       MGIC_HIP(hipStreamWaitEvent(st, evE, 0));
       side_pending = false;
@@ -325,6 +441,31 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     // everything the main stream did so far (src's valid cells, the exposed
     // first exchange, rhs/coefficient ghosts) is what the side step reads
     if (overlap) MGIC_HIP(hipEventRecord(evM, st));
+    if (split && (!last || want_out)) {
+      // slabs of every local box (the local copies read neighbours' slabs),
+      // then their exchange on the side stream, then the interiors
+      for (int b = 0; b < grid->nlocal(); ++b)
+        kern::gsrb_sweep_slabs(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
+                               args_hom_[b], s, zin, kSplitDepth, st);
+      MGIC_HIP(hipEventRecord(evM, st));
+      MGIC_HIP(hipStreamWaitEvent(side, evM, 0));
+      if (last) dst->exchange(side);  // the face ghosts the caller wants
+      else dst->exchange_shell(side);
+      MGIC_HIP(hipEventRecord(evE, side));
+      side_pending = true;
+      for (int b = 0; b < grid->nlocal(); ++b) {
+        long o = 0;
+        const BoxArgs ia = split_interior(args_hom_[b], &o);
+        const long nc = (long)ia.nx * ia.ny * ia.nz;
+        prof_mark(st, nc, true, 2);
+        kern::gsrb_sweep_fused(dst->p[b] + o, src->p[b] + o, rhs.p[b] + o, m_aCoef->p[b] + o,
+                               m_bCoef->p[b] + o, ia, s, zin, nullptr, prm.fused_smoother, st);
+        prof_mark(st, nc, false, 2);
+      }
+      std::swap(src, dst);
+      it += k;
+      continue;
+    }
     for (int b = 0; b < grid->nlocal(); ++b) {
       // the roofline instrumentation times the sweep kernels only (the
       // sweep+restriction launch moves other bytes)
@@ -337,7 +478,12 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
         kern::gsrb_sweep_fused_restrict(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b],
                                         m_bCoef->p[b], args_hom_[b], s, rst->p[b],
                                         rst->grid->box_args_plain(b), st);
-      else
+      else if (grow) {
+        long o = 0;
+        const BoxArgs ga = grow_exchanged(args_hom_[b], grow, &o);
+        kern::gsrb_sweep_fused(dst->p[b] + o, src->p[b] + o, rhs.p[b] + o, m_aCoef->p[b] + o,
+                               m_bCoef->p[b] + o, ga, s, zin, nullptr, prm.fused_smoother, st);
+      } else
         kern::gsrb_sweep_fused(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
                                args_hom_[b], s, zin, last && acc ? acc->p[b] : nullptr,
                                prm.fused_smoother, st);
@@ -361,7 +507,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     for (int b = 0; b < grid->nlocal(); ++b)
       kern::blas(0, dpsi.p[b], src->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
     if (want_out) dpsi.exchange(st);
-  } else if (want_out && !overlap) {
+  } else if (want_out && !overlap && !split && !out_ready) {
     dpsi.exchange(st);
   }
   return restrict_last;
@@ -813,7 +959,7 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
   // it; r does not change between pre- and post-smoothing)
   int rf = 0;
   if (op.grid->has_memory_faces() && op.fusedSmootherApplies() && op.prm.relax_mode == 1) {
-    r.exchange(st);
+    op.rhsHalo(r, st);
     rf = kRhsHaloReady;
   }
   const int out = halo_out ? kHaloOut : 0;

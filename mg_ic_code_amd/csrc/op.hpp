@@ -37,7 +37,15 @@ struct OpParams {
                                      // stream while the main stream sweeps the box.
                                      // 0 off (default: measured slower on one GPU, the
                                      // slab sweeps cost more than the exchange they hide),
-                                     // 1 when every box has >= 96^3 cells, 2 always
+                                     // 1 when every box has >= 96^3 cells, 2 always;
+                                     // boundary-first split (no redundant slabs: the
+                                     // main stream sweeps the slabs, then the interior
+                                     // while the side stream exchanges the slabs):
+                                     // 3 when every box has >= 64^3 cells, 4 always
+  int deep_halo = 0;                 // fused sweeps on exchanged layouts: 4-deep ghost
+                                     // shells, two sweeps per exchange (the first on the
+                                     // box grown by 2 across exchanged faces); 0 off,
+                                     // 1 every level, 2 levels of boxes <= 128^3
 };
 
 // relax flags (MultiGrid::cycle): the caller exchanged rhs's ghost layer
@@ -147,6 +155,11 @@ class VariableCoeffPoissonOperator {
   bool fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false,
                   LevelData *acc = nullptr, int flags = 0, LevelData *rst = nullptr);
   bool overlapApplies() const;
+  bool splitApplies() const;
+  bool deepApplies() const;
+  // r's ghosts for the fused sweeps' rings (once per MultiGrid level visit):
+  // face layer 1, or the 4-deep shell in deep-halo mode
+  void rhsHalo(LevelData &r, hipStream_t st) const;
   // relax(e, r, n); phi += e -- the increment folded into the last fused
   // sweep (e is left as scratch in that case)
   void relaxAccumulate(LevelData &e, const LevelData &r, int n, LevelData &phi, int flags = 0);

@@ -124,7 +124,7 @@ def test_chf_dropin_op_res_restrict_bitwise(rng):
 # ----------------------------------------------------------------- operator level
 def build_pair(comm, rng, n, parts, *, alpha=1.0, beta=-1.0, avg=1, prolong=1, bc_lo=(0, 0, 0),
                bc_hi=(0, 0, 0), bc_value=0.0, periodic=(0, 0, 0), nlevels=3, bottom=0,
-               relax_mode=1, agglomerate_below=0, fused=1, bvar=True, overlap=1):
+               relax_mode=1, agglomerate_below=0, fused=1, bvar=True, overlap=1, deep=0):
     dom = (0, 0, 0, n - 1, n - 1, n - 1)
     dx = 100.0 / n
     boxes = split_domain(dom, parts)
@@ -138,7 +138,8 @@ def build_pair(comm, rng, n, parts, *, alpha=1.0, beta=-1.0, avg=1, prolong=1, b
     fphi.set_zero()
     prm = mg.OperatorParams(alpha=alpha, beta=beta, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bc_value,
                             coefficient_average_type=avg, prolong_type=prolong,
-                            relax_mode=relax_mode, fused_smoother=fused, overlap_exchange=overlap)
+                            relax_mode=relax_mode, fused_smoother=fused, overlap_exchange=overlap,
+                            deep_halo=deep)
     fac = mg.defineOperatorFactory(grid, fa, fb, prm)
     amg = mg.AMRMultiGrid(fac, mg.SolverParams(max_depth=nlevels - 1, bottom_solver=bottom,
                                                 agglomerate_below=agglomerate_below))
@@ -235,7 +236,7 @@ def test_fill_bc_matches_oracle(comm, rng):
 @pytest.mark.parametrize("parts,prolong,avg", [((1, 1, 1), 1, 1), ((1, 1, 1), 0, 0),
                                                ((2, 2, 2), 1, 1), ((2, 1, 2), 0, 1)])
 @pytest.mark.parametrize("fused", [2, 3])  # z-streaming / 3D-block sweep kernel
-@pytest.mark.parametrize("overlap", [0, 2])  # halo exchange on a second stream
+@pytest.mark.parametrize("overlap", [0, 2, 4])  # halo exchange on a second stream
 def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused, overlap):
     n = 32
     S = build_pair(comm, rng, n, parts, prolong=prolong, avg=avg, nlevels=3, bottom=0,
@@ -289,7 +290,7 @@ def test_vcycle_ragged_mixed_bc_bitwise(rng, comm, fused, bvar):
 
 
 @pytest.mark.parametrize("fused", [2, 3])
-@pytest.mark.parametrize("overlap", [0, 2])
+@pytest.mark.parametrize("overlap", [0, 2, 4])
 def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, overlap):
     # the RCCL pack -> send/recv -> unpack path, exercised on one GPU by
     # routing same-rank copies through self send/recv
@@ -328,7 +329,7 @@ def test_bicgstab_bottom_within_tolerance(comm, rng):
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
 
 
-@pytest.mark.parametrize("overlap", [0, 2])
+@pytest.mark.parametrize("overlap", [0, 2, 4])
 def test_agglomerated_hierarchy_matches_single_box(comm, rng, overlap):
     n = 32
     S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16,
@@ -357,7 +358,7 @@ def test_binary_bh_inputs_on_device(comm):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("fused,overlap", [(2, 0), (3, 2), (2, 2)])
+@pytest.mark.parametrize("fused,overlap", [(2, 0), (3, 2), (2, 2), (2, 4), (3, 4)])
 def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused, overlap):
     # 128^3: GPU single box == GPU 8 boxes == oracle, bit for bit
     n = 128
@@ -391,15 +392,71 @@ def test_overlapped_halo_large_periodic_box_bitwise(rng, rccl):
         c = mg.Comm()
     n = 192
     out = []
-    for overlap in (0, 2):
+    for overlap in (0, 2, 4):
         S = build_pair(c, np.random.default_rng(5), n, (1, 1, 1), periodic=(1, 1, 1), alpha=1.0,
                        nlevels=3, bottom=0, bvar=False, overlap=overlap)
         amg = S["amg"]
         amg.init_residual(S["fphi"], S["frhs"], S["fres"])
         norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(3)]
         out.append((norms, S["fphi"].download(0)))
-    assert out[0][0] == out[1][0]
-    assert np.array_equal(out[0][1], out[1][1])
+    for r in out[1:]:
+        assert out[0][0] == r[0]
+        assert np.array_equal(out[0][1], r[1])
+
+
+@pytest.mark.parametrize("nsmooth", [1, 3, 4])
+@pytest.mark.parametrize("periodic", [(0, 0, 0), (1, 0, 1)])
+@pytest.mark.parametrize("parts,n,fused", [((2, 2, 2), 32, 1), ((2, 1, 3), 48, 2), ((3, 2, 1), 48, 3)])
+def test_deep_halo_vcycle_bitwise(rng, nsmooth, periodic, parts, n, fused):
+    # 4-deep shells, two sweeps per exchange (grown-box first sweep): the same
+    # V-cycle iterates as the 2-deep schedule and the oracle, bit for bit, on
+    # local copies and RCCL self messages, down to 4-cell coarse boxes
+    for c in (mg.Comm(), None):
+        if c is None:
+            c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+            c.set_self_messages(True)
+        out = []
+        for deep in (0, 1):
+            S = build_pair(c, np.random.default_rng(9), n, parts, periodic=periodic, alpha=1.0,
+                           nlevels=3, bottom=0, fused=fused, overlap=0, deep=deep)
+            amg = mg.AMRMultiGrid(S["fac"], mg.SolverParams(max_depth=2, n_pre=nsmooth,
+                                                            n_post=nsmooth, n_bottom=nsmooth,
+                                                            bottom_solver=0))
+            amg.init_residual(S["fphi"], S["frhs"], S["fres"])
+            norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
+            out.append((norms, download_global(S["fphi"], S["grid"], (n,) * 3)))
+        assert out[0][0] == out[1][0]
+        assert np.array_equal(out[0][1], out[1][1])
+    if nsmooth == 4:
+        o = S["o"]
+        o.init_residual(0)
+        assert [o.iteration(0) for _ in range(2)] == out[0][0]
+        assert np.array_equal(o.get(0, oracle.PHI, 0), out[0][1])
+
+
+@pytest.mark.parametrize("nsmooth", [1, 3])
+@pytest.mark.parametrize("periodic", [(0, 0, 0), (1, 0, 1)])
+def test_split_halo_sweeps_odd_counts_bitwise(rng, nsmooth, periodic):
+    # boundary-first split (overlap_exchange 4) with odd sweep counts (the
+    # result ends in the scratch buffer) on ragged multi-box layouts, local
+    # copies and RCCL self messages, against the serial schedule and oracle
+    n = 48
+    for c in (mg.Comm(), None):
+        if c is None:
+            c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+            c.set_self_messages(True)
+        out = []
+        for overlap in (0, 4):
+            S = build_pair(c, np.random.default_rng(3), n, (2, 1, 3), periodic=periodic,
+                           alpha=1.0, nlevels=3, bottom=0, overlap=overlap)
+            amg = mg.AMRMultiGrid(S["fac"], mg.SolverParams(max_depth=2, n_pre=nsmooth,
+                                                            n_post=nsmooth, n_bottom=nsmooth,
+                                                            bottom_solver=0))
+            amg.init_residual(S["fphi"], S["frhs"], S["fres"])
+            norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
+            out.append((norms, download_global(S["fphi"], S["grid"], (n,) * 3)))
+        assert out[0][0] == out[1][0]
+        assert np.array_equal(out[0][1], out[1][1])
 
 
 @pytest.mark.parametrize("shape,lo", [((70, 20, 13), (0, 0, 0)), ((37, 9, 40), (3, -5, 7)),

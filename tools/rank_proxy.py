@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--local", action="store_true", help="local copies instead of RCCL")
+    ap.add_argument("--deep", type=int, default=0, help="deep halo (two sweeps per exchange)")
+    ap.add_argument("--periodic", default="1,1,1", help="periodic directions (exchanged faces)")
     args = ap.parse_args()
     import mg_ic_code_amd as mg
     from mg_ic_code_amd.params import read_params_file
@@ -39,7 +41,8 @@ def main():
         comm = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
         comm.set_self_messages(True)
     dom = (0, 0, 0, n - 1, n - 1, n - 1)
-    grid = mg.Grid(comm, dom, [dom], prm.L / n, periodic=(1, 1, 1))
+    per = tuple(int(v) for v in args.periodic.split(","))
+    grid = mg.Grid(comm, dom, [dom], prm.L / n, periodic=per)
     fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
     bh = prm.bh()
     mg.set_binary_bh_coefs(fa, frhs, bh)
@@ -47,7 +50,7 @@ def main():
     fphi.set_zero()
     op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, coefficient_average_type=1,
                            prolong_type=1, relax_mode=1, fused_smoother=1,
-                           overlap_exchange=args.overlap)
+                           overlap_exchange=args.overlap, deep_halo=args.deep)
     fac = mg.defineOperatorFactory(grid, fa, fb, op)
     amg = mg.AMRMultiGrid(fac, mg.SolverParams(max_depth=args.levels - 1, n_pre=4, n_post=4,
                                                n_bottom=4, bottom_solver=0))
@@ -61,7 +64,8 @@ def main():
     comm.synchronize()
     dt = time.perf_counter() - t0
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
-    print(json.dumps({"size": n, "overlap": args.overlap, "rccl": not args.local,
+    print(json.dumps({"size": n, "overlap": args.overlap, "deep": args.deep, "periodic": per,
+                      "rccl": not args.local,
                       "vcycles_per_s": round(args.steps / dt, 2),
                       "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
 
