@@ -129,6 +129,11 @@ MGIC_API int mgic_plan_create(int rank, int size, const int domain[6], const int
                               int nsrc, const int *src_boxes, const int *src_owners, int ndst,
                               const int *dst_boxes, const int *dst_owners, int with_valid,
                               int with_faces, mgic_plan *out);
+/* the ghost-shell exchange (faces, edges and corners, `depth` deep) of one
+ * layout: what the fused sweeps exchange (depth 2; 4 in deep-halo mode) */
+MGIC_API int mgic_plan_create_shell(int rank, int size, const int domain[6],
+                                    const int periodic[3], int nboxes, const int *boxes,
+                                    const int *owners, int depth, mgic_plan *out);
 MGIC_API int mgic_plan_destroy(mgic_plan p);
 MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpack, int *n_peers);
 MGIC_API int mgic_plan_items(mgic_plan p, int which, long long *items);

@@ -105,6 +105,7 @@ SIGNATURES = {
     "mgic_field_set_val_all": [H, c_double],
     "mgic_op_update_psi": [H, H, H],
     "mgic_plan_create": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PI, PI, c_int, c_int, PH],
+    "mgic_plan_create_shell": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PH],
     "mgic_plan_destroy": [H],
     "mgic_plan_sizes": [H, PI, PI, PI, PI],
     "mgic_plan_items": [H, c_int, PLL],

@@ -346,6 +346,33 @@ MGIC_API int mgic_plan_create(int rank, int size, const int domain[6], const int
     *out = p.release();
   });
 }
+MGIC_API int mgic_plan_create_shell(int rank, int size, const int domain[6],
+                                    const int periodic[3], int nboxes, const int *boxes,
+                                    const int *owners, int depth, mgic_plan *out) {
+  return guard([&] {
+    NEED(domain);
+    NEED(boxes);
+    NEED(owners);
+    NEED(out);
+    MGIC_CHECK(nboxes >= 1, "empty layout");
+    MGIC_CHECK(depth >= 1 && depth <= kGhost, "shell depth exceeds the allocated ghosts");
+    bool per[3] = {false, false, false};
+    if (periodic)
+      for (int d = 0; d < 3; ++d) per[d] = periodic[d] != 0;
+    auto comm = Comm::host_only(rank, size);
+    std::vector<Box> b;
+    std::vector<int> o;
+    for (int i = 0; i < nboxes; ++i) {
+      b.push_back(Box::make(boxes + 6 * i));
+      o.push_back(owners[i]);
+    }
+    auto p = std::make_unique<mgic_plan_s>();
+    p->src = std::make_shared<Grid>(comm, Box::make(domain), per, 1.0, b, o);
+    p->dst = p->src;
+    p->plan = build_copy_plan(*p->src, *p->dst, false, false, false, depth);
+    *out = p.release();
+  });
+}
 MGIC_API int mgic_plan_destroy(mgic_plan p) {
   return guard([&] { delete p; });
 }

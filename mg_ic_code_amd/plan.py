@@ -35,14 +35,23 @@ def _ints(v):
 
 class HostPlan:
     def __init__(self, rank, size, domain, src_boxes, src_owners, dst_boxes=None,
-                 dst_owners=None, periodic=(0, 0, 0), with_valid=False, with_faces=True):
+                 dst_owners=None, periodic=(0, 0, 0), with_valid=False, with_faces=True,
+                 shell=0):
+        """shell > 0: the `shell`-deep ghost-shell exchange of the src layout
+        (faces, edges, corners; mgic_plan_create_shell) instead."""
         if dst_boxes is None:
             dst_boxes, dst_owners = src_boxes, src_owners
         h = ctypes.c_void_p()
-        _lib.call("mgic_plan_create", int(rank), int(size), _ints(domain), _ints(periodic),
-                  len(src_boxes), _ints([v for b in src_boxes for v in b]), _ints(src_owners),
-                  len(dst_boxes), _ints([v for b in dst_boxes for v in b]), _ints(dst_owners),
-                  int(bool(with_valid)), int(bool(with_faces)), ctypes.byref(h))
+        if shell > 0:
+            _lib.call("mgic_plan_create_shell", int(rank), int(size), _ints(domain),
+                      _ints(periodic), len(src_boxes), _ints([v for b in src_boxes for v in b]),
+                      _ints(src_owners), int(shell), ctypes.byref(h))
+        else:
+            _lib.call("mgic_plan_create", int(rank), int(size), _ints(domain), _ints(periodic),
+                      len(src_boxes), _ints([v for b in src_boxes for v in b]), _ints(src_owners),
+                      len(dst_boxes), _ints([v for b in dst_boxes for v in b]),
+                      _ints(dst_owners), int(bool(with_valid)), int(bool(with_faces)),
+                      ctypes.byref(h))
         self._h = h
         self.rank, self.size = int(rank), int(size)
         self.src_local = [i for i, o in enumerate(src_owners) if o == rank]

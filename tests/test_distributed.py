@@ -197,3 +197,86 @@ def test_two_rank_gather_to_rank0_and_scatter_back():
     res = de.run_world(_gather_worker, 2, (dom, (2, 1, 2), [0, 1, 1, 0]))
     for ok, bad in res:
         assert ok and bad == 0
+
+
+def _deep_worker(rank, world, n, parts, owners, periodic, seed):
+    """Deep-halo schedule across ranks: one 4-deep ghost-shell exchange, then
+    sweep 1 on the box grown by 2 across exchanged faces and sweep 2 on the
+    box (each as the fused sweep's passes: RED on the region grown by one
+    more, then BLACK), with no exchange in between."""
+    import oracle
+    from oracle import Fab
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    boxes = split_domain(dom, parts)
+    rng = np.random.default_rng(seed)
+    u0, rhs = rng.uniform(-1, 1, (n, n, n)), rng.uniform(-1, 1, (n, n, n))
+    a, b = rng.uniform(-2.0, -0.5, (n, n, n)), rng.uniform(0.5, 2.0, (n, n, n))
+    dx, alpha, beta, G = 0.1, 1.0, -1.0, 4
+    plan = HostPlan(rank, world, dom, boxes, owners, periodic=periodic, shell=G)
+    flats = [de.alloc(plan, 0, i) for i in range(len(plan.src_local))]
+    for i, bi in enumerate(plan.src_local):
+        bx = boxes[bi]
+        de.box_view(flats[i], plan.geom(0, i), bx)[...] = u0[bx[2]:bx[5] + 1, bx[1]:bx[4] + 1,
+                                                              bx[0]:bx[3] + 1]
+    de.execute(plan, flats, flats)
+    for grow in (2, 0):
+        for i, bi in enumerate(plan.src_local):
+            bx = boxes[bi]
+            full = de.box_view(flats[i], plan.geom(0, i), bx, ghost=G)
+            glo = tuple(v - G for v in bx[:3])
+            # coefficient fabs over the box grown by G (periodic images)
+            idx = [np.arange(bx[d] - G, bx[3 + d] + G + 1) for d in range(3)]
+            idx = [np.mod(ix, n) if periodic[d] else np.clip(ix, 0, n - 1) for d, ix in enumerate(idx)]
+            ax = np.ix_(idx[2], idx[1], idx[0])
+            ag, bg, rg = (np.ascontiguousarray(x[ax]) for x in (a, b, rhs))
+            lam = np.zeros_like(ag)
+            exch = [[periodic[d] or bx[d] > 0, periodic[d] or bx[3 + d] < n - 1] for d in range(3)]
+            hi_g = tuple(v + G for v in bx[3:])
+            oracle.lam(Fab(lam, glo), Fab(ag, glo), glo, hi_g, alpha, beta, dx)
+            for colour, g in ((0, grow + 1), (1, grow)):
+                lo = tuple(bx[d] - (g if exch[d][0] else 0) for d in range(3))
+                hi = tuple(bx[3 + d] + (g if exch[d][1] else 0) for d in range(3))
+                # homogeneous DiriBC order 1 on domain faces: ghost = -near
+                if not exch[0][0]:
+                    full[:, :, G - 1] = -full[:, :, G]
+                if not exch[0][1]:
+                    full[:, :, -G] = -full[:, :, -G - 1]
+                if not exch[1][0]:
+                    full[:, G - 1, :] = -full[:, G, :]
+                if not exch[1][1]:
+                    full[:, -G, :] = -full[:, -G - 1, :]
+                if not exch[2][0]:
+                    full[G - 1] = -full[G]
+                if not exch[2][1]:
+                    full[-G] = -full[-G - 1]
+                uf = np.ascontiguousarray(full)
+                oracle.gsrb(Fab(uf, glo), Fab(rg, glo), lo, hi, dx, alpha, Fab(ag, glo), beta,
+                            Fab(bg, glo), Fab(lam, glo), colour)
+                full[...] = uf
+    return {bi: np.array(de.box_view(flats[i], plan.geom(0, i), boxes[bi]))
+            for i, bi in enumerate(plan.src_local)}
+
+
+@pytest.mark.parametrize("periodic", [(0, 0, 0), (1, 1, 0)])
+def test_two_rank_deep_halo_two_sweeps_match_single_box_oracle(periodic):
+    # the 4-deep shell plan across ranks carries everything two sweeps need
+    import oracle
+    n, parts, owners, seed = 16, (2, 2, 2), [0, 1, 1, 0, 1, 0, 0, 1], 5
+    res = de.run_world(_deep_worker, 2, (n, parts, owners, periodic, seed))
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    boxes = split_domain(dom, parts)
+    got = np.full((n, n, n), np.nan)
+    for r in res:
+        for bi, arr in r.items():
+            bx = boxes[bi]
+            got[bx[2]:bx[5] + 1, bx[1]:bx[4] + 1, bx[0]:bx[3] + 1] = arr
+    rng = np.random.default_rng(seed)
+    u0, rhs = rng.uniform(-1, 1, (n, n, n)), rng.uniform(-1, 1, (n, n, n))
+    a, b = rng.uniform(-2.0, -0.5, (n, n, n)), rng.uniform(0.5, 2.0, (n, n, n))
+    o = oracle.OracleMG([dom], dom, 0.1, alpha=1.0, beta=-1.0, nlevels=1, periodic=periodic)
+    for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs), (oracle.PHI, u0)):
+        o.set(0, f, 0, arr)
+    o.setup()
+    o.level_gsrb(0, oracle.PHI, oracle.RHS)
+    o.level_gsrb(0, oracle.PHI, oracle.RHS)
+    assert np.array_equal(got, o.get(0, oracle.PHI, 0))
