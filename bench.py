@@ -50,6 +50,11 @@ def parse():
                     help="4-deep ghost shells, two sweeps per exchange: 0 off, 1 every level, "
                          "2 levels of boxes <= 128^3; default 1 for N > 1 (RCCL exchanges: "
                          "fewer, larger messages), 0 on one GPU (local copies are cheap)")
+    ap.add_argument("--roofline-events", choices=("relax", "launch"), default="relax",
+                    help="HIP events for the smoother roofline: one pair per relax call "
+                         "(default; time / launches) or one pair per launch")
+    ap.add_argument("--no-roofline-events", action="store_true",
+                    help="no events in the timed region (roofline fields null)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -125,7 +130,8 @@ def main():
     comm.synchronize()
 
     fine_cells = max((b[3] - b[0] + 1) * (b[4] - b[1] + 1) * (b[5] - b[2] + 1) for b in boxes)
-    mg.prof_smoother(True, fine_cells)
+    mg.prof_smoother(not args.no_roofline_events, fine_cells,
+                     per_relax=args.roofline_events == "relax")
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -217,7 +223,11 @@ def main():
                         "(u, rhs, aCoef in, u out); traffic = PMC HBM bytes per launch "
                         "(profiles/traffic_smoother.json)",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
-                "avg_launch_ms": round(avg_launch_ms, 5),
+                "avg_launch_ms": round(avg_launch_ms, 5) if launches else None,
+                "timing": ("off" if args.no_roofline_events else
+                           "HIP events on the operator stream, one pair per relax call "
+                           "(interval / launches)" if args.roofline_events == "relax"
+                           else "HIP events on the operator stream, one pair per launch"),
                 "launches_timed": launches,
             },
             "cpu_baseline": cpu,

@@ -335,9 +335,11 @@ MGIC_API void mgic_solve_params_default(mgic_solve_params *p);
 MGIC_API int mgic_mg_solve(mgic_mg mg, mgic_field phi, mgic_field rhs, const mgic_solve_params *p,
                            int *iterations, double *final_norm);
 
-/* ---- instrumentation: hipEvents around every smoother launch on boxes of
- * at least min_cells cells; passes = colour passes those launches performed
- * (1 per-colour launch, 2 one fused sweep, 4 two fused sweeps) */
+/* ---- instrumentation: hipEvents around the smoother launches on boxes of
+ * at least min_cells cells (enable 1: a pair per launch; 2: a pair per run of
+ * consecutive launches within one relax call -- fewer records in the timed
+ * stream); launches / passes = launches timed and the colour passes they
+ * performed (1 per-colour launch, 2 one fused sweep, 4 two fused sweeps) */
 MGIC_API int mgic_prof_smoother(int enable, long min_cells);
 MGIC_API int mgic_prof_smoother_read(int *launches, long *passes, double *total_ms);
 

@@ -757,8 +757,11 @@ def set_binary_bh_coefs(acoef: LevelData, rhs: LevelData, bh: dict) -> None:
     call("mgic_field_binary_bh", acoef.handle, rhs.handle, vals)
 
 
-def prof_smoother(enable: bool, min_cells: int = 0) -> None:
-    call("mgic_prof_smoother", int(bool(enable)), int(min_cells))
+def prof_smoother(enable: bool, min_cells: int = 0, per_relax: bool = False) -> None:
+    """HIP events around the fine-level smoother launches: one pair per launch,
+    or (per_relax) one pair per run of consecutive launches in a relax call
+    (fewer event records in the timed stream; time / launches = the average)."""
+    call("mgic_prof_smoother", (2 if per_relax else 1) if enable else 0, int(min_cells))
 
 
 def prof_smoother_read() -> Tuple[int, int, float]:

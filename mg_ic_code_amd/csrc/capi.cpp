@@ -1240,7 +1240,7 @@ MGIC_API int mgic_mg_solve(mgic_mg mg, mgic_field phi, mgic_field rhs, const mgi
   });
 }
 MGIC_API int mgic_prof_smoother(int enable, long min_cells) {
-  return guard([&] { prof_enable(enable != 0, min_cells); });
+  return guard([&] { prof_enable(enable != 0, min_cells, enable == 2 ? 2 : 1); });
 }
 MGIC_API int mgic_prof_smoother_read(int *launches, long *passes, double *total_ms) {
   return guard([&] {

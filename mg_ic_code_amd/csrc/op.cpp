@@ -10,46 +10,75 @@ namespace mgic {
 
 // --------------------------------------------------------------- profiling
 namespace {
+// HIP events around the fine-level smoother launches (bench.py's roofline).
+// mode 1: one event pair per launch.  mode 2: one pair per run of
+// consecutive counted launches (a relax call), time / launches = the
+// average launch: an event record between two kernels costs a ~5-10 us
+// gap on this stack, which mode 1 adds to the timed V-cycle 16 times.
 struct SmootherProf {
-  bool on = false;
+  int mode = 0;
   long min_cells = 0;
   std::vector<hipEvent_t> ev;
   size_t used = 0;
   bool open = false;
-  long passes = 0;  // colour passes covered by the recorded launches
+  long passes = 0;    // colour passes covered by the recorded launches
+  long launches = 0;  // launches inside the recorded intervals
+  hipStream_t st = nullptr;
 } g_prof;
+
+void prof_record(hipStream_t st) {
+  if (g_prof.used + 1 > g_prof.ev.size()) {
+    const size_t add = std::max<size_t>(256, g_prof.ev.size());
+    for (size_t i = 0; i < add; ++i) {
+      hipEvent_t e;
+      MGIC_HIP(hipEventCreate(&e));
+      g_prof.ev.push_back(e);
+    }
+  }
+  MGIC_HIP(hipEventRecord(g_prof.ev[g_prof.used++], st));
+}
 }  // namespace
 
-void prof_enable(bool on, long min_cells) {
-  g_prof.on = on;
+void prof_enable(bool on, long min_cells, int mode) {
+  g_prof.mode = on ? mode : 0;
   g_prof.min_cells = min_cells;
   g_prof.used = 0;
   g_prof.open = false;
   g_prof.passes = 0;
+  g_prof.launches = 0;
 }
 
-void prof_mark(hipStream_t st, long ncells, bool begin, int passes) {
-  if (!g_prof.on || ncells < g_prof.min_cells) return;
-  if (begin) {
-    if (g_prof.used + 2 > g_prof.ev.size()) {
-      const size_t add = std::max<size_t>(256, g_prof.ev.size());
-      for (size_t i = 0; i < add; ++i) {
-        hipEvent_t e;
-        MGIC_HIP(hipEventCreate(&e));
-        g_prof.ev.push_back(e);
-      }
-    }
-    MGIC_HIP(hipEventRecord(g_prof.ev[g_prof.used], st));
-    g_prof.open = true;
-  } else if (g_prof.open) {
-    MGIC_HIP(hipEventRecord(g_prof.ev[g_prof.used + 1], st));
-    g_prof.used += 2;
-    g_prof.passes += passes;
+void prof_flush() {
+  if (g_prof.mode == 2 && g_prof.open) {
+    prof_record(g_prof.st);
     g_prof.open = false;
   }
 }
 
+void prof_mark(hipStream_t st, long ncells, bool begin, int passes) {
+  if (!g_prof.mode) return;
+  if (ncells < g_prof.min_cells) {  // an uncounted launch closes a mode-2 interval
+    if (begin) prof_flush();
+    return;
+  }
+  if (begin) {
+    if (g_prof.open && g_prof.mode == 2 && st == g_prof.st) return;  // interval continues
+    prof_flush();
+    prof_record(st);
+    g_prof.open = true;
+    g_prof.st = st;
+  } else if (g_prof.open) {
+    g_prof.passes += passes;
+    g_prof.launches += 1;
+    if (g_prof.mode == 1) {
+      prof_record(st);
+      g_prof.open = false;
+    }
+  }
+}
+
 int prof_read(double *total_ms, long *passes) {
+  prof_flush();
   double tot = 0.0;
   if (g_prof.used) MGIC_HIP(hipEventSynchronize(g_prof.ev[g_prof.used - 1]));
   for (size_t i = 0; i + 1 < g_prof.used; i += 2) {
@@ -59,7 +88,7 @@ int prof_read(double *total_ms, long *passes) {
   }
   *total_ms = tot;
   if (passes) *passes = g_prof.passes;
-  return (int)(g_prof.used / 2);
+  return (int)g_prof.launches;
 }
 
 // --------------------------------------------------------------- operator
@@ -501,6 +530,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     std::swap(src, dst);
     it += k;
   }
+  prof_flush();  // the interval ends with the relax
   if (side_pending) MGIC_HIP(hipStreamWaitEvent(st, evE, 0));
   if (acc) return false;  // the last sweep went into acc; dpsi is scratch now
   if (src != &dpsi) {  // the result sits in the scratch buffer

@@ -185,7 +185,8 @@ std::shared_ptr<LevelData> average_coef(const LevelData &fine, std::shared_ptr<G
 
 // Smoother instrumentation: when enabled, every smoother launch on a box of
 // at least min_cells cells is bracketed by hipEvents on its stream.
-void prof_enable(bool on, long min_cells);
+void prof_enable(bool on, long min_cells, int mode = 1);  // mode 1 per launch, 2 per relax
+void prof_flush();
 int prof_read(double *total_ms, long *passes);  // returns launches timed, total ms
 // bracket one smoother launch (no-op unless enabled and ncells >= min_cells)
 void prof_mark(hipStream_t st, long ncells, bool begin, int passes);
