@@ -51,6 +51,12 @@ void gsrb_sweep_fused_restrict(double *u_out, double *u_in, const double *rhs, c
 void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       int depth, hipStream_t st);
+// two red+black sweeps u_in -> u_out in one z-streaming launch (128x16
+// tiles, 6-plane LDS ring, coefficients carried in registers): boxes whose
+// six faces are domain faces, constant bCoef, above the block-kernel size
+bool gsrb_sweep_fused2s_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
+void gsrb_sweep_fused2s(double *u_out, const double *u_in, const double *rhs, const double *a,
+                        const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st);
 // two red+black sweeps u_in -> u_out in one launch (temporal blocking);
 // BC folded in-kernel, u_in is not modified (zero_in: not read either)
 void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,

@@ -275,10 +275,15 @@ bool VariableCoeffPoissonOperator::fusedSmootherApplies() const {
   return prm.fused_smoother != 0;
 }
 
+// MGIC_SWEEPS_PER_LAUNCH: 1 (default) one sweep per launch; 2 pairs sweeps
+// in the two-sweep kernel where it applies (bit-identical; measured the same
+// 0.886 ms per 512^3 sweep, slower at 256^3: both kernels are issue/latency
+// bound at two waves per SIMD, not HBM bound); 3 the older wide-ring
+// two-sweep kernel (measurement only)
 static int sweeps_per_launch() {
   static const int v = [] {
     const char *e = getenv("MGIC_SWEEPS_PER_LAUNCH");
-    return e ? std::max(1, std::min(2, atoi(e))) : 1;
+    return e ? std::max(1, std::min(3, atoi(e))) : 1;
   }();
   return v;
 }
@@ -412,7 +417,11 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     }
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
-  const int per = acc ? 1 : sweeps_per_launch();
+  // two sweeps per launch (temporal blocking) on boxes with only domain faces
+  bool two = !halo && sweeps_per_launch() >= 2 && n >= 2;
+  for (int b = 0; two && b < grid->nlocal(); ++b)
+    two = sweeps_per_launch() == 3 || kern::gsrb_sweep_fused2s_applies(args_hom_[b], s, prm.fused_smoother);
+  const int per = two ? 2 : 1;
   const bool want_out = halo && (flags & kHaloOut) && !acc;
   const bool overlap = halo && per == 1 && overlapApplies();
   const bool split = halo && per == 1 && !overlap && splitApplies();
@@ -434,7 +443,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     evE = grid->comm->event(1);
   }
   // the last sweep restricts too (single sweep kernel over every box)
-  bool restrict_last = rst != nullptr && !acc && !(zero_in && n == 1) && !halo && per == 1;
+  bool restrict_last = rst != nullptr && !acc && !(zero_in && n == 1) && !halo;
   if (restrict_last) {
     const Grid &cg = *rst->grid;
     restrict_last = cg.nlocal() == grid->nlocal();
@@ -446,7 +455,10 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   bool side_pending = false;
   for (int it = 0; it < n;) {
     const bool zin = zero_in && it == 0;
-    const int k = (per == 2 && !halo && n - it >= 2) ? 2 : 1;
+    // a pair, unless it would swallow a special last sweep (+ restriction,
+    // phi += e)
+    const int left = n - it;
+    const int k = per == 2 && (left >= 3 || (left == 2 && !restrict_last && !acc)) ? 2 : 1;
     const bool last = it + k == n;
     if (deep) {
       if (vd < 2) {
@@ -500,9 +512,12 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
       // sweep+restriction launch moves other bytes)
       const long nc = last && restrict_last ? 0 : grid->geom[b].valid.ncells();
       prof_mark(st, nc, true, 2 * k);
-      if (k == 2)  // two sweeps in one launch (temporal blocking)
+      if (k == 2 && sweeps_per_launch() == 3)
         kern::gsrb_sweep_fused2x(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
                                  args_hom_[b], s, zin, st);
+      else if (k == 2)  // two sweeps in one launch (temporal blocking)
+        kern::gsrb_sweep_fused2s(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], args_hom_[b], s,
+                                 zin, st);
       else if (last && restrict_last)  // + restrictResidual(rst, result, rhs)
         kern::gsrb_sweep_fused_restrict(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b],
                                         m_bCoef->p[b], args_hom_[b], s, rst->p[b],

@@ -1286,6 +1286,255 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused2x(double *__restrict__ uo,
   }
 }
 
+
+// ---- two sweeps per launch, z-streaming (temporal blocking) --------------
+// k_gsrb_fused6's scheme carried two sweeps deep on a 128 x 16 tile: at step
+// p a workgroup updates RED(sweep 1) on plane p over the tile grown by 3,
+// BLACK(1) on plane p-1 grown by 2, RED(2) on plane p-2 grown by 1 and
+// BLACK(2) on plane p-3 over the tile, then stores plane p-3.  Each plane
+// lives in one slot of a 6-plane LDS ring (red / black split as in fused6)
+// from its load until its store and is updated in place by the four stages
+// (a colour pass reads only the other colour).  rhs/a pairs are loaded once,
+// one step ahead, and the element each later stage needs is kept in
+// registers (no reloads).  The domain BC is folded into each update (a ghost
+// is the image of the cell being updated, before its update -- the value
+// ParseBC writes before each colour pass); only tiles reaching a face pay.
+// Boxes whose six faces are domain faces, bCoef one value (bval).
+// Compulsory traffic: 32 B/cell per TWO sweeps (u, rhs, a in, u out).
+template <int TX, int TY, int NT>
+struct F2S {
+  static_assert(TX % 2 == 0, "TX must be even");
+  static constexpr int PW = TX / 2 + 4;      // pairs per region row (x0-4 .. x0+TX+3)
+  static constexpr int LH = TY + 8;          // region rows y0-4 .. y0+TY+3
+  static constexpr int CP = PW * LH;         // pairs per plane
+  static constexpr int NS = 6;               // LDS ring planes p-4 .. p+1
+  static constexpr int NRP = PW * (TY + 6);  // update pairs: rows y0-3 .. y0+TY+2
+  static constexpr int NL = (CP + NT - 1) / NT;
+  static constexpr int NP = (NRP + NT - 1) / NT;
+};
+
+template <int TX, int TY, int NT, bool ZIN>
+__global__ __launch_bounds__(NT) void k_gsrb_fused2s(double *__restrict__ uo,
+                                                     const double *__restrict__ ui,
+                                                     const double *__restrict__ rhs,
+                                                     const double *__restrict__ a,
+                                                     const BoxArgs g, const StencilCoefs s, int kc,
+                                                     int ntx, int nty, int nblocks) {
+  using F = F2S<TX, TY, NT>;
+  constexpr int PW = F::PW, CP = F::CP, NS = F::NS, NRP = F::NRP, NL = F::NL, NP = F::NP;
+  __shared__ double R[NS * CP];  // red element of every pair
+  __shared__ double B[NS * CP];  // black element
+  const int bid = blockIdx.x;    // XCD-aware tile order, as k_gsrb_fused6
+  const int q8 = nblocks / 8, r8 = nblocks % 8;
+  const int L = (bid % 8) * q8 + min(bid % 8, r8) + bid / 8;
+  const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
+  const int z0 = (L / (ntx * nty)) * kc, z1 = min(z0 + kc, g.nz);
+  const int tid = threadIdx.x;
+  const long sy = g.sy, sz = g.sz;
+  const int nx = g.nx, ny = g.ny, nz = g.nz;
+  const int xpmax = (nx + 2) & ~1;  // last pair start inside the padded row (x <= nx + 3)
+  const int q0 = (x0 + g.glo[0] + g.glo[1] + g.glo[2]) & 1;
+  auto slot = [](int p) { return ((p % NS) + NS) % NS; };
+  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+
+  long loff[NL];
+  int lgy[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = tid + i * NT;
+    const int r = c / PW, m = c - r * PW;
+    lgy[i] = y0 - 4 + r;
+    loff[i] = c < CP ? (long)min(x0 - 4 + 2 * m, xpmax) + (long)clampi(lgy[i], -4, ny + 3) * sy : 0;
+  }
+  // update pairs: ring level of each element (0 tile, 1..3 the rings, 99 off
+  // the box or no pair), BC-face flags, LDS index, store offset
+  long rcoff[NP], roff[NP];
+  int rgy[NP], rgx0[NP], rci[NP], rw[NP], rbc[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int c = tid + i * NT;
+    const int rr = c / PW, m = c - rr * PW;
+    rgy[i] = y0 - 3 + rr;
+    rgx0[i] = x0 - 4 + 2 * m;
+    rci[i] = c < NRP ? (rr + 1) * PW + m : PW + 1;  // padding slots read a valid cell
+    roff[i] = (long)rgx0[i] + (long)rgy[i] * sy;
+    rcoff[i] = c < NRP ? (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], -4, ny + 3) * sy : 0;
+    const int gy = rgy[i];
+    const int dy = gy < 0 || gy >= ny ? 99 : (gy < y0 ? y0 - gy : (gy >= y0 + TY ? gy - (y0 + TY - 1) : 0));
+    int w2 = 0, f2 = 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int gx = rgx0[i] + e;
+      const int dx = gx < 0 || gx >= nx ? 99 : (gx < x0 ? x0 - gx : (gx >= x0 + TX ? gx - (x0 + TX - 1) : 0));
+      const int w = c < NRP ? max(dx, dy) : 99;
+      w2 |= (w > 15 ? 15 : w) << (4 * e);
+      f2 |= ((gx == 0) | ((gx == nx - 1) << 1) | ((gy == 0) << 2) | ((gy == ny - 1) << 3)) << (4 * e);
+    }
+    rw[i] = w2;
+    rbc[i] = f2;
+  }
+  // does any cell this workgroup updates touch an x / y domain face?
+  const bool edge = x0 - 3 <= 0 || x0 + TX + 2 >= nx - 1 || y0 - 3 <= 0 || y0 + TY + 2 >= ny - 1;
+
+  double pu0[NL], pu1[NL];
+  double nr0[NP], nr1[NP], na0[NP], na1[NP];  // pairs of plane p+1 (in flight)
+  double cr0[NP], cr1[NP], ca0[NP], ca1[NP];  // pairs of plane p
+  double k1r[NP], k1a[NP], k1R[NP], k1A[NP];  // plane p-1: black element, red element
+  double k2r[NP], k2a[NP], k2R[NP], k2A[NP];  // plane p-2: black element, red element
+  double k3r[NP], k3a[NP];                    // plane p-3: black element
+
+  auto fetch_u = [&](int p) {
+    const long pz = (long)clampi(p, -4, nz + 3) * sz;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      if (ZIN) {
+        pu0[i] = 0.0;
+        pu1[i] = 0.0;
+      } else {
+        const double2 v = *reinterpret_cast<const double2 *>(ui + loff[i] + pz);
+        pu0[i] = v.x;
+        pu1[i] = v.y;
+      }
+    }
+  };
+  // a plane enters the ring in two halves: its slot's previous plane (p-6)
+  // is read as R by the last stage of the previous step, so the R half is
+  // written only after the step's first barrier
+  auto put_half = [&](int p, bool red) {
+    double *Xs = (red ? R : B) + slot(p) * CP;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int c = tid + i * NT;
+      if (NL * NT > CP && c >= CP) continue;
+      const int q = (q0 + lgy[i] + p) & 1;  // 1: the red element is the second
+      Xs[c] = red ? bsel(q, pu1[i], pu0[i]) : bsel(q, pu0[i], pu1[i]);
+    }
+  };
+  auto put_u = [&](int p) {
+    put_half(p, true);
+    put_half(p, false);
+  };
+  auto fetch_c = [&](int p) {
+    const long pz = (long)clampi(p, -4, nz + 3) * sz;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const double2 vr = *reinterpret_cast<const double2 *>(rhs + rcoff[i] + pz);
+      const double2 va = *reinterpret_cast<const double2 *>(a + rcoff[i] + pz);
+      nr0[i] = vr.x; nr1[i] = vr.y;
+      na0[i] = va.x; na1[i] = va.y;
+    }
+  };
+  // one colour pass on plane p over the ring of width w: RED updates the red
+  // element of every pair from the black neighbours, BLACK the converse
+  auto stage = [&](bool red, int p, int w, const double *cr, const double *ca) {
+    double *Xs = (red ? R : B) + slot(p) * CP;
+    const double *Ns = (red ? B : R) + slot(p) * CP;
+    const double *Nm = (red ? B : R) + slot(p - 1) * CP;
+    const double *Np = (red ? B : R) + slot(p + 1) * CP;
+    const bool zlo = p == 0, zhi = p == nz - 1;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int q = (q0 + rgy[i] + p) & 1;
+      const int e = red ? q : 1 - q;  // element updated: 1 = the second of the pair
+      const int sh = 4 * e;
+      if (((rw[i] >> sh) & 15) > w) continue;
+      const int ci = rci[i];
+      const double uc = Xs[ci];
+      double xm = e ? Ns[ci] : Ns[ci - 1];
+      double xp = e ? Ns[ci + 1] : Ns[ci];
+      double ym = Ns[ci - PW], yp = Ns[ci + PW], zm = Nm[ci], zp = Np[ci];
+      if (edge) {  // SetBCs.cpp:49-131 folded: ghost = image of uc
+        const int f = rbc[i] >> sh;
+        if (f & 1) xm = ghost_of(g.bcm[0], g.bcc[0], uc);
+        if (f & 2) xp = ghost_of(g.bcm[1], g.bcc[1], uc);
+        if (f & 4) ym = ghost_of(g.bcm[2], g.bcc[2], uc);
+        if (f & 8) yp = ghost_of(g.bcm[3], g.bcc[3], uc);
+      }
+      if (zlo) zm = ghost_of(g.bcm[4], g.bcc[4], uc);
+      if (zhi) zp = ghost_of(g.bcm[5], g.bcc[5], uc);
+      const double av = ca[i];
+      const double tx = (xp + xm) - 2.0 * uc;
+      const double ty = (yp + ym) - 2.0 * uc;
+      const double tz = (zp + zm) - 2.0 * uc;
+      const double lap = (tx + ty) + tz;                     // .ChF:111-120
+      double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
+      const double ldpsi = lap * s.dxinv * s.bval;           // .ChF:122
+      lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
+      const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
+      Xs[ci] = uc - lam * (lofdpsi - cr[i]);                 // .ChF:127-128
+    }
+  };
+
+  fetch_u(z0 - 4);
+  put_u(z0 - 4);
+  fetch_u(z0 - 3);
+  put_u(z0 - 3);
+  fetch_u(z0 - 2);
+  fetch_c(z0 - 3);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    cr0[i] = nr0[i]; cr1[i] = nr1[i];
+    ca0[i] = na0[i]; ca1[i] = na1[i];
+    k1r[i] = k1a[i] = k1R[i] = k1A[i] = 0.0;
+    k2r[i] = k2a[i] = k2R[i] = k2A[i] = 0.0;
+    k3r[i] = k3a[i] = 0.0;
+  }
+  for (int p = z0 - 3; p <= z1 + 2; ++p) {
+    put_half(p + 1, false);
+    fetch_c(p + 1);
+    double er[NP], ea[NP];  // red element of plane p
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int q = (q0 + rgy[i] + p) & 1;
+      er[i] = bsel(q, cr1[i], cr0[i]);
+      ea[i] = bsel(q, ca1[i], ca0[i]);
+    }
+    __syncthreads();
+    put_half(p + 1, true);  // R of plane p+1 is first read next step
+    fetch_u(p + 2);
+    if (p >= max(z0 - 3, 0) && p <= min(z1 + 2, nz - 1)) stage(true, p, 3, er, ea);
+    __syncthreads();
+    if (p - 1 >= max(z0 - 2, 0) && p - 1 <= min(z1 + 1, nz - 1)) stage(false, p - 1, 2, k1r, k1a);
+    __syncthreads();
+    if (p - 2 >= max(z0 - 1, 0) && p - 2 <= min(z1, nz - 1)) stage(true, p - 2, 1, k2R, k2A);
+    __syncthreads();
+    const int k = p - 3;
+    if (k >= z0 && k < z1) {  // BLACK(2) on the tile, then store plane k
+      stage(false, k, 0, k3r, k3a);
+      // each thread stores the pairs it updated (its own LDS writes: no barrier)
+      const double *Rs = R + slot(k) * CP, *Bs = B + slot(k) * CP;
+      double *dst = uo + (long)k * sz;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int gy = rgy[i];
+        if (gy < y0 || gy >= y0 + TY || gy >= ny || rgx0[i] < x0 || rgx0[i] >= x0 + TX ||
+            rgx0[i] >= nx || tid + i * NT >= NRP)
+          continue;
+        const int qb = 1 - ((q0 + gy + k) & 1);  // 1: the black element is the second
+        const double red = Rs[rci[i]], blk = Bs[rci[i]];
+        double2 w;
+        w.x = bsel(qb, red, blk);
+        w.y = bsel(qb, blk, red);
+        if (rgx0[i] + 1 < nx) *reinterpret_cast<double2 *>(dst + roff[i]) = w;
+        else dst[roff[i]] = w.x;
+      }
+    }
+    // the elements later stages need move down one plane
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int qb = 1 - ((q0 + rgy[i] + p) & 1);
+      k3r[i] = k2r[i]; k3a[i] = k2a[i];
+      k2r[i] = k1r[i]; k2a[i] = k1a[i];
+      k2R[i] = k1R[i]; k2A[i] = k1A[i];
+      k1r[i] = bsel(qb, cr1[i], cr0[i]);
+      k1a[i] = bsel(qb, ca1[i], ca0[i]);
+      k1R[i] = er[i];
+      k1A[i] = ea[i];
+      cr0[i] = nr0[i]; cr1[i] = nr1[i];
+      ca0[i] = na0[i]; ca1[i] = na1[i];
+    }
+  }
+}
 }  // namespace
 
 // workgroups of kernel `k` the whole device holds at once
@@ -1390,6 +1639,44 @@ static int fused2x_variant() {
     return e ? atoi(e) : 0;
   }();
   return v;
+}
+
+static long block_max_cells();
+
+template <int TX, int TY, int NT>
+static void launch_fused2s(double *u_out, const double *u_in, const double *rhs, const double *a,
+                           const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st) {
+  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
+  static const int slots = resident_slots(k_gsrb_fused2s<TX, TY, NT, false>, NT);
+  const int kc = choose_kc(ntx * nty, g.nz, slots, 6);
+  const int ntz = (g.nz + kc - 1) / kc;
+  const int nblocks = ntx * nty * ntz;
+  const dim3 grid((unsigned)nblocks), block(NT);
+  if (zero_in)
+    k_gsrb_fused2s<TX, TY, NT, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, g, s, kc, ntx,
+                                                             nty, nblocks);
+  else
+    k_gsrb_fused2s<TX, TY, NT, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, g, s, kc, ntx,
+                                                              nty, nblocks);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(kHipErr, std::string("two-sweep launch: ") + hipGetErrorString(e));
+}
+
+bool gsrb_sweep_fused2s_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
+  static const int enabled = [] {
+    const char *e = getenv("MGIC_TWO_SWEEPS");
+    return e ? atoi(e) : 1;
+  }();
+  if (!enabled || !s.bconst) return false;
+  for (int f = 0; f < 6; ++f)
+    if (!g.bcm[f]) return false;  // exchanged faces would need a 4-deep shell
+  if (kind == 0 || kind == 3) return false;
+  return kind == 2 || (long)g.nx * g.ny * g.nz > block_max_cells();  // z-streaming territory
+}
+
+void gsrb_sweep_fused2s(double *u_out, const double *u_in, const double *rhs, const double *a,
+                        const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st) {
+  launch_fused2s<128, 16, 512>(u_out, u_in, rhs, a, g, s, zero_in, st);
 }
 
 void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,

@@ -619,3 +619,51 @@ def test_chf_dropin_setleveldata_bitwise(rng):
             ints(*(h + 1 for h in hi)) + [ctypes.byref(ctypes.c_double(dx))] + ints(*lo) + ints(*hi)
         getattr(mg.lib, name)(*args)
         assert np.array_equal(out, fn(src, lo, hi, dx)), name
+
+
+_TWO_SWEEPS_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import mg_ic_code_amd as mg, oracle
+for shape, lo, bc_lo, bc_hi, bcv in (((48, 40, 56), (-16, 8, 32), (0, 1, 0), (1, 0, 1), 0.25),
+                                     ((64, 64, 64), (0, 0, 0), (0, 0, 0), (0, 0, 0), 0.0)):
+    rng = np.random.default_rng(17)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    nz, ny, nx = shape[2], shape[1], shape[0]
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx)); rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    b = np.ones((nz, ny, nx))
+    grid = mg.Grid(mg.Comm(), dom, [dom], 0.37)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    fa.upload(0, a); fb.upload(0, b); frhs.upload(0, rhs); fphi.set_zero()
+    prm = mg.OperatorParams(alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bcv,
+                            coefficient_average_type=1, prolong_type=1, fused_smoother=2)
+    amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, prm),
+                          mg.SolverParams(max_depth=2, n_pre=5, n_post=4, n_bottom=4,
+                                          bottom_solver=0))
+    o = oracle.OracleMG([dom], dom, 0.37, alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi,
+                        bc_value=bcv, nlevels=3, avg_type=1, prolong_type=1, bottom_solver=0,
+                        n_pre=5, n_post=4, n_bottom=4)
+    for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs)):
+        o.set(0, f, 0, arr)
+    o.setup()
+    amg.init_residual(fphi, frhs, fres); o.init_residual(0)
+    for _ in range(2):
+        assert amg.iteration(fphi, frhs, fres, 0) == o.iteration(0)
+    assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
+print("two-sweep OK")
+"""
+
+
+def test_two_sweep_kernel_vcycle_bitwise():
+    # the temporally blocked two-sweep kernel (MGIC_SWEEPS_PER_LAUNCH=2, read
+    # once per process: a child process), odd and even sweep counts, ragged
+    # mixed-BC box and a cube, against the oracle bit for bit
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MGIC_SWEEPS_PER_LAUNCH="2")
+    r = subprocess.run([sys.executable, "-c", _TWO_SWEEPS_CHILD, root], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "two-sweep OK" in r.stdout
