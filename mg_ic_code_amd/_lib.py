@@ -12,7 +12,8 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_long, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmgic.so")
+# MGIC_LIB_PATH: another build of the library (A/B measurements only)
+LIB_PATH = os.environ.get("MGIC_LIB_PATH") or os.path.join(_HERE, "libmgic.so")
 
 
 class MgicError(RuntimeError):

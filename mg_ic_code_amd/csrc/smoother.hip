@@ -139,7 +139,8 @@ __device__ __forceinline__ void fused6_segment(T *__restrict__ R, T *__restrict_
   // including along exchanged faces, whose shell cells are loaded as they
   // are.  Cells that are ghosts of two BC faces (never read) get garbage.
   long loff[NL];
-  int lgy[NL], lbc[NL];
+  int lgy[NL], lbc[NL], lym[NL];
+  T lyc[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int c = tid + i * NT;
@@ -165,6 +166,11 @@ __device__ __forceinline__ void fused6_segment(T *__restrict__ R, T *__restrict_
     }
     lbc[i] = c < CP ? bx | (by << 2) : 0;
     loff[i] = c < CP ? (long)gx + (long)gy * sy : 0;
+    // the y-face BC of the pair, static indices only: g.bcm[1 + by] with a
+    // per-lane index puts BoxArgs in memory and costs a dependent load +
+    // vmcnt(0) per pair inside the z loop
+    lym[i] = by == 1 ? g.bcm[2] : by == 2 ? g.bcm[3] : 0;
+    lyc[i] = (T)(by == 1 ? g.bcc[2] : g.bcc[3]);
   }
   // ring pairs owned by this thread (coefficient loads, red/black updates)
   long roff[NP], rcoff[NP];
@@ -209,6 +215,8 @@ __device__ __forceinline__ void fused6_segment(T *__restrict__ R, T *__restrict_
   auto put_u = [&](int p) {
     T *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
     const int zf = (g.bcm[4] && p == -1) ? 4 : (g.bcm[5] && p == nz) ? 5 : -1;
+    const int zmode = zf == 4 ? g.bcm[4] : g.bcm[5];  // uniform; static indices
+    const T zc = (T)(zf == 4 ? g.bcc[4] : g.bcc[5]);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = tid + i * NT;
@@ -217,16 +225,15 @@ __device__ __forceinline__ void fused6_segment(T *__restrict__ R, T *__restrict_
       if (!ZIN) {  // BC images (a zero input images to zero: homogeneous BC)
         const int bx = lbc[i] & 3, by = lbc[i] >> 2;
         if (by) {
-          const int f = 1 + by;
-          u0 = ghost_of(g.bcm[f], (T)g.bcc[f], u0);
-          u1 = ghost_of(g.bcm[f], (T)g.bcc[f], u1);
+          u0 = ghost_of(lym[i], lyc[i], u0);
+          u1 = ghost_of(lym[i], lyc[i], u1);
         }
         if (bx == 1) u1 = ghost_of(g.bcm[0], (T)g.bcc[0], u0);
         else if (bx == 2) u0 = ghost_of(g.bcm[1], (T)g.bcc[1], u1);
         else if (bx == 3) u1 = ghost_of(g.bcm[1], (T)g.bcc[1], u0);
         if (zf >= 0) {
-          u0 = ghost_of(g.bcm[zf], (T)g.bcc[zf], u0);
-          u1 = ghost_of(g.bcm[zf], (T)g.bcc[zf], u1);
+          u0 = ghost_of(zmode, zc, u0);
+          u1 = ghost_of(zmode, zc, u1);
         }
       }
       const int q = (q0 + lgy[i] + p) & 1;  // 1: the red element is the second
@@ -716,7 +723,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
 
   // region pairs: loads (BC images applied on entry, as k_gsrb_fused6)
   long loff[NL];
-  int lgy[NL], lbc[NL];
+  int lgy[NL], lbc[NL], lym[NL];
+  double lyc[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int c = tid + i * NT;
@@ -742,6 +750,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
     }
     lbc[i] = c < CP ? bx | (by << 2) : 0;
     loff[i] = c < CP ? (long)gx + (long)gy * sy : 0;
+    lym[i] = by == 1 ? g.bcm[2] : by == 2 ? g.bcm[3] : 0;  // static indices (fused6)
+    lyc[i] = by == 1 ? g.bcc[2] : g.bcc[3];
   }
   // ring pairs (tile + 2): coefficient loads, red / black updates, stores
   long rcoff[NP];
@@ -770,6 +780,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
   const bool rown = fxr < nx && fyr < ny;
   const int cci = (2 * cy + 3) * PW + cx + 2;  // LDS index of the (fxr, fyr) pair
   const long frow = (long)min(fxr, xpmax) + (long)min(fyr, ny - 1) * sy;
+  const bool xyface = (g.bcm[0] && x0 == 0) || (g.bcm[1] && x0 + TX >= nx) ||
+                      (g.bcm[2] && y0 == 0) || (g.bcm[3] && y0 + TY >= ny);
 
   double pu0[NL], pu1[NL];
   double cr0[NP], cr1[NP], ca0[NP], ca1[NP], cb0[NP], cb1[NP];
@@ -792,6 +804,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
   auto put_u = [&](int p) {
     double *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
     const int zf = (g.bcm[4] && p == -1) ? 4 : (g.bcm[5] && p == nz) ? 5 : -1;
+    const int zmode = zf == 4 ? g.bcm[4] : g.bcm[5];
+    const double zc = zf == 4 ? g.bcc[4] : g.bcc[5];
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       const int c = tid + i * NT;
@@ -799,16 +813,15 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
       double u0 = pu0[i], u1 = pu1[i];
       const int bx = lbc[i] & 3, by = lbc[i] >> 2;
       if (by) {
-        const int f = 1 + by;
-        u0 = ghost_of(g.bcm[f], g.bcc[f], u0);
-        u1 = ghost_of(g.bcm[f], g.bcc[f], u1);
+        u0 = ghost_of(lym[i], lyc[i], u0);
+        u1 = ghost_of(lym[i], lyc[i], u1);
       }
       if (bx == 1) u1 = ghost_of(g.bcm[0], g.bcc[0], u0);
       else if (bx == 2) u0 = ghost_of(g.bcm[1], g.bcc[1], u1);
       else if (bx == 3) u1 = ghost_of(g.bcm[1], g.bcc[1], u0);
       if (zf >= 0) {
-        u0 = ghost_of(g.bcm[zf], g.bcc[zf], u0);
-        u1 = ghost_of(g.bcm[zf], g.bcc[zf], u1);
+        u0 = ghost_of(zmode, zc, u0);
+        u1 = ghost_of(zmode, zc, u1);
       }
       const int q = (q0 + lgy[i] + p) & 1;
       Rs[c] = bsel(q, u1, u0);
@@ -904,23 +917,25 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
       // the colour of a row is uniform over the workgroup (fyr even), so each
       // element comes from R or B by a uniform choice: element e of a pair
       // is red iff e == (q0 + row + plane) & 1
-      auto el = [&](const double *Rp_, const double *Bp_, int ci, int e, int row, int k) {
-        return (e == ((q0 + row + k) & 1)) ? Rp_[ci] : Bp_[ci];
+      // (the parity of row fyr + dr is that of y0 + dr: written with y0, the
+      // choice is visibly uniform and selects a base address, not a value)
+      auto el = [&](const double *Rp_, const double *Bp_, int ci, int e, int dr, int k) {
+        return ((e == ((q0 + y0 + dr + k) & 1)) ? Rp_ : Bp_)[ci];
       };
       double v[4][2], zm[2][2], zp[2][2], xl[2], xr[2];
 #pragma unroll
       for (int r = 0; r < 4; ++r)  // rows fyr-1 .. fyr+2 of plane k
 #pragma unroll
-        for (int e = 0; e < 2; ++e) v[r][e] = el(Rs, Bs, cci + (r - 1) * PW, e, fyr + r - 1, kr3);
+        for (int e = 0; e < 2; ++e) v[r][e] = el(Rs, Bs, cci + (r - 1) * PW, e, r - 1, kr3);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
-        const int ci = cci + jj * PW, row = fyr + jj;
-        xl[jj] = el(Rs, Bs, ci - 1, 1, row, kr3);
-        xr[jj] = el(Rs, Bs, ci + 1, 0, row, kr3);
+        const int ci = cci + jj * PW;
+        xl[jj] = el(Rs, Bs, ci - 1, 1, jj, kr3);
+        xr[jj] = el(Rs, Bs, ci + 1, 0, jj, kr3);
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          zm[jj][e] = el(Rm, Bm, ci, e, row, kr3 - 1);
-          zp[jj][e] = el(Rp, Bp, ci, e, row, kr3 + 1);
+          zm[jj][e] = el(Rm, Bm, ci, e, jj, kr3 - 1);
+          zp[jj][e] = el(Rp, Bp, ci, e, jj, kr3 + 1);
         }
       }
 #pragma unroll
@@ -934,10 +949,12 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
           double vxp = ii ? xr[jj] : v[jj + 1][1];
           double vym = v[jj][ii], vyp = v[jj + 2][ii];
           double vzm = zm[jj][ii], vzp = zp[jj][ii];
-          if (i == 0 && g.bcm[0]) vxm = ghost_of(g.bcm[0], g.bcc[0], uc);
-          if (i == nx - 1 && g.bcm[1]) vxp = ghost_of(g.bcm[1], g.bcc[1], uc);
-          if (j == 0 && g.bcm[2]) vym = ghost_of(g.bcm[2], g.bcc[2], uc);
-          if (j == ny - 1 && g.bcm[3]) vyp = ghost_of(g.bcm[3], g.bcc[3], uc);
+          if (xyface) {  // only tiles on an x / y domain face (uniform)
+            if (i == 0 && g.bcm[0]) vxm = ghost_of(g.bcm[0], g.bcc[0], uc);
+            if (i == nx - 1 && g.bcm[1]) vxp = ghost_of(g.bcm[1], g.bcc[1], uc);
+            if (j == 0 && g.bcm[2]) vym = ghost_of(g.bcm[2], g.bcc[2], uc);
+            if (j == ny - 1 && g.bcm[3]) vyp = ghost_of(g.bcm[3], g.bcc[3], uc);
+          }
           if (kr3 == 0 && g.bcm[4]) vzm = ghost_of(g.bcm[4], g.bcc[4], uc);
           if (kr3 == nz - 1 && g.bcm[5]) vzp = ghost_of(g.bcm[5], g.bcc[5], uc);
           const double tx = (vxp + vxm) - 2.0 * uc;
@@ -1694,7 +1711,9 @@ void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, co
 // tile shape, for measurement (MGIC_FUSED_VARIANT): 0 = 128x16 / 512 threads
 // (default: one 106 KB workgroup per CU, 1 KB contiguous rows, u halo 1.29x,
 // coefficient ring 1.16x), 1 = 60x8 / 256 (4 workgroups per CU); a 256x8 /
-// 512 variant measured 0.90 ms.  512^3 sweep: 0.89 / 1.05 ms; 256^3: 0.142 /
+// 512 variant measured 0.90 ms, 128x16 / 1024 threads (four waves per SIMD,
+// 107 VGPRs) 0.93 ms, loads two steps ahead (three rotating register sets)
+// 0.89 ms: neither more waves nor deeper prefetch moves it.  512^3 sweep: 0.89 / 1.05 ms; 256^3: 0.142 /
 // 0.168 ms.
 static int fused_variant() {
   static int v = [] {

@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--local", action="store_true", help="local copies instead of RCCL")
     ap.add_argument("--deep", type=int, default=0, help="deep halo (two sweeps per exchange)")
     ap.add_argument("--periodic", default="1,1,1", help="periodic directions (exchanged faces)")
+    ap.add_argument("--shape", default=None,
+                    help="nx,ny,nz of the rank's box (default: a --size cube); e.g. 512,512,256 "
+                         "periodic 0,0,1 for one rank of the 2-GPU z-slab split")
     args = ap.parse_args()
     import mg_ic_code_amd as mg
     from mg_ic_code_amd.params import read_params_file
@@ -40,7 +43,8 @@ def main():
     else:
         comm = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
         comm.set_self_messages(True)
-    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    shp = tuple(int(v) for v in args.shape.split(",")) if args.shape else (n, n, n)
+    dom = (0, 0, 0, shp[0] - 1, shp[1] - 1, shp[2] - 1)
     per = tuple(int(v) for v in args.periodic.split(","))
     grid = mg.Grid(comm, dom, [dom], prm.L / n, periodic=per)
     fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
@@ -64,7 +68,7 @@ def main():
     comm.synchronize()
     dt = time.perf_counter() - t0
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
-    print(json.dumps({"size": n, "overlap": args.overlap, "deep": args.deep, "periodic": per,
+    print(json.dumps({"size": n, "shape": shp, "overlap": args.overlap, "deep": args.deep, "periodic": per,
                       "rccl": not args.local,
                       "vcycles_per_s": round(args.steps / dt, 2),
                       "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
