@@ -1758,11 +1758,14 @@ static void launch_block(T *u_out, T *u_in, const T *rhs, const T *a, const T *b
 }
 
 // boxes of at most this many cells take the block kernel (MGIC_BLOCK_MAX_CELLS;
-// 0 = never); MGIC_BLOCK_VARIANT picks its tile for measurement
+// 0 = never); MGIC_BLOCK_VARIANT picks its tile for measurement.  132^3, not
+// 128^3: the deep halo's grown boxes at the 64^3-per-rank level (130^3) run
+// 20 us per sweep here against 31 us streamed (one rank of the 8-GPU run:
+// 1.92 -> 1.87 ms per V-cycle)
 static long block_max_cells() {
   static long v = [] {
     const char *e = getenv("MGIC_BLOCK_MAX_CELLS");
-    return e ? atol(e) : 128L * 128 * 128;
+    return e ? atol(e) : 132L * 132 * 132;
   }();
   return v;
 }
