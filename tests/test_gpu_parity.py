@@ -667,3 +667,43 @@ def test_two_sweep_kernel_vcycle_bitwise():
                        capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "two-sweep OK" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_post", [1, 3])
+@pytest.mark.parametrize("bvar", [False, True])
+def test_streaming_vcycle_post_sweeps_bitwise(rng, comm, n_post, bvar):
+    # z-streaming kernels at every level, an odd number of post-smoothing
+    # sweeps (n_post = 1: the sweep after the prolongation is also the one
+    # that adds phi += e), random or constant bCoef; against the oracle bit
+    # for bit
+    shape = (64, 48, 40)
+    lo = (-32, 16, 0)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    bc_lo, bc_hi, bcv = (1, 0, 0), (0, 1, 1), -0.5
+    nz, ny, nx = shape[2], shape[1], shape[0]
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    b = rng.uniform(0.5, 2.0, (nz, ny, nx)) if bvar else np.ones((nz, ny, nx))
+    rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    grid = mg.Grid(comm, dom, [dom], 0.41)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    fa.upload(0, a)
+    fb.upload(0, b)
+    frhs.upload(0, rhs)
+    fphi.set_zero()
+    prm = mg.OperatorParams(alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bcv,
+                            coefficient_average_type=1, prolong_type=1, fused_smoother=2)
+    amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, prm),
+                          mg.SolverParams(max_depth=2, n_pre=2, n_post=n_post, n_bottom=3,
+                                          bottom_solver=0))
+    o = oracle.OracleMG([dom], dom, 0.41, alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi,
+                        bc_value=bcv, nlevels=3, avg_type=1, prolong_type=1, bottom_solver=0,
+                        n_pre=2, n_post=n_post, n_bottom=3)
+    for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs)):
+        o.set(0, f, 0, arr)
+    o.setup()
+    amg.init_residual(fphi, frhs, fres)
+    o.init_residual(0)
+    for _ in range(3):
+        assert amg.iteration(fphi, frhs, fres, 0) == o.iteration(0)
+    assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
