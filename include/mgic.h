@@ -26,6 +26,8 @@
 #ifndef MGIC_H
 #define MGIC_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -317,6 +319,10 @@ MGIC_API int mgic_field_layout(mgic_field f, int domain[6], int periodic[3], dou
                                int *rank, int *size);
 MGIC_API int mgic_field_box(mgic_field f, int i, int lohi[6], int *owner, int *local_index);
 MGIC_API int mgic_field_barrier(mgic_field f);
+/* page-locked host memory (hipHostMalloc) for staging device output: the
+ * D2H copies of mgic_field_*_vars run at full PCIe rate into it */
+MGIC_API int mgic_host_alloc(size_t bytes, void **out);
+MGIC_API int mgic_host_free(void *p);
 
 /* MultilevelLinearOp::preCond: e = 0, then `iters` AMRMultiGrid iterations
  * on (e, r), homogeneous BC (Main_PoissonSolver.cpp:107-117) */

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_int, c_long, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_int, c_long, c_size_t, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MGIC_LIB_PATH: another build of the library (A/B measurements only)
@@ -191,6 +191,8 @@ SIGNATURES = {
     "mgic_field_layout": [H, PI, PI, PD, PI, PI, PI],
     "mgic_field_box": [H, c_int, PI, PI, PI],
     "mgic_field_barrier": [H],
+    "mgic_host_alloc": [c_size_t, PH],
+    "mgic_host_free": [c_void_p],
     "mgic_prof_smoother": [c_int, c_long],
     "mgic_prof_smoother_read": [PI, POINTER(c_long), PD],
     # ChomboFortran drop-ins (include/mgic_chf.h); argtypes left open

@@ -685,6 +685,18 @@ MGIC_API int mgic_field_barrier(mgic_field f) {
     MGIC_HIP(hipStreamSynchronize(c.stream()));
   });
 }
+MGIC_API int mgic_host_alloc(size_t bytes, void **out) {
+  return guard([&] {
+    NEED(out);
+    *out = nullptr;
+    MGIC_HIP(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  });
+}
+MGIC_API int mgic_host_free(void *p) {
+  return guard([&] {
+    if (p) MGIC_HIP(hipHostFree(p));
+  });
+}
 MGIC_API int mgic_field_binary_bh(mgic_field acoef, mgic_field rhs, const double bh[13]) {
   return mgic_field_nl_coefs(nullptr, acoef, rhs, bh);
 }

@@ -15,6 +15,8 @@
 #include <map>
 #include <stdexcept>
 #include <string>
+#include <thread>
+#include <exception>
 #include <vector>
 
 namespace {
@@ -263,10 +265,41 @@ void write_fields(const std::string &fname, Job &J, const std::vector<mgic_field
   if (rank == 0) create_file(fname, J);
   mg(mgic_field_barrier(lead[0]));
   const long long kSlabBytes = 256ll << 20;  // host staging per slab
-  std::vector<double> host;
+  // two page-locked slabs: slab i+1 is computed and copied D2H while a
+  // writer thread puts slab i into the file (only that thread calls HDF5
+  // meanwhile; the main thread only calls libmgic)
+  struct Pinned {
+    double *p = nullptr;
+    size_t n = 0;
+    void reserve(size_t m) {
+      if (m <= n) return;
+      if (p) mgic_host_free(p);
+      p = nullptr;
+      n = 0;
+      void *q = nullptr;
+      mg(mgic_host_alloc(sizeof(double) * m, &q));
+      p = static_cast<double *>(q);
+      n = m;
+    }
+    ~Pinned() {
+      if (p) mgic_host_free(p);
+    }
+  } host[2];
+  std::thread writer;
+  std::exception_ptr werr;
+  auto join = [&] {
+    if (writer.joinable()) writer.join();
+    if (werr) std::rethrow_exception(werr);
+  };
   for (int r = 0; r < size; ++r) {
     if (r == rank) {
       DataWriter W(fname, nlev);
+      struct Joiner {  // an exception leaves no writer thread on W or the slabs
+        std::thread &t;
+        ~Joiner() {
+          if (t.joinable()) t.join();
+        }
+      } joiner{writer};
       for (int l = 0; l < nlev; ++l) {
         const LevelLayout &L = J.levels[l];
         long long off = 0;
@@ -280,14 +313,29 @@ void write_fields(const std::string &fname, Job &J, const std::vector<mgic_field
             const long long plane = (long long)nx * ny;
             int nk = (int)std::max<long long>(1, kSlabBytes / (8ll * J.ncomp * plane));
             if (nk > nz) nk = nz;
-            host.resize((size_t)J.ncomp * plane * nk);
+            int cur = 0;
             for (int k0 = 0; k0 < nz; k0 += nk) {
               const int kk = std::min(nk, nz - k0);
-              produce(l, loc, k0, kk, host.data());
-              for (int c = 0; c < J.ncomp; ++c)
-                W.write(l, (hsize_t)(off + c * nc + k0 * plane), (hsize_t)(kk * plane),
-                        host.data() + (size_t)c * kk * plane);
+              if (host[cur].n < (size_t)J.ncomp * plane * nk) {
+                join();  // the writer may still read the other slab, not this one
+                host[cur].reserve((size_t)J.ncomp * plane * nk);
+              }
+              double *buf = host[cur].p;
+              produce(l, loc, k0, kk, buf);
+              join();
+              const int ncomp = J.ncomp;
+              writer = std::thread([&W, &werr, l, off, nc, k0, kk, plane, ncomp, buf] {
+                try {
+                  for (int c = 0; c < ncomp; ++c)
+                    W.write(l, (hsize_t)(off + c * nc + k0 * plane), (hsize_t)(kk * plane),
+                            buf + (size_t)c * kk * plane);
+                } catch (...) {
+                  werr = std::current_exception();
+                }
+              });
+              cur ^= 1;
             }
+            join();
           }
           off += nc * J.ncomp;
         }
