@@ -707,3 +707,48 @@ def test_streaming_vcycle_post_sweeps_bitwise(rng, comm, n_post, bvar):
     for _ in range(3):
         assert amg.iteration(fphi, frhs, fres, 0) == o.iteration(0)
     assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
+
+
+@pytest.mark.gpu
+def test_full_size_512_vcycle_bitwise():
+    # BASELINE config C3 at its full size: the 512^3 3-level V-cycle of
+    # bench.py (SetBinaryBH source on device, harmonic averaging, linear
+    # prolongation, nu = 4, 4 bottom sweeps) -- two AMRMultiGrid iterations on
+    # the GPU against the C oracle (OpenMP), phi and the residual norms bit
+    # for bit.  ~8 GB of host memory, ~20 s.
+    import os
+    from mg_ic_code_amd.params import read_params_file
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prm = read_params_file(os.path.join(root, "tests", "golden", "params.txt"))
+    n = 512
+    dx = prm.L / n
+    bh = prm.bh()
+    bh["domain_length"] = dx * n
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    grid = mg.Grid(mg.Comm(), dom, [dom], dx)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    mg.set_binary_bh_coefs(fa, frhs, bh)
+    fb.set_val(1.0)
+    fphi.set_zero()
+    op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                           bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
+                           coefficient_average_type=1, prolong_type=1, relax_mode=1,
+                           fused_smoother=1)
+    amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, op),
+                          mg.SolverParams(max_depth=2, n_pre=4, n_post=4, n_bottom=4,
+                                          bottom_solver=0))
+    r0 = amg.init_residual(fphi, frhs, fres, norm_type=0)
+    rg = [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(2)]
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    o = oracle.OracleMG([dom], dom, dx, alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                        bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value, nlevels=3, avg_type=1,
+                        prolong_type=1, bottom_solver=0, n_pre=4, n_post=4, n_bottom=4)
+    a = fa.download(0)
+    o.set(0, oracle.ACOEF, 0, a)
+    o.set(0, oracle.BCOEF, 0, np.ones_like(a))
+    del a
+    o.set(0, oracle.RHS, 0, frhs.download(0))
+    o.setup()
+    assert o.init_residual(0) == r0
+    assert [o.iteration(0) for _ in range(2)] == rg
+    assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
