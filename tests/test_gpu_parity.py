@@ -752,3 +752,44 @@ def test_full_size_512_vcycle_bitwise():
     assert o.init_residual(0) == r0
     assert [o.iteration(0) for _ in range(2)] == rg
     assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
+
+
+@pytest.mark.gpu
+def test_full_size_256_single_level_gsrb_and_residual_bitwise():
+    # BASELINE config C2 at its full size: 256^3 single level, SetBinaryBH
+    # source, the GSRB smoother (8 fused sweeps from dpsi = 0) and then the
+    # residual rhs - L(dpsi) with the inhomogeneous BC, against the oracle
+    # bit for bit (the "GSRB smoother vs CPU residual" of the config)
+    import os
+    from mg_ic_code_amd.params import read_params_file
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prm = read_params_file(os.path.join(root, "tests", "golden", "params.txt"))
+    n = 256
+    dx = prm.L / n
+    bh = prm.bh()
+    bh["domain_length"] = dx * n
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    grid = mg.Grid(mg.Comm(), dom, [dom], dx)
+    fa, fb, frhs, fu, fres = (mg.LevelData(grid) for _ in range(5))
+    mg.set_binary_bh_coefs(fa, frhs, bh)
+    fb.set_val(1.0)
+    fu.set_zero()
+    op = mg.defineOperatorFactory(
+        grid, fa, fb, mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                                        bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
+                                        relax_mode=1, fused_smoother=1)).AMRnewOp()
+    op.relax(fu, frhs, 8)
+    op.residualI(fres, fu, frhs, homogeneous=False)
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    o = oracle.OracleMG([dom], dom, dx, alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                        bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value, nlevels=1)
+    a = fa.download(0)
+    o.set(0, oracle.ACOEF, 0, a)
+    o.set(0, oracle.BCOEF, 0, np.ones_like(a))
+    o.set(0, oracle.RHS, 0, frhs.download(0))
+    o.set(0, oracle.PHI, 0, np.zeros_like(a))
+    o.setup()
+    o.relax(0, oracle.PHI, oracle.RHS, 8)
+    o.residual(0, oracle.RESID, oracle.PHI, oracle.RHS, 0)
+    assert np.array_equal(fu.download(0), o.get(0, oracle.PHI, 0))
+    assert np.array_equal(fres.download(0), o.get(0, oracle.RESID, 0))
