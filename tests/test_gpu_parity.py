@@ -793,3 +793,47 @@ def test_full_size_256_single_level_gsrb_and_residual_bitwise():
     o.residual(0, oracle.RESID, oracle.PHI, oracle.RHS, 0)
     assert np.array_equal(fu.download(0), o.get(0, oracle.PHI, 0))
     assert np.array_equal(fres.download(0), o.get(0, oracle.RESID, 0))
+
+
+@pytest.mark.gpu
+def test_full_size_512_eight_boxes_rccl_deep_halo_bitwise():
+    # BASELINE config C4's code path at its full size on one GPU: 512^3 as the
+    # 8-GPU split (2x2x2 boxes of 256^3), every exchange through RCCL
+    # self send/recv, the deep halo N > 1 runs with -- against the single-box
+    # run (itself bit-identical to the oracle, test_full_size_512_vcycle_
+    # bitwise), phi and residual norms bit for bit over two iterations
+    import os
+    from mg_ic_code_amd.decomposition import decompose
+    from mg_ic_code_amd.params import read_params_file
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prm = read_params_file(os.path.join(root, "tests", "golden", "params.txt"))
+    n = 512
+    dx = prm.L / n
+    bh = prm.bh()
+    bh["domain_length"] = dx * n
+    out = []
+    for parts, deep in (((1, 1, 1), 0), ((2, 2, 2), 1)):
+        if parts == (1, 1, 1):
+            c = mg.Comm()
+        else:
+            c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+            c.set_self_messages(True)
+        dom, boxes, owners = decompose((n, n, n), 1, boxes_per_rank=parts)
+        grid = mg.Grid(c, dom, boxes, dx, owners=owners)
+        fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+        mg.set_binary_bh_coefs(fa, frhs, bh)
+        fb.set_val(1.0)
+        fphi.set_zero()
+        op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                               bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
+                               coefficient_average_type=1, prolong_type=1, relax_mode=1,
+                               fused_smoother=1, deep_halo=deep)
+        amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, op),
+                              mg.SolverParams(max_depth=2, n_pre=4, n_post=4, n_bottom=4,
+                                              bottom_solver=0))
+        norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
+        norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(2)]
+        out.append((norms, download_global(fphi, grid, (n,) * 3)))
+        del amg, fa, fb, frhs, fphi, fres, grid
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])
