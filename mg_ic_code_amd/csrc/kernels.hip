@@ -180,6 +180,68 @@ __device__ __forceinline__ V2<T> ld2(const T *__restrict__ p) {
   return *reinterpret_cast<const V2<T> *>(p);
 }
 
+// k_residual_z on x-pairs: a thread owns columns (2i, 2i+1) of a z chunk, so
+// u, rhs, a (and b) are one 16-B load per pair and the x neighbours inside
+// the pair come from registers (xl, xr: the cells either side).  Rows are
+// padded and the valid-lo 16-B aligned (FabGeom), so the pair's second cell
+// is always allocated; at an odd nx the last pair writes its first cell
+// only.  Same expressions, per cell, as k_residual.
+template <bool BC, class RT>
+__global__ __launch_bounds__(256) void k_residual_z2(RT *__restrict__ r,
+                                                     const double *__restrict__ u,
+                                                     const double *__restrict__ rhs,
+                                                     const double *__restrict__ a,
+                                                     const double *__restrict__ b, const BoxArgs g,
+                                                     const StencilCoefs s, int kc) {
+  const int i = 2 * (blockIdx.x * TX + threadIdx.x);
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, g.nz);
+  if (i >= g.nx || j >= g.ny) return;
+  const long col = (long)i + (long)j * g.sy;
+  const bool two = i + 1 < g.nx;
+  const bool fx0 = i == 0 && g.bcm[0];
+  const bool fx1a = i == g.nx - 1 && g.bcm[1], fx1b = i + 1 == g.nx - 1 && g.bcm[1];
+  const bool fy0 = j == 0 && g.bcm[2], fy1 = j == g.ny - 1 && g.bcm[3];
+  double2 um = ld2(u + col + (long)(k0 - 1) * g.sz);  // ghost plane -1 is allocated
+  double2 uc = ld2(u + col + (long)k0 * g.sz);
+  for (int k = k0; k < k1; ++k) {
+    const long idx = col + (long)k * g.sz;
+    const double2 up = ld2(u + idx + g.sz);  // plane nz (ghost) when k = nz - 1
+    const double xl = u[idx - 1], xr = u[idx + 2];
+    const double2 ym = ld2(u + idx - g.sy), yp = ld2(u + idx + g.sy);
+    const double2 rv = ld2(rhs + idx), av = ld2(a + idx);
+    const double2 bv = BC ? make_double2(s.bval, s.bval) : ld2(b + idx);
+    auto cell = [&](double c, double xm, double xp, double ymv, double ypv, double zm, double zp,
+                    double rr, double aa, double bb, bool bxm, bool bxp) {
+      if (bxm) xm = ghost_of(g.bcm[0], g.bcc[0], c);
+      if (bxp) xp = ghost_of(g.bcm[1], g.bcc[1], c);
+      if (fy0) ymv = ghost_of(g.bcm[2], g.bcc[2], c);
+      if (fy1) ypv = ghost_of(g.bcm[3], g.bcc[3], c);
+      if (k == 0 && g.bcm[4]) zm = ghost_of(g.bcm[4], g.bcc[4], c);
+      if (k == g.nz - 1 && g.bcm[5]) zp = ghost_of(g.bcm[5], g.bcc[5], c);
+      const double res = rr - s.alpha * aa * c;            // .ChF:314-316
+      const double tx = (xp + xm) - 2.0 * c;
+      const double ty = (ypv + ymv) - 2.0 * c;
+      const double tz = (zp + zm) - 2.0 * c;
+      double ldpsi = (tx + ty) + tz;                       // .ChF:320-329
+      ldpsi = ldpsi * s.dxinv * s.beta * bb;               // .ChF:331
+      return (RT)(res + ldpsi);                            // .ChF:333
+    };
+    const RT r0 = cell(uc.x, xl, uc.y, ym.x, yp.x, um.x, up.x, rv.x, av.x, bv.x, fx0, fx1a);
+    const RT r1 = cell(uc.y, uc.x, xr, ym.y, yp.y, um.y, up.y, rv.y, av.y, bv.y, false, fx1b);
+    if (two) {
+      V2<RT> w;
+      w.x = r0;
+      w.y = r1;
+      *reinterpret_cast<V2<RT> *>(r + idx) = w;
+    } else {
+      r[idx] = r0;
+    }
+    um = uc;
+    uc = up;
+  }
+}
+
 template <class T, bool BC>
 __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxArgs cg,
                                                   const T *__restrict__ u,
@@ -972,7 +1034,17 @@ void residual(double *r, const double *u, const double *rhs, const double *a, co
     const char *e = getenv("MGIC_RESIDUAL_KC");
     return e ? atoi(e) : 16;
   }();
-  if (mode > 0) {  // z-streaming, chunks of `mode` planes
+  static const int pairs = [] {
+    const char *e = getenv("MGIC_RESIDUAL_PAIRS");
+    return e ? atoi(e) : 1;
+  }();
+  if (mode > 0 && pairs) {  // z-streaming on x-pairs, chunks of `mode` planes
+    const int kc = mode < g.nz ? mode : g.nz;
+    dim3 grid = grid_cells((g.nx + 1) / 2, g.ny, g.nz);
+    grid.z = (unsigned)((g.nz + kc - 1) / kc);
+    if (s.bconst) k_residual_z2<true, double><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+    else k_residual_z2<false, double><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  } else if (mode > 0) {  // z-streaming, chunks of `mode` planes
     const int kc = mode < g.nz ? mode : g.nz;
     dim3 grid = grid_cells(g.nx, g.ny, g.nz);
     grid.z = (unsigned)((g.nz + kc - 1) / kc);
@@ -1202,10 +1274,10 @@ void residual_to_f(float *r, const double *u, const double *rhs, const double *a
                    const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
   const int kc = 16 < g.nz ? 16 : g.nz;
-  dim3 grid = grid_cells(g.nx, g.ny, g.nz);
+  dim3 grid = grid_cells((g.nx + 1) / 2, g.ny, g.nz);
   grid.z = (unsigned)((g.nz + kc - 1) / kc);
-  if (s.bconst) k_residual_z<true, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
-  else k_residual_z<false, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  if (s.bconst) k_residual_z2<true, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  else k_residual_z2<false, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
   check_launch();
 }
 
