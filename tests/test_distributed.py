@@ -1,4 +1,4 @@
-"""world_size = 2 tests of the multi-rank path on CPU (gloo).
+"""world_size = 2, 4 and 8 tests of the multi-rank path on CPU (gloo).
 
 The GPU path moves halos with RCCL over xGMI, and the data it moves is
 fixed by the per-rank CopyPlan. These tests take that exact plan from
@@ -207,7 +207,7 @@ def _deep_worker(rank, world, n, parts, owners, periodic, seed):
     import oracle
     from oracle import Fab
     dom = (0, 0, 0, n - 1, n - 1, n - 1)
-    boxes = split_domain(dom, parts)
+    boxes = list(parts) if isinstance(parts, list) else split_domain(dom, parts)
     rng = np.random.default_rng(seed)
     u0, rhs = rng.uniform(-1, 1, (n, n, n)), rng.uniform(-1, 1, (n, n, n))
     a, b = rng.uniform(-2.0, -0.5, (n, n, n)), rng.uniform(0.5, 2.0, (n, n, n))
@@ -274,6 +274,35 @@ def test_two_rank_deep_halo_two_sweeps_match_single_box_oracle(periodic):
     u0, rhs = rng.uniform(-1, 1, (n, n, n)), rng.uniform(-1, 1, (n, n, n))
     a, b = rng.uniform(-2.0, -0.5, (n, n, n)), rng.uniform(0.5, 2.0, (n, n, n))
     o = oracle.OracleMG([dom], dom, 0.1, alpha=1.0, beta=-1.0, nlevels=1, periodic=periodic)
+    for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs), (oracle.PHI, u0)):
+        o.set(0, f, 0, arr)
+    o.setup()
+    o.level_gsrb(0, oracle.PHI, oracle.RHS)
+    o.level_gsrb(0, oracle.PHI, oracle.RHS)
+    assert np.array_equal(got, o.get(0, oracle.PHI, 0))
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bench_split_deep_halo_two_sweeps_match_single_box_oracle(world):
+    # the exact splits bench.py --gpus 4 / 8 run (decompose: 1x2x2 slabs /
+    # 2x2x2 boxes, one box per rank), rehearsed with `world` gloo ranks on the
+    # CPU: one 4-deep shell exchange carries two sweeps, bit-identical to the
+    # single-box oracle
+    import oracle
+    from mg_ic_code_amd.decomposition import decompose
+    n, seed = 16, 7
+    dom, boxes, owners = decompose((n, n, n), world)
+    assert len(boxes) == world and sorted(owners) == list(range(world))
+    res = de.run_world(_deep_worker, world, (n, list(boxes), list(owners), (0, 0, 0), seed))
+    got = np.full((n, n, n), np.nan)
+    for r in res:
+        for bi, arr in r.items():
+            bx = boxes[bi]
+            got[bx[2]:bx[5] + 1, bx[1]:bx[4] + 1, bx[0]:bx[3] + 1] = arr
+    rng = np.random.default_rng(seed)
+    u0, rhs = rng.uniform(-1, 1, (n, n, n)), rng.uniform(-1, 1, (n, n, n))
+    a, b = rng.uniform(-2.0, -0.5, (n, n, n)), rng.uniform(0.5, 2.0, (n, n, n))
+    o = oracle.OracleMG([dom], dom, 0.1, alpha=1.0, beta=-1.0, nlevels=1)
     for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs), (oracle.PHI, u0)):
         o.set(0, f, 0, arr)
     o.setup()
