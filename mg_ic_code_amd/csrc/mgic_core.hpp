@@ -151,7 +151,11 @@ enum BcMode : int {
   kBcMemory = 0,     // ghost holds exchanged data (internal / periodic face)
   kBcDirichlet = 1,  // ghost = c - near            (c = 2*value; DiriBC order 1)
   kBcNeumannHom = 2, // ghost = near
-  kBcNeumann = 3     // ghost = near + c            (c = isign*dx*value)
+  kBcNeumann = 3,    // ghost = near + c            (c = isign*dx*value)
+  // homogeneous QuadCFInterp ghost of an AMR level's coarse-fine face:
+  // ((8/15)*0 + (2/3)*near) + (-0.2)*next (k_cf_interp<true>); the 3D-block
+  // sweep kernel only (it refills these ghosts between its colour passes)
+  kBcCFHom = 4
 };
 
 struct BoxArgs {

@@ -265,8 +265,54 @@ void VariableCoeffPoissonOperator::setTime(double t) {
   m_lambdaNeedsResetting = true;
 }
 
-bool VariableCoeffPoissonOperator::fusedSmootherApplies() const {
-  if (cf) return false;  // CF ghosts are refilled before every colour pass
+// An AMR level whose boxes are isolated patches (no box face touches another
+// box, no periodic images): every non-domain face is a coarse-fine face, so
+// homogeneousCFInterp before each colour pass (.cpp:296) is a per-face ghost
+// rule of the two cells next to it, which the 3D-block sweep applies in LDS
+// at entry and again between its red and black passes (MGIC_CF_FUSED=0: the
+// per-colour path).  Mixed faces (part CF, part fine-fine) stay per colour.
+bool VariableCoeffPoissonOperator::cfFusedApplies() {
+  if (cf_fused_ >= 0) return cf_fused_ == 1;
+  static const int enabled = [] {
+    const char *e = getenv("MGIC_CF_FUSED");
+    return e ? atoi(e) : 1;
+  }();
+  bool ok = enabled && prm.fused_smoother != 0;
+  for (int d = 0; d < 3; ++d) ok = ok && !grid->periodic[d];
+  const std::vector<Box> &bx = grid->boxes;
+  for (size_t i = 0; ok && i < bx.size(); ++i)
+    for (size_t j = 0; ok && j < bx.size(); ++j) {
+      if (i == j) continue;
+      for (int d = 0; ok && d < 3; ++d) {  // box i grown by one across its d faces
+        Box g = bx[i];
+        g.lo[d] -= 1;
+        g.hi[d] += 1;
+        bool meet = true;
+        for (int e = 0; e < 3; ++e)
+          meet = meet && g.lo[e] <= bx[j].hi[e] && bx[j].lo[e] <= g.hi[e];
+        ok = !meet;
+      }
+    }
+  for (int n = 0; ok && n < grid->nlocal(); ++n) {
+    const FabGeom &fg = grid->geom[n];
+    ok = fg.nx % 2 == 0 && fg.valid.lo[0] % 2 == 0;  // the kernel's x pairs
+  }
+  args_cf_.clear();
+  for (int n = 0; ok && n < grid->nlocal(); ++n) {
+    BoxArgs a = args_hom_[n];
+    for (int f = 0; f < 6; ++f)
+      if (a.bcm[f] == kBcMemory) {
+        a.bcm[f] = kBcCFHom;
+        a.bcc[f] = 0.0;
+      }
+    args_cf_.push_back(a);
+  }
+  cf_fused_ = ok ? 1 : 0;
+  return ok;
+}
+
+bool VariableCoeffPoissonOperator::fusedSmootherApplies() {
+  if (cf) return cfFusedApplies();  // isolated patches only (see above)
   // Both colour passes of a sweep in one launch per box.  Faces on the
   // domain boundary fold the BC; exchanged faces (box or periodic
   // neighbours) get a 2-deep ghost shell before the sweep, from which the
@@ -401,7 +447,14 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
   if (!sweep_tmp_) sweep_tmp_ = create();
-  const bool halo = grid->has_memory_faces();
+  // AMR level > 0 (isolated patches): no exchanges, coarse-fine faces as
+  // ghost rules, 3D-block kernel, no fused restriction / two-sweep launches
+  const bool cfl = cf != nullptr;
+  if (cfl) MGIC_CHECK(cfFusedApplies(), "fused sweep on a coarse-fine level it does not apply to");
+  const std::vector<BoxArgs> &sargs = cfl ? args_cf_ : args_hom_;
+  const int skind = cfl ? 3 : prm.fused_smoother;
+  if (cfl) rst = nullptr;
+  const bool halo = !cfl && grid->has_memory_faces();
   const bool deep_ok = halo && deepApplies();
   if (halo) {  // ghost layer 1 of rhs / aCoef / bCoef for the red ring on the halo
     if (!(flags & kRhsHaloReady)) rhsHalo(const_cast<LevelData &>(rhs), st);
@@ -418,7 +471,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
   // two sweeps per launch (temporal blocking) on boxes with only domain faces
-  bool two = !halo && sweeps_per_launch() >= 2 && n >= 2;
+  bool two = !halo && !cfl && sweeps_per_launch() >= 2 && n >= 2;
   for (int b = 0; two && b < grid->nlocal(); ++b)
     two = sweeps_per_launch() == 3 || kern::gsrb_sweep_fused2s_applies(args_hom_[b], s, prm.fused_smoother);
   const int per = two ? 2 : 1;
@@ -529,8 +582,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
                                m_bCoef->p[b] + o, ga, s, zin, nullptr, prm.fused_smoother, st);
       } else
         kern::gsrb_sweep_fused(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
-                               args_hom_[b], s, zin, last && acc ? acc->p[b] : nullptr,
-                               prm.fused_smoother, st);
+                               sargs[b], s, zin, last && acc ? acc->p[b] : nullptr, skind, st);
       prof_mark(st, nc, false, 2 * k);
     }
     if (overlap && (!last || want_out)) {

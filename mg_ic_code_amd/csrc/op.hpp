@@ -138,11 +138,16 @@ class VariableCoeffPoissonOperator {
   // partials (count `total`, per-box blocks) -> final -> allreduce -> host
   double finish_reduce(int kind, double *parts, int total, int slot);
   std::vector<BoxArgs> args_hom_, args_inhom_, args_plain_;
+  // AMR level > 0 with isolated patches: args_hom_ with the coarse-fine
+  // faces marked kBcCFHom, for the 3D-block fused sweep (cfFusedApplies)
+  std::vector<BoxArgs> args_cf_;
+  int cf_fused_ = -1;  // -1 undecided, 0 / 1
+  bool cfFusedApplies();
   std::unique_ptr<LevelData> jac_tmp_;
   std::unique_ptr<LevelData> sweep_tmp_;  // out-of-place buffer of the fused sweep
 
  public:
-  bool fusedSmootherApplies() const;
+  bool fusedSmootherApplies();
   // kernel arguments for other drivers (the mixed-precision V-cycle)
   const BoxArgs &boxArgs(int n, bool homogeneous) { return args(n, homogeneous); }
   StencilCoefs stencil() { return coefs(); }

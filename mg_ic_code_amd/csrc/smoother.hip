@@ -493,26 +493,20 @@ __device__ __forceinline__ void block_tile(T *__restrict__ R, T *__restrict__ B,
     R[c] = bsel(q, u1, u0);
     B[c] = bsel(q, u0, u1);
   }
-  // 2b. the domain BC, in LDS: each BC-face ghost of the region takes the
-  // image of the cell it touches -- the values ParseBC writes before the
-  // pass (same cells, including the extension onto exchanged faces' ghost
-  // layers), so the input is never written and the sweep is one launch.  Only tiles touching a BC face (a workgroup-uniform test) pay.
-  // (the region reaches the hi ghost at n once x0 + TX + 1 >= n)
-  if (!ZIN && ((g.bcm[0] && x0 == 0) || (g.bcm[1] && x0 + TX + 1 >= nx) || (g.bcm[2] && y0 == 0) ||
-               (g.bcm[3] && y0 + TY + 1 >= ny) || (g.bcm[4] && z0 == 0) ||
-               (g.bcm[5] && z0 + TZ + 1 >= nz))) {
-    __syncthreads();
-    const int n3[3] = {nx, ny, nz}, o3[3] = {x0 - 2, y0 - 2, z0 - 2};
-    constexpr int E3[3] = {TX + 4, TY + 4, TZ + 4};  // region extent per direction
-    auto lds = [&](int x, int y, int z) -> T * {  // the LDS slot of cell (x, y, z)
-      const int rx = x - o3[0];
-      const int idx = ((z - o3[2]) * F::LH + (y - o3[1])) * PW + (rx >> 1);
-      const int red = (rx & 1) == ((q0 + y + z) & 1);
-      return red ? &R[idx] : &B[idx];
-    };
+  // the ghosts of the region's BC faces (cf_only: the coarse-fine faces),
+  // from the LDS values
+  const int n3[3] = {nx, ny, nz}, o3[3] = {x0 - 2, y0 - 2, z0 - 2};
+  constexpr int E3[3] = {TX + 4, TY + 4, TZ + 4};  // region extent per direction
+  auto lds = [&](int x, int y, int z) -> T * {  // the LDS slot of cell (x, y, z)
+    const int rx = x - o3[0];
+    const int idx = ((z - o3[2]) * F::LH + (y - o3[1])) * PW + (rx >> 1);
+    const int red = (rx & 1) == ((q0 + y + z) & 1);
+    return red ? &R[idx] : &B[idx];
+  };
+  auto fill_ghosts = [&](bool cf_only) {
     for (int face = 0; face < 6; ++face) {
       const int mode = g.bcm[face];
-      if (!mode) continue;
+      if (!mode || (cf_only && mode != kBcCFHom)) continue;
       const int dir = face >> 1, side = face & 1;
       const int gc = side == 0 ? -1 : n3[dir];  // ghost coordinate along dir
       if (gc < o3[dir] || gc >= o3[dir] + E3[dir]) continue;  // face not in this region
@@ -529,9 +523,34 @@ __device__ __forceinline__ void block_tile(T *__restrict__ R, T *__restrict__ B,
         c[d1] = lo1 + t / w0;
         T *gp = lds(c[0], c[1], c[2]);
         c[dir] = side == 0 ? 0 : n3[dir] - 1;
-        *gp = ghost_of(mode, (T)g.bcc[face], *lds(c[0], c[1], c[2]));
+        const T f1 = *lds(c[0], c[1], c[2]);
+        if (mode == kBcCFHom) {  // k_cf_interp<true>: ps = 0, f1, f2 one / two cells in
+          c[dir] = side == 0 ? 1 : n3[dir] - 2;
+          const T f2 = *lds(c[0], c[1], c[2]);
+          *gp = ((T)(8.0 / 15.0) * (T)0 + (T)(2.0 / 3.0) * f1) + (T)(-0.2) * f2;
+        } else {
+          *gp = ghost_of(mode, (T)g.bcc[face], f1);
+        }
       }
     }
+  };
+  // does the region reach a coarse-fine face? (uniform)
+  bool cf_tile = false;
+  for (int face = 0; face < 6; ++face) {
+    const int gc = (face & 1) == 0 ? -1 : n3[face >> 1];
+    cf_tile = cf_tile || (g.bcm[face] == kBcCFHom && gc >= o3[face >> 1] &&
+                          gc < o3[face >> 1] + E3[face >> 1]);
+  }
+  // 2b. the domain BC, in LDS: each BC-face ghost of the region takes the
+  // image of the cell it touches -- the values ParseBC writes before the
+  // pass (same cells, including the extension onto exchanged faces' ghost
+  // layers), so the input is never written and the sweep is one launch.  Only tiles touching a BC face (a workgroup-uniform test) pay.
+  // (the region reaches the hi ghost at n once x0 + TX + 1 >= n)
+  if (!ZIN && ((g.bcm[0] && x0 == 0) || (g.bcm[1] && x0 + TX + 1 >= nx) || (g.bcm[2] && y0 == 0) ||
+               (g.bcm[3] && y0 + TY + 1 >= ny) || (g.bcm[4] && z0 == 0) ||
+               (g.bcm[5] && z0 + TZ + 1 >= nz))) {
+    __syncthreads();
+    fill_ghosts(false);
   }
   auto upd = [&](T uc, T xm, T xp, T ym, T yp, T zm, T zp,
                  T rv, T av, T bv) -> T {
@@ -563,6 +582,10 @@ __device__ __forceinline__ void block_tile(T *__restrict__ R, T *__restrict__ B,
                 bsel(q, cr[i][1], cr[i][0]), bsel(q, ca[i][1], ca[i][0]), bsel(q, cb[i][1], cb[i][0]));
   }
   __syncthreads();
+  if (cf_tile) {  // homogeneousCFInterp again before the black pass (.cpp:296): red cells moved
+    fill_ghosts(true);
+    __syncthreads();
+  }
   // 4. BLACK cells of the tile + store
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
