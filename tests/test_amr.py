@@ -20,11 +20,16 @@ def _shape(b):
     return (b[5] - b[2] + 1, b[4] - b[1] + 1, b[3] - b[0] + 1)
 
 
-def _data(rng, nlev, bvar=True):
+# patches touching domain faces (level 1: x lo, y hi; level 2: x lo, y hi):
+# their boxes mix domain-BC and coarse-fine faces
+BOXES_EDGE = [DOM0, (0, 16, 12, 47, 63, 45), (0, 40, 36, 73, 127, 77)]
+
+
+def _data(rng, nlev, bvar=True, boxes=BOXES):
     out = []
     for l in range(nlev):
-        s = _shape(BOXES[l])
-        out.append(dict(box=BOXES[l], a=rng.uniform(-2.0, -0.5, s),
+        s = _shape(boxes[l])
+        out.append(dict(box=boxes[l], a=rng.uniform(-2.0, -0.5, s),
                         b=rng.uniform(0.5, 2.0, s) if bvar else np.ones(s),
                         rhs=rng.uniform(-1, 1, s)))
     return out
@@ -145,6 +150,26 @@ def test_amr_vcycle_matches_oracle_bitwise(comm, bvar):
     for l in range(3):
         assert np.array_equal(_get(F[l]), o.phis[l][1:-1, 1:-1, 1:-1]), l
     assert g < 5e-2 * g0  # (random bCoef: about 0.34 per iteration for this seed)
+
+
+@pytest.mark.gpu
+def test_amr_vcycle_boundary_patches_bitwise(comm):
+    # patches on the domain boundary: the fused sweeps on those levels fold the
+    # domain BC and the coarse-fine ghost rule in the same tiles
+    rng = np.random.default_rng(6)
+    lv = _data(rng, 3, True, BOXES_EDGE)
+    amr, F = _gpu(comm, lv)
+    o = _oracle(lv)
+    phis = [o.L[l].full() for l in range(3)]
+    res = o.init_residual(phis, [x["rhs"] for x in lv])
+    assert amr.init_residual([f["phi"] for f in F], [f["rhs"] for f in F], 0) == \
+        max(np.abs(r).max() for r in res)
+    for _ in range(3):
+        g = amr.iteration([f["phi"] for f in F], [f["rhs"] for f in F], 0)
+        res = o.iteration()
+        assert g == max(np.abs(r).max() for r in res)
+    for l in range(3):
+        assert np.array_equal(_get(F[l]), o.phis[l][1:-1, 1:-1, 1:-1]), l
 
 
 @pytest.mark.gpu
