@@ -1829,10 +1829,19 @@ void gsrb_sweep_fused(double *u_out, double *u_in, const double *rhs, const doub
 void gsrb_sweep_fused_f(float *u_out, float *u_in, const float *rhs, const float *a,
                         const float *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                         double *acc, int kind, hipStream_t st) {
+  // fp32 streaming tiles: 128x32 with 1024 threads (95 KB LDS, four waves
+  // per SIMD): 4.03 ms per 1024^3 sweep against 4.31-4.39 for 128x16 / 512
+  // (MGIC_FUSED_F_VARIANT=1), 128x32 / 512 and 256x16 / 512 (4.45, 4.39)
+  static const int fv = [] {
+    const char *e = getenv("MGIC_FUSED_F_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
   if (kind == 3 || (kind != 2 && (long)g.nx * g.ny * g.nz <= block_max_cells()))
     launch_block<float, 32, 8, 4, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
-  else
+  else if (fv == 1)
     launch_fused6<float, 128, 16, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
+  else
+    launch_fused6<float, 128, 32, 1024>(u_out, u_in, rhs, a, b, g, s, zero_in, acc, st);
 }
 
 template <int TX, int TY, int NT>
