@@ -18,7 +18,10 @@ set_constant_K_integrand (:133-147).  Every field stays in HBM, and each step
 is a libmgic kernel.  With output_dir set, the reference's HDF5 files are
 written as it writes them: output_solver_data before every solve (:181) and
 output_final_data after the loop (:229), through libmgic_io (output.py).
-Not covered: AMR levels (max_level > 0).
+After the loop the reference stops with MayDay::Error when the final |dpsi|
+is above 1e-1 (:221-225), before output_final_data: `poisson_solve` raises
+NLDivergenceError at the same point, so a diverged solve writes no
+checkpoint.  Not covered: AMR levels (max_level > 0).
 """
 from __future__ import annotations
 
@@ -34,6 +37,20 @@ from .core import (AMRMultiGrid, BiCGStabSolver, Grid, LevelData, MultilevelLine
 from ._lib import call
 from .output import output_final_data, output_solver_data
 from .params import PoissonParameters
+
+
+# Main_PoissonSolver.cpp:221-225: "a fairly generous threshold"
+NL_DIVERGENCE_THRESHOLD = 1e-1
+
+
+class NLDivergenceError(RuntimeError):
+    """MayDay::Error("NL iterations did not converge - may need a better initial
+    guess") of Main_PoissonSolver.cpp:223-224.  Carries the loop's result."""
+
+    def __init__(self, result: "NLResult"):
+        super().__init__("NL iterations did not converge - may need a better initial guess "
+                         f"(final |dpsi| = {result.dpsi_norms[-1]!r})")
+        self.result = result
 
 
 @dataclass
@@ -107,7 +124,22 @@ def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
         if nrm < prm.tolerance or nrm > 1e5:
             res.converged = nrm < prm.tolerance
             break
+    write = None
     if output_dir is not None:  # :227-230
-        output_final_data([psi], bh, prm.max_level, [2], os.path.join(output_dir,
-                                                                      "vcPoissonFinal.3d.hdf5"))
+        def write():
+            output_final_data([psi], bh, prm.max_level, [2],
+                              os.path.join(output_dir, "vcPoissonFinal.3d.hdf5"))
+    return finish_nl_loop(res, write)
+
+
+def finish_nl_loop(res: NLResult, write_final=None) -> NLResult:
+    """The end of poissonSolve (Main_PoissonSolver.cpp:218-230): raise when the
+    final |dpsi| exceeds 1e-1 (MayDay::Error, :221-225) -- before anything is
+    written -- else write the final data (`write_final`, :229) and return.
+    The comparison is the reference's `dpsi_norm > 1e-1`, so a NaN norm passes
+    it as it does there."""
+    if res.dpsi_norms and res.dpsi_norms[-1] > NL_DIVERGENCE_THRESHOLD:
+        raise NLDivergenceError(res)
+    if write_final is not None:
+        write_final()
     return res

@@ -268,3 +268,24 @@ def test_nl_loop_writes_reference_files(tmp_path):
                            res.psi.download(0))
     np.testing.assert_allclose(data, o, rtol=1e-13, atol=1e-300)
     assert h5read.attr(f, "/max_level") == prm.max_level
+
+
+@pytest.mark.gpu
+def test_nl_loop_divergence_raises_and_writes_no_checkpoint(tmp_path):
+    # Main_PoissonSolver.cpp:221-225: MayDay::Error before output_final_data
+    # when the final |dpsi| > 1e-1.  Momenta of 50 make |dpsi| ~ 58 after the
+    # first NL step (test_nl_host.py pins that on the oracle loop).
+    import dataclasses
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.nl import NLDivergenceError, poisson_solve
+    from mg_ic_code_amd.params import read_params_file
+    prm = read_params_file(os.path.join(ROOT, "tests", "golden", "params.txt"))
+    prm = dataclasses.replace(prm, bh1_momentum=50.0, bh2_momentum=-50.0)
+    n = 16
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    grid = mg.Grid(mg.Comm(), dom, [dom], prm.domainLength[0] / n)
+    with pytest.raises(NLDivergenceError) as ei:
+        poisson_solve(grid, prm, max_depth=2, max_NL_iterations=1, output_dir=str(tmp_path))
+    assert ei.value.result.dpsi_norms[-1] > 1e-1
+    # the solver-data file before the solve is written (:181), the checkpoint is not
+    assert sorted(os.listdir(tmp_path)) == ["vcPoissonOut.3d_0.hdf5"]
