@@ -137,6 +137,31 @@ def test_mixed_vcycle_matches_fp32_oracle_bitwise(comm, fused, bvar, use_fmg):
 
 
 @pytest.mark.gpu
+def test_mixed_streaming_multi_tile_bitwise(comm):
+    # the fp32 streaming sweep's 128x32 tiles with several x and y tiles and
+    # several z chunks per column (264 x 72 x 40: 3 x 3 tiles, kc = 8 on 256
+    # resident workgroups), plus a ragged last tile in x and y -- the tile
+    # edges the 48x40x56 case above never reaches
+    import mg_ic_code_amd as mg
+    rng = np.random.default_rng(11)
+    shape = (264, 72, 40)
+    lo = (0, -8, 8)  # coarsenable by 8: three depths (MGnewOp stops otherwise)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    dx = 0.21
+    bc_lo, bc_hi, bcv = (0, 0, 1), (1, 0, 0), 0.5
+    a, b, rhs = _problem(rng, shape, False)
+    S = _gpu(comm, dom, [dom], dx, a, b, rhs, 3, 2, bc_lo, bc_hi, bcv)
+    mm = mg.MixedMultiGrid(S["fac"], S["sp"])
+    assert mm.num_depths == 3
+    m = MixedOracle(_oracle(dom, dx, a, b, rhs, 3, bc_lo, bc_hi, bcv), 1.0, -1.0, bc_lo, bc_hi)
+    assert mm.init_residual(S["fphi"], S["frhs"], S["fres"], 0) == \
+        np.abs(m.init_residual(np.zeros(shape[::-1]))).max()
+    for _ in range(2):
+        assert mm.iteration(S["fphi"], S["frhs"], S["fres"], 0) == np.abs(m.iteration()).max()
+    assert np.array_equal(_phi(S), m.phi)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rccl", [False, True])
 def test_mixed_multibox_matches_single_box(rccl):
     import mg_ic_code_amd as mg
