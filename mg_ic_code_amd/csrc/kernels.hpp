@@ -51,6 +51,17 @@ void gsrb_sweep_fused_restrict(double *u_out, double *u_in, const double *rhs, c
 void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const double *a,
                       const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
                       int depth, hipStream_t st);
+// Two consecutive red+black sweeps u_in -> u_out in one z-streaming launch
+// (temporal blocking, smoother_tb.hip): bit-identical to two
+// gsrb_sweep_fused calls; zero_in / acc as there.  Constant bCoef; domain
+// faces, or exchanged faces whose 4-deep ghost shell of u and rhs / aCoef is
+// filled.  _applies also keeps boxes the 3D-block kernel takes (kind 3, or
+// kind 1 at most gsrb_block_max_cells() cells) on that kernel.
+bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
+void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
+                    const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
+                    hipStream_t st);
+long gsrb_block_max_cells();
 // two red+black sweeps u_in -> u_out in one z-streaming launch (128x16
 // tiles, 6-plane LDS ring, coefficients carried in registers): boxes whose
 // six faces are domain faces, constant bCoef, above the block-kernel size

@@ -321,15 +321,14 @@ bool VariableCoeffPoissonOperator::fusedSmootherApplies() {
   return prm.fused_smoother != 0;
 }
 
-// MGIC_SWEEPS_PER_LAUNCH: 1 (default) one sweep per launch; 2 pairs sweeps
-// in the two-sweep kernel where it applies (bit-identical; measured the same
-// 0.886 ms per 512^3 sweep, slower at 256^3: both kernels are issue/latency
-// bound at two waves per SIMD, not HBM bound); 3 the older wide-ring
-// two-sweep kernel (measurement only)
+// MGIC_SWEEPS_PER_LAUNCH: 2 (default) pairs consecutive sweeps in the
+// temporally blocked kernel (smoother_tb.hip) where it applies; 1 one sweep
+// per launch; 3 / 4 the round-1 two-sweep kernels (wide ring / 128x16
+// rings recomputing lambda per update; measurement only)
 static int sweeps_per_launch() {
   static const int v = [] {
     const char *e = getenv("MGIC_SWEEPS_PER_LAUNCH");
-    return e ? std::max(1, std::min(3, atoi(e))) : 1;
+    return e ? std::max(1, std::min(4, atoi(e))) : 2;
   }();
   return v;
 }
@@ -471,10 +470,15 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
   // two sweeps per launch (temporal blocking) on boxes with only domain faces
-  bool two = !halo && !cfl && sweeps_per_launch() >= 2 && n >= 2;
+  const int spl = sweeps_per_launch();
+  bool two = !halo && !cfl && spl >= 2 && n >= 2;
   for (int b = 0; two && b < grid->nlocal(); ++b)
-    two = sweeps_per_launch() == 3 || kern::gsrb_sweep_fused2s_applies(args_hom_[b], s, prm.fused_smoother);
+    two = spl == 3 ||
+          (spl == 4 ? kern::gsrb_sweep_fused2s_applies(args_hom_[b], s, prm.fused_smoother)
+                    : kern::gsrb_sweep_tb2_applies(args_hom_[b], s, prm.fused_smoother));
   const int per = two ? 2 : 1;
+  // the new kernel takes the phi += e sweep too; the round-1 ones do not
+  const bool pair_acc = two && spl == 2;
   const bool want_out = halo && (flags & kHaloOut) && !acc;
   const bool overlap = halo && per == 1 && overlapApplies();
   const bool split = halo && per == 1 && !overlap && splitApplies();
@@ -495,8 +499,11 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     evM = grid->comm->event(0);
     evE = grid->comm->event(1);
   }
-  // the last sweep restricts too (single sweep kernel over every box)
-  bool restrict_last = rst != nullptr && !acc && !(zero_in && n == 1) && !halo;
+  // the last sweep restricts too (single sweep kernel over every box) when
+  // it is a single sweep: with pairs, a separate restriction is cheaper than
+  // splitting the last pair
+  bool restrict_last = rst != nullptr && !acc && !(zero_in && n == 1) && !halo &&
+                       !(pair_acc && n % 2 == 0);
   if (restrict_last) {
     const Grid &cg = *rst->grid;
     restrict_last = cg.nlocal() == grid->nlocal();
@@ -511,7 +518,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     // a pair, unless it would swallow a special last sweep (+ restriction,
     // phi += e)
     const int left = n - it;
-    const int k = per == 2 && (left >= 3 || (left == 2 && !restrict_last && !acc)) ? 2 : 1;
+    const int k = per == 2 && (left >= 3 || (left == 2 && !restrict_last && (!acc || pair_acc))) ? 2 : 1;
     const bool last = it + k == n;
     if (deep) {
       if (vd < 2) {
@@ -565,12 +572,15 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
       // sweep+restriction launch moves other bytes)
       const long nc = last && restrict_last ? 0 : grid->geom[b].valid.ncells();
       prof_mark(st, nc, true, 2 * k);
-      if (k == 2 && sweeps_per_launch() == 3)
+      if (k == 2 && spl == 3)
         kern::gsrb_sweep_fused2x(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
                                  args_hom_[b], s, zin, st);
-      else if (k == 2)  // two sweeps in one launch (temporal blocking)
+      else if (k == 2 && spl == 4)
         kern::gsrb_sweep_fused2s(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], args_hom_[b], s,
                                  zin, st);
+      else if (k == 2)  // two sweeps in one launch (temporal blocking), + phi += e
+        kern::gsrb_sweep_tb2(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], args_hom_[b], s, zin,
+                             last && acc ? acc->p[b] : nullptr, st);
       else if (last && restrict_last)  // + restrictResidual(rst, result, rhs)
         kern::gsrb_sweep_fused_restrict(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b],
                                         m_bCoef->p[b], args_hom_[b], s, rst->p[b],

@@ -40,33 +40,15 @@
 #include <cstdlib>
 
 #include "kernels.hpp"
+#include "sweep_util.hpp"
 
 namespace mgic {
 namespace kern {
 
 namespace {
 
-template <class T>
-__device__ __forceinline__ T ghost_of(int mode, T c, T near) {
-  return mode == kBcDirichlet ? (c - near) : (mode == kBcNeumannHom ? near : near + c);
-}
-
-// q ? x : y as an integer bit select: a "cond ? arr1[i] : arr0[i]" on
-// register arrays is otherwise turned into a select of two stack addresses
-// and lowered to scratch memory.  Exact (no arithmetic on the values).
-__device__ __forceinline__ double bsel(int q, double x, double y) {
-  // per 32-bit half, so each half is one v_bitop3 / v_bfi
-  const unsigned m = 0u - (unsigned)(q & 1);
-  const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
-  const unsigned long long yb = (unsigned long long)__double_as_longlong(y);
-  const unsigned lo = ((unsigned)xb & m) | ((unsigned)yb & ~m);
-  const unsigned hi = ((unsigned)(xb >> 32) & m) | ((unsigned)(yb >> 32) & ~m);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-__device__ __forceinline__ float bsel(int q, float x, float y) {
-  const unsigned m = 0u - (unsigned)(q & 1);
-  return __uint_as_float((__float_as_uint(x) & m) | (__float_as_uint(y) & ~m));
-}
+using sweep::bsel;
+using sweep::ghost_of;
 
 // element type traits: a lane pair is one 16-B (double) / 8-B (float) load
 template <class T> struct Vec2;
@@ -1792,6 +1774,8 @@ static long block_max_cells() {
   }();
   return v;
 }
+
+long gsrb_block_max_cells() { return block_max_cells(); }
 
 static int block_variant() {
   static int v = [] {

@@ -1,0 +1,651 @@
+// smoother_tb.hip -- two red+black GSRB sweeps per launch (temporal blocking)
+// for gfx950.
+//
+// Two consecutive levelGSRB calls (Source/VariableCoeffPoissonOperator.cpp:
+// 290-331; arithmetic of GSRBHELMHOLTZVC3D, VariableCoeffPoissonOperatorF.
+// ChF:56-139) on one box in one z-streaming launch, out of place (u_in ->
+// u_out), bit-identical to four per-colour passes (same expressions,
+// -ffp-contract=off).  Compulsory HBM traffic: u, rhs, aCoef read once and u
+// written once per TWO sweeps (16 B/cell/sweep) against 32 for the single
+// fused sweep.
+//
+// Pipeline.  A workgroup owns a TX x TY (x, y) tile and streams a chunk of
+// z planes through a 6-plane LDS ring (red and black element of every x pair
+// in separate arrays, so every LDS access is stride 1).  At step p it runs
+// four colour passes on four planes, each on the tile grown by the cells the
+// later passes read:
+//     sweep-1 red   plane p     tile + 3
+//     sweep-1 black plane p-1   tile + 2
+//     sweep-2 red   plane p-2   tile + 1
+//     sweep-2 black plane p-3   tile        -> stored
+// Every pass updates the ring array in place (red and black cells are
+// disjoint), so one copy of each plane suffices.
+//
+// What makes it cheaper per cell than the single sweep run twice:
+//   * a thread owns the same x pairs in all four passes, so each pair's
+//     coefficients are prepared ONCE per plane -- rhs, alpha*a and lambda =
+//     1/(alpha*a + 6 beta/dx^2) (.cpp:234-243, the one fp64 division) -- and
+//     carried in registers, split into the red and the black element, to the
+//     two passes that use them; the register sets rotate over a 4-step
+//     unrolled loop, so nothing is moved;
+//   * alpha = 1, beta = -1, bCoef = 1 (the reference's configuration,
+//     Main_PoissonSolver.cpp:40, set_b_coef) is a specialisation that drops
+//     three multiplications by exact constants (x*1 = x, x - (-1*y) = x + y
+//     in IEEE arithmetic): 15 fp64 operations per cell update;
+//   * the domain BC costs nothing in the passes of interior tiles: ghosts
+//     enter the ring as ParseBC's images of the loaded cells, and since a
+//     ghost is only ever read by the cell it images, a face cell's update
+//     re-images its own ghosts (the value ParseBC writes before the next
+//     colour pass); only tiles that reach an x / y domain face run that code.
+// Exchanged faces (kBcMemory) read a 4-deep ghost shell of u and rhs/aCoef
+// (the deep-halo exchange): the rings run onto the shell up to depth 3 and
+// produce there exactly the neighbours' own values, as in the deep-halo
+// schedule of op.cpp.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <type_traits>
+
+#include "kernels.hpp"
+#include "sweep_util.hpp"
+
+namespace mgic {
+namespace kern {
+
+namespace {
+
+using sweep::bsel;
+
+template <int N>
+using IC = std::integral_constant<int, N>;
+
+// in-kernel time stamps for tools/tb2_probe.hip (diagnostic builds only)
+#ifndef TB2_STAMP
+#define TB2_STAMP(id, p) ((void)0)
+#endif
+// diagnostic builds of tools/tb2_probe.hip only: bit 0 skips the global
+// loads, bit 1 the colour passes, bit 2 the stores (wrong results, timing)
+#ifndef TB2_PROBE_SKIP
+#define TB2_PROBE_SKIP 0
+#endif
+
+// Geometry.  Rows of the LDS ring are SHIFTED pairings: in row y of plane k
+// pair m holds cells (X, X+1) with X = x0 - 6 + 2m + s, s = (x0 + y + k +
+// sum(glo)) & 1, so the first element of every pair is RED ((i+j+k) even,
+// GSRBHELMHOLTZVC3D's redBlack = 0) and the second BLACK.  No lane ever
+// selects between its elements by colour: red values live in R, black ones
+// in B, loaded and stored as 16-B pairs (8-B aligned in odd rows).  With the
+// shift the neighbours are at fixed pair offsets:
+//     red  (m):  x-1, x+1 = B[m-1], B[m];  y+-1, z+-1 = B[m-1+s] of that row / plane
+//     black(m):  x-1, x+1 = R[m], R[m+1];  y+-1, z+-1 = R[m+s]
+// (a neighbouring row or plane has the opposite shift).
+template <int TX, int TY, int NT>
+struct TB2 {
+  static_assert(TX % 2 == 0, "TX must be even");
+  static constexpr int PW = TX / 2 + 5;            // pairs per LDS row: X = x0-6+s .. x0+TX+2+s
+  static constexpr int LH = TY + 8;                // LDS rows y0-4 .. y0+TY+3
+  static constexpr int CP = PW * LH;               // pairs per plane
+  static constexpr int SS = CP + 2 * PW + 2;       // slot stride: + a scratch row
+  static constexpr int PAD = CP + PW + 1;          // write target of elements never updated
+  static constexpr int NS = 8;                     // ring slots (planes p+1 .. p-5 live)
+  static constexpr int UW = PW - 1;                // update pairs per row: m = 1 .. PW-1
+  static constexpr int NRP = UW * (TY + 6);        // update pairs: rows y0-3 .. y0+TY+2
+  static constexpr int NL = (CP + NT - 1) / NT;
+  static constexpr int NP = (NRP + NT - 1) / NT;
+  static constexpr int LDS_BYTES = 2 * NS * SS * 8;
+};
+
+// a ParseBC ghost as one add: ghost_of(mode, c, v) == (sign ^ v) + gc
+// exactly (c - v == c + (-v); v + (-0.0) == v for every v, signed zeros
+// included), with sign/gc per domain face
+// (built on the host, one per face, so the kernel holds no BC-mode logic)
+struct TB2Ghosts {
+  double c[6];
+  unsigned sgn[6];  // 0x80000000: negate v (Dirichlet)
+};
+TB2Ghosts make_ghosts(const BoxArgs &g) {
+  TB2Ghosts r{};
+  for (int f = 0; f < 6; ++f) {
+    const int mode = g.bcm[f];
+    r.sgn[f] = mode == kBcDirichlet ? 0x80000000u : 0u;
+    r.c[f] = mode == kBcNeumannHom ? -0.0 : g.bcc[f];
+  }
+  return r;
+}
+__device__ __forceinline__ double ghost(const TB2Ghosts &gg, int f, double v) {
+  const long long b = __double_as_longlong(v) ^ ((long long)gg.sgn[f] << 32);
+  return __longlong_as_double(b) + gg.c[f];
+}
+
+// One tile (x0, y0) of the box, planes [z0, z1).  FAST: alpha == 1, beta ==
+// -1, bval == 1 (exact specialisation, see above); EDGE: the tile's rings
+// reach an x / y domain face (BC code compiled in).
+template <int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE>
+__device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restrict__ B,
+                                         double *__restrict__ uo, double *__restrict__ acc,
+                                         const double *__restrict__ ui,
+                                         const double *__restrict__ rhs,
+                                         const double *__restrict__ a, const BoxArgs &g,
+                                         const StencilCoefs &s, const TB2Ghosts &gg, int x0,
+                                         int y0, int z0, int z1) {
+  using F = TB2<TX, TY, NT>;
+  static_assert(F::NP == 1, "one update pair per thread");
+  constexpr int PW = F::PW, CP = F::CP, SS = F::SS, UW = F::UW, NRP = F::NRP, NL = F::NL;
+  const int nx = g.nx, ny = g.ny, nz = g.nz;
+  const int tid = threadIdx.x;
+  const long sy = g.sy, sz = g.sz;
+  // the tile clipped to the box: ring levels are distances from it
+  const int tx1 = min(x0 + TX, nx) - 1, ty1 = min(y0 + TY, ny) - 1;
+  // updatable cells per direction: inside the box at a domain face; up to
+  // depth 3 into the (4-deep) ghost shell at an exchanged face
+  const int uxlo = g.bcm[0] ? 0 : -3, uxhi = g.bcm[1] ? nx - 1 : nx + 2;
+  const int uylo = g.bcm[2] ? 0 : -3, uyhi = g.bcm[3] ? ny - 1 : ny + 2;
+  const bool zdl = g.bcm[4] != 0, zdh = g.bcm[5] != 0;
+  const int pstart = z0 - 3, pend = z1 + 3;
+  // the shift s of a lane's row at plane pstart + t is (gsum + y + t) & 1
+  const int gsum = g.glo[0] + g.glo[1] + g.glo[2] + x0 + pstart;
+  // in-plane offsets are BYTE offsets from the plane's allocated corner
+  // (x = -16, y = -4): non-negative 32-bit values, so every global access is
+  // a uniform 64-bit plane base + a 32-bit lane offset
+  const long corner = -16 - 4 * sy;
+  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+  auto plane = [&](const double *f, int p) {  // corner of (clamped) plane p
+    return reinterpret_cast<const char *>(f + corner + (long)clampi(p, -4, nz + 3) * sz);
+  };
+  // the lane offset is laundered per access: otherwise the compiler hoists
+  // "array + lane offset" out of the z loop as 64-bit per-lane pointers (two
+  // VGPRs each, for every array and offset variant) instead of using the
+  // uniform plane base + 32-bit offset form
+  auto at2 = [](const char *base, unsigned off) {
+    asm volatile("" : "+v"(off));
+    return *reinterpret_cast<const double2 *>(base + off);
+  };
+  auto boff = [&](int x, int y) {  // byte offset of cell (x, y) from the corner
+    return (unsigned)(8 * (16 + x + (long)(y + 4) * sy));
+  };
+
+  // ---- loads of u (slot c = LDS pair index), per plane parity t ----------
+  // A pair holding a ghost of an x / y domain face loads the cells the ghost
+  // images and transforms them (image(); lbc bits per t: 0-2 x rule, 3-4 y
+  // rule), so every ghost enters the ring as the value ParseBC writes before
+  // the first colour pass (SetBCs.cpp:49-131)
+  unsigned loff[2][NL];
+  int lbc[NL], ldst[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int c = tid + i * NT;
+    const int r = c / PW, m = c - r * PW;
+    const int gy = y0 - 4 + r;
+    ldst[i] = c < CP ? c : F::PAD;
+    int bits = 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int X = x0 - 6 + 2 * m + ((gsum + gy + t) & 1);
+      int gx = clampi(X, -6, nx + 3), bx = 0, ly = clampi(gy, -4, ny + 3), by = 0;
+      if (g.bcm[0] && X == -1) {  // (-1, 0): element 0 <- image of element 1
+        bx = 1;
+      } else if (g.bcm[0] && X == -2) {  // (-2, -1) <- image of 0: load (0, 1)
+        gx = 0;
+        bx = 2;
+      } else if (g.bcm[1] && X == nx - 1) {  // (nx-1, nx): element 1 <- image of element 0
+        bx = 3;
+      } else if (g.bcm[1] && X == nx) {  // (nx, nx+1) <- image of nx-1: load (nx-2, nx-1)
+        gx = nx - 2;
+        bx = 4;
+      }
+      if (g.bcm[2] && gy == -1) {
+        ly = 0;
+        by = 1;
+      } else if (g.bcm[3] && gy == ny) {
+        ly = ny - 1;
+        by = 2;
+      }
+      loff[t][i] = c < CP ? boff(gx, ly) : 0u;
+      bits |= (c < CP ? bx | (by << 3) : 0) << (5 * t);
+    }
+    lbc[i] = bits;
+  }
+  // ---- the update pair: c -> row rr (y0-3+rr), pair m = 1 + c % UW --------
+  // per parity t: roff (global byte offset of the pair), yzo (LDS index
+  // offset of the red element's y / z neighbours: s - 1; the black one's is
+  // s), wra (LDS write index of the red element, low 16 bits, and the black
+  // one: the pair, or PAD for an element never updated -- ring level > 3 or
+  // outside the updatable cells; an element updated at ring W keeps a value
+  // no later pass reads once W falls below its level, so no pass needs a
+  // select), rinf (bits 0-3 / 4-7: domain faces the red / black element
+  // borders; 8-9: store mask of the red / black element)
+  unsigned roff[2], wra[2];
+  int yzo[2], rinf[2];
+  const int c0 = tid;
+  const int rr = c0 / UW, m0 = 1 + c0 - rr * UW;
+  const int gyr = y0 - 3 + rr;
+  const bool row_ok = c0 < NRP;
+  const int ci = row_ok ? (rr + 1) * PW + m0 : F::PAD;
+  {
+    const int dy = gyr < y0 ? y0 - gyr : (gyr > ty1 ? gyr - ty1 : 0);
+    const bool yok = row_ok && gyr >= uylo && gyr <= uyhi;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int sh = (gsum + gyr + t) & 1;
+      const int X = x0 - 6 + 2 * m0 + sh;
+      roff[t] = row_ok ? boff(clampi(X, -6, nx + 3), clampi(gyr, -4, ny + 3)) : 0u;
+      yzo[t] = sh - 1;
+      int bits = 0;
+      unsigned w = 0;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int gx = X + e;
+        const int dx = gx < x0 ? x0 - gx : (gx > tx1 ? gx - tx1 : 0);
+        const bool upd_ok = yok && gx >= uxlo && gx <= uxhi && max(dx, dy) <= 3;
+        w |= (unsigned)(upd_ok ? ci : F::PAD) << (16 * e);
+        const int f = ((g.bcm[0] && gx == 0) ? 1 : 0) | ((g.bcm[1] && gx == nx - 1) ? 2 : 0) |
+                      ((g.bcm[2] && gyr == 0) ? 4 : 0) | ((g.bcm[3] && gyr == ny - 1) ? 8 : 0);
+        bits |= (upd_ok ? f : 0) << (4 * e);
+        const bool st = row_ok && gyr >= y0 && gyr <= ty1 && gx >= x0 && gx <= tx1;
+        bits |= (st ? 1 : 0) << (8 + e);
+      }
+      rinf[t] = bits;
+      wra[t] = w;
+    }
+  }
+  // z extent of each pass: the chunk grown by the pass's ring width,
+  // clipped to the box at a domain face
+  auto klo = [&](int w) { return zdl ? max(z0 - w, 0) : z0 - w; };
+  auto khi = [&](int w) { return zdh ? min(z1 - 1 + w, nz - 1) : z1 - 1 + w; };
+
+  double pu0[NL], pu1[NL];           // u pairs of plane p+2 in flight
+  double nr0, nr1, na0, na1;         // rhs / aCoef pair of plane p+1 in flight
+  // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
+  // when the plane's pair arrives, last used by sweep-2 red three steps
+  // later), black of planes p-1 .. p-4 (made one step later from rb / ab);
+  // moved down one plane at the end of every step
+  double R0r, R0a, R0l, R1r, R1a, R1l, R2r, R2a, R2l, R3r, R3a, R3l;
+  double B0r, B0a, B0l, B1r, B1a, B1l, B2r, B2a, B2l, B3r, B3a, B3l;
+  double rb = 0.0, ab = 0.0;
+  double ac0 = 0.0, ac1 = 0.0, an0 = 0.0, an1 = 0.0;  // ACC: acc pair of planes p-4 / p-3
+  R0r = R0a = R0l = R1r = R1a = R1l = R2r = R2a = R2l = R3r = R3a = R3l = 0.0;
+  B0r = B0a = B0l = B1r = B1a = B1l = B2r = B2a = B2l = B3r = B3a = B3l = 0.0;
+
+  // CHK = false: a step of the steady range (below), where every pass is
+  // active, no pass or load touches a z face plane and every plane is inside
+  // the allocation -- no checks, unclamped plane pointers from pz = p * sz
+  auto planec = [&](const double *f, bool chk, int p, long pz) {
+    return chk ? plane(f, p) : reinterpret_cast<const char *>(f + corner + pz);
+  };
+  auto fetch_u = [&](int t, bool chk, int p, long pz) {
+    // a z ghost plane of a domain face loads the plane it images
+    const char *pl = chk ? plane(ui, (zdl && p == -1) ? 0 : (zdh && p == nz) ? nz - 1 : p)
+                         : planec(ui, false, p, pz);
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      if (ZIN || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
+        pu0[i] = 0.0;
+        pu1[i] = 0.0;
+      } else {
+        const double2 v = at2(pl, loff[t][i]);
+        pu0[i] = v.x;
+        pu1[i] = v.y;
+      }
+    }
+  };
+  // ghost pairs of the fetched plane p -> ParseBC's images (ghosts of two
+  // faces, never read, get garbage)
+  auto image = [&](int t, bool chk, int p) {
+    if (EDGE) {
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int bits = lbc[i] >> (5 * t), bx = bits & 7, by = (bits >> 3) & 3;
+        if (!(bx | by)) continue;
+        double u0 = pu0[i], u1 = pu1[i];
+        if (by) {
+          const int yf = by == 1 ? 2 : 3;
+          u0 = ghost(gg, yf, u0);
+          u1 = ghost(gg, yf, u1);
+        }
+        if (bx == 1) u0 = ghost(gg, 0, u1);
+        else if (bx == 2) u1 = ghost(gg, 0, u0);
+        else if (bx == 3) u1 = ghost(gg, 1, u0);
+        else if (bx == 4) u0 = ghost(gg, 1, u1);
+        pu0[i] = u0;
+        pu1[i] = u1;
+      }
+    }
+    if (chk && ((zdl && p == -1) || (zdh && p == nz))) {
+      const int zf = p == -1 ? 4 : 5;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        pu0[i] = ghost(gg, zf, pu0[i]);
+        pu1[i] = ghost(gg, zf, pu1[i]);
+      }
+    }
+  };
+  auto put = [&](int sl) {  // into ring slot sl: red element -> R, black -> B
+    double *Rs = R + sl * SS, *Bs = B + sl * SS;
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      Rs[ldst[i]] = pu0[i];
+      Bs[ldst[i]] = pu1[i];
+    }
+  };
+  auto fetch_c = [&](int t, bool chk, int p, long pz) {
+    if (TB2_PROBE_SKIP & 1) {
+      nr0 = 0.5;
+      nr1 = 0.25;
+      na0 = -1.5;
+      na1 = -1.25;
+      return;
+    }
+    const double2 vr = at2(planec(rhs, chk, p, pz), roff[t]);
+    const double2 va = at2(planec(a, chk, p, pz), roff[t]);
+    nr0 = vr.x;
+    nr1 = vr.y;
+    na0 = va.x;
+    na1 = va.y;
+  };
+  auto lam = [&](double aa) { return 1.0 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
+  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
+                 double rv, double aa, double lm) -> double {
+    const double tx = (xp + xm) - 2.0 * uc;
+    const double ty = (yp + ym) - 2.0 * uc;
+    const double tz = (zp + zm) - 2.0 * uc;
+    const double lap = (tx + ty) + tz;  // .ChF:111-120
+    double lofdpsi = aa * uc;           // .ChF:107-108
+    if (FAST) {
+      lofdpsi = lofdpsi + lap * s.dxinv;  // .ChF:122-124 with bCoef 1, beta -1
+    } else {
+      const double ldpsi = lap * s.dxinv * s.bval;  // .ChF:122
+      lofdpsi = lofdpsi - s.beta * ldpsi;           // .ChF:124
+    }
+    return uc - lm * (lofdpsi - rv);  // .ChF:127-128
+  };
+  // One colour pass on plane k (ring slot sl, parity t) over the ring of
+  // width W, split into its LDS reads (gather), update chain and writes
+  // (scatter), so that a phase runs two passes' reads, then their chains,
+  // then their writes: the compiler cannot move one update's LDS accesses
+  // across another's.  A ghost is read only by the cell it images, so a face
+  // cell's update rewrites its ghosts (in the other colour's array, at
+  // positions no pass updates) with the image of its new value: what ParseBC
+  // writes before the next colour pass that reads them.
+  struct Pass {
+    bool on, chk;
+    int sl, t, k;
+    double uc, xm, xp, ym, yp, zm, zp, v;
+  };
+  auto gather = [&](Pass &P, bool red, int W, int sl, int t, bool chk, int k) {
+    P.on = (!chk || (k >= klo(W) && k <= khi(W))) && !(TB2_PROBE_SKIP & 2);  // uniform
+    P.sl = sl;
+    P.t = t;
+    P.k = k;
+    P.chk = chk;
+    if (!P.on) return;
+    const double *X = (red ? R : B) + sl * SS;
+    const double *N = (red ? B : R) + sl * SS;
+    const double *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
+    const double *Np = (red ? B : R) + ((sl + 1) & 7) * SS;
+    const int o = yzo[t] + (red ? 0 : 1);  // y / z neighbours: pair m-1+s (red), m+s (black)
+    P.uc = X[ci];
+    P.xm = N[ci - (red ? 1 : 0)];
+    P.xp = N[ci + (red ? 0 : 1)];
+    P.ym = N[ci + o - PW];
+    P.yp = N[ci + o + PW];
+    P.zm = Nm[ci + o];
+    P.zp = Np[ci + o];
+  };
+  auto scatter = [&](Pass &P, bool red) {
+    if (!P.on) return;
+    const int sl = P.sl, t = P.t;
+    double *X = (red ? R : B) + sl * SS;
+    const unsigned w = red ? (wra[t] & 0xffffu) : (wra[t] >> 16);
+    X[w] = P.v;
+    if (EDGE) {
+      const int f = (rinf[t] >> (red ? 0 : 4)) & 15;
+      if (f) {
+        double *N = (red ? B : R) + sl * SS;
+        const int o = yzo[t] + (red ? 0 : 1);
+        if (f & 1) N[ci - (red ? 1 : 0)] = ghost(gg, 0, P.v);
+        if (f & 2) N[ci + (red ? 0 : 1)] = ghost(gg, 1, P.v);
+        if (f & 4) N[ci + o - PW] = ghost(gg, 2, P.v);
+        if (f & 8) N[ci + o + PW] = ghost(gg, 3, P.v);
+      }
+    }
+    const bool zl = P.chk && zdl && P.k == 0, zh = P.chk && zdh && P.k == nz - 1;
+    if (zl || zh) {  // z ghosts of the face plane (every lane: an element
+                     // never updated owns its ghost alone)
+      double *Nz = (red ? B : R) + ((zl ? sl + 7 : sl + 1) & 7) * SS;
+      const int zf = zl ? 4 : 5;
+      Nz[ci + yzo[t] + (red ? 0 : 1)] = ghost(gg, zf, P.v);
+    }
+  };
+  // plane k's tile cells -> u_out (or acc += them), from ring slot sl
+  auto store = [&](int sl, int t, bool chk, int k, long kz) {
+    if ((chk && (k < z0 || k >= z1)) || (TB2_PROBE_SKIP & 4)) return;
+    const int st = (rinf[t] >> 8) & 3;
+    if (!st) return;
+    double2 w;
+    w.x = R[sl * SS + ci];
+    w.y = B[sl * SS + ci];
+    if (ACC) {  // phi += e (incr, scale 1) in the same pass
+      w.x = ac0 + w.x;
+      w.y = ac1 + w.y;
+    }
+    unsigned off = roff[t];
+    asm volatile("" : "+v"(off));
+    char *d = reinterpret_cast<char *>((ACC ? acc : uo) + corner + (chk ? (long)k * sz : kz)) + off;
+    if (st == 3) *reinterpret_cast<double2 *>(d) = w;
+    else if (st == 1) *reinterpret_cast<double *>(d) = w.x;
+    else *reinterpret_cast<double *>(d + 8) = w.y;
+  };
+  // One pipeline step at plane p (t: its parity relative to pstart; slot
+  // sl = p & 7), two barriers:
+  //   phase A: sweep-1 red of plane p (ring 3), sweep-2 red of plane p-3 (ring 1)
+  //   phase B: sweep-1 black of plane p-1 (ring 2), sweep-2 black of plane
+  //            p-4 (the tile) + its store
+  // The two passes of a phase touch disjoint planes; phase A reads black
+  // cells only, phase B red ones.  Live ring planes p+1 .. p-5; plane p+1 is
+  // written over plane p-7.
+  auto step = [&](auto tc, auto cc, int p, long pz) {
+    constexpr int T = decltype(tc)::value, U = T ^ 1;  // parity of p, of p +- 1
+    constexpr bool CHK = decltype(cc)::value != 0;
+    asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
+    const int sl = p & 7;
+    TB2_STAMP(0, p);
+    // coefficient sets: black of plane p-1 from the raw black element, red
+    // of plane p from its pair fetched last step (alpha * a, .ChF:107)
+    B0r = rb;
+    B0a = FAST ? ab : s.alpha * ab;
+    B0l = lam(B0a);
+    R0r = nr0;
+    R0a = FAST ? na0 : s.alpha * na0;
+    R0l = lam(R0a);
+    rb = nr1;
+    ab = na1;
+    image(U, CHK, p + 1);
+    put((sl + 1) & 7);
+    fetch_c(U, CHK, p + 1, pz + sz);
+    if (ACC) {
+      ac0 = an0;
+      ac1 = an1;
+      const double2 v = at2(planec(acc, CHK, p - 3, pz - 3 * sz), roff[U]);
+      an0 = v.x;
+      an1 = v.y;
+    }
+    fetch_u(T, CHK, p + 2, pz + 2 * sz);
+    TB2_STAMP(1, p);
+    __syncthreads();
+    TB2_STAMP(2, p);
+    {
+      Pass A;
+      gather(A, true, 3, sl, T, CHK, p);
+      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, R0r, R0a, R0l);
+      scatter(A, true);
+      gather(A, true, 1, (sl + 5) & 7, U, CHK, p - 3);
+      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, R3r, R3a, R3l);
+      scatter(A, true);
+    }
+    TB2_STAMP(3, p);
+    __syncthreads();
+    TB2_STAMP(4, p);
+    {
+      Pass A;
+      gather(A, false, 2, (sl + 7) & 7, U, CHK, p - 1);
+      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, B0r, B0a, B0l);
+      scatter(A, false);
+      gather(A, false, 0, (sl + 4) & 7, T, CHK, p - 4);
+      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, B3r, B3a, B3l);
+      scatter(A, false);
+    }
+    TB2_STAMP(5, p);
+    store((sl + 4) & 7, T, CHK, p - 4, pz - 4 * sz);
+    TB2_STAMP(6, p);
+    // every set moves down one plane
+    R3r = R2r; R3a = R2a; R3l = R2l;
+    R2r = R1r; R2a = R1a; R2l = R1l;
+    R1r = R0r; R1a = R0a; R1l = R0l;
+    B3r = B2r; B3a = B2a; B3l = B2l;
+    B2r = B1r; B2a = B1a; B2l = B1l;
+    B1r = B0r; B1a = B0a; B1l = B0l;
+  };
+
+  fetch_u(1, true, pstart - 1, 0);
+  image(1, true, pstart - 1);
+  put((pstart - 1) & 7);
+  fetch_u(0, true, pstart, 0);
+  image(0, true, pstart);
+  put(pstart & 7);
+  fetch_u(1, true, pstart + 1, 0);
+  fetch_c(0, true, pstart, 0);
+  // the steady range [pA, pB]: every pass active, no pass touching a z face
+  // plane (k = 0 .. 4 at a lower, k >= nz - 4 at an upper domain face) and
+  // every load and the store inside the allocation / the chunk
+  int pA = max(max(klo(3), klo(2) + 1), max(klo(1) + 3, klo(0) + 4));
+  pA = max(max(pA, z0 + 4), zdl ? 5 : -1);
+  int pB = min(min(khi(3), khi(2) + 1), min(khi(1) + 3, khi(0) + 4));
+  pB = min(min(pB, z1 + 3), zdh ? nz - 3 : nz + 1);
+  int p = pstart;
+  for (; p <= pend; p += 2) {
+    step(IC<0>{}, IC<1>{}, p, 0);
+    step(IC<1>{}, IC<1>{}, p + 1, 0);
+  }
+}
+
+template <int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST>
+__global__ __launch_bounds__(NT) void k_gsrb_tb2(double *__restrict__ uo,
+                                                 double *__restrict__ acc,
+                                                 const double *__restrict__ ui,
+                                                 const double *__restrict__ rhs,
+                                                 const double *__restrict__ a,
+                                                 const BoxArgs g, const StencilCoefs s,
+                                                 const TB2Ghosts gg, int kc, int ntx, int nty,
+                                                 int nblocks) {
+  using F = TB2<TX, TY, NT>;
+  __shared__ double R[F::NS * F::SS];  // red element of every pair, 8 plane slots
+  __shared__ double B[F::NS * F::SS];  // black element
+  const int L = sweep::xcd_tile(blockIdx.x, nblocks);
+  const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
+  const int z0 = (L / (ntx * nty)) * kc;
+  const int z1 = min(z0 + kc, g.nz);
+  // uniform: do the tile's rings (3 cells) reach an x / y domain face?
+  const bool edge = (g.bcm[0] && x0 <= 3) || (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx) ||
+                    (g.bcm[2] && y0 <= 3) || (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny);
+  if (edge)
+    tb2_tile<TX, TY, NT, ZIN, ACC, FAST, true>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
+                                               z1);
+  else
+    tb2_tile<TX, TY, NT, ZIN, ACC, FAST, false>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
+                                                z1);
+}
+
+template <int TX, int TY, int NT>
+int tb2_resident_slots() {
+  static const int slots = [] {
+    int dev = 0, ncu = 0, per = 0;
+    MGIC_HIP(hipGetDevice(&dev));
+    MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    MGIC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per, k_gsrb_tb2<TX, TY, NT, false, false, true>, NT, 0));
+    return (per > 0 ? per : 1) * (ncu > 0 ? ncu : 1);
+  }();
+  return slots;
+}
+
+// z chunk per workgroup: minimise rounds(kc) * (kc + pipeline fill), the
+// fill being 7 steps rounded up with the chunk to the 2-step unroll
+int tb2_choose_kc(int tiles, int nz, int slots) {
+  int best = nz;
+  double best_cost = 1e300;
+  for (int kc = nz; kc >= 8; --kc) {
+    const long nb = (long)tiles * ((nz + kc - 1) / kc);
+    const long rounds = (nb + slots - 1) / slots;
+    const double cost = (double)rounds * (double)(((kc + 7 + 1) / 2) * 2);
+    if (cost < best_cost * 0.999) {
+      best_cost = cost;
+      best = kc;
+    }
+  }
+  return best;
+}
+
+template <int TX, int TY, int NT>
+void launch_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
+                const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
+                hipStream_t st) {
+  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
+  static const int kc_env = [] {
+    const char *e = getenv("MGIC_TB2_KC");
+    return e ? atoi(e) : 0;
+  }();
+  int kc = kc_env >= 8 ? (kc_env < g.nz ? kc_env : g.nz)
+                       : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<TX, TY, NT>());
+  const int ntz = (g.nz + kc - 1) / kc;
+  const int nblocks = ntx * nty * ntz;
+  const dim3 grid((unsigned)nblocks), block(NT);
+  const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0;
+  const TB2Ghosts gg = make_ghosts(g);
+#define MGIC_TB2(Z, A, FA)                                                                     \
+  k_gsrb_tb2<TX, TY, NT, Z, A, FA><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, g, s, gg, \
+                                                           kc, ntx, nty, nblocks)
+  if (acc) {
+    if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
+    if (fast) MGIC_TB2(false, true, true);
+    else MGIC_TB2(false, true, false);
+  } else if (zero_in) {
+    if (fast) MGIC_TB2(true, false, true);
+    else MGIC_TB2(true, false, false);
+  } else {
+    if (fast) MGIC_TB2(false, false, true);
+    else MGIC_TB2(false, false, false);
+  }
+#undef MGIC_TB2
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(kHipErr, std::string("two-sweep launch: ") + hipGetErrorString(e));
+}
+
+}  // namespace
+
+bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
+  if (!s.bconst || kind == 0 || kind == 3) return false;
+  if (kind == 1 && (long)g.nx * g.ny * g.nz <= gsrb_block_max_cells()) return false;
+  for (int f = 0; f < 6; ++f)  // the CF ghost rule of AMR levels is not folded here
+    if (g.bcm[f] == kBcCFHom) return false;
+  // a 4-deep shell must exist on every exchanged face; tiny boxes go to the
+  // 3D-block kernel
+  return g.nx >= 8 && g.ny >= 8 && g.nz >= 8;
+}
+
+// tile shape (MGIC_TB2_VARIANT, measurement): a thread owns one x pair of
+// the update region ((TX/2 + 4) x (TY + 6) pairs <= NT) and carries its
+// coefficient sets in registers; 1024 threads = four waves per SIMD at 128
+// VGPRs.  0: 64 x 22 (1008 pairs, 148 KB LDS), 1: 64 x 16 (792 pairs)
+void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
+                    const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
+                    hipStream_t st) {
+  static const int v = [] {
+    const char *e = getenv("MGIC_TB2_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  if (v == 1) launch_tb2<64, 16, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+  else launch_tb2<64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+}
+
+}  // namespace kern
+}  // namespace mgic

@@ -501,6 +501,52 @@ def test_fused_sweep_matches_oracle_and_passes(comm, rng, shape, lo, nsweeps):
     assert np.array_equal(outs[0], o.get(0, oracle.PHI, 0))
 
 
+@pytest.mark.parametrize("shape,lo", [((70, 20, 13), (0, 0, 0)), ((37, 9, 40), (3, -5, 7)),
+                                      ((130, 47, 45), (-64, 1, 1)), ((64, 44, 24), (0, 0, 0))])
+@pytest.mark.parametrize("nsweeps", [2, 3, 4, 5])
+@pytest.mark.parametrize("coefs", [(1.0, -1.0, 1.0), (0.75, -1.3, 1.7)])
+def test_two_sweep_relax_matches_oracle(comm, rng, shape, lo, nsweeps, coefs):
+    # the temporally blocked two-sweep kernel (smoother_tb.hip: constant
+    # bCoef, fused_smoother=2 forces the streaming path) in relax(): pairs of
+    # sweeps plus a single one for odd counts, against the oracle and the
+    # per-colour passes bit for bit.  Ragged tiles (64 x 22) in x and y,
+    # several z chunks, odd global offsets (colour parity), mixed
+    # inhomogeneous Dirichlet / Neumann faces; alpha = 1, beta = -1, b = 1 is
+    # the kernel's exact specialisation, the other triple the general path.
+    alpha, beta, bval = coefs
+    nx, ny, nz = shape
+    dom = (lo[0], lo[1], lo[2], lo[0] + nx - 1, lo[1] + ny - 1, lo[2] + nz - 1)
+    dx = 0.7
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    b = np.full((nz, ny, nx), bval)
+    rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    u0 = rng.uniform(-1, 1, (nz, ny, nx))
+    bc_lo, bc_hi = (0, 1, 1), (1, 0, 0)
+    outs = []
+    for fused in (2, 0):
+        grid = mg.Grid(comm, dom, [dom], dx)
+        fa, fb, fr, fu = (mg.LevelData(grid) for _ in range(4))
+        fa.upload(0, a)
+        fb.upload(0, b)
+        fr.upload(0, rhs)
+        fu.upload(0, u0)
+        prm = mg.OperatorParams(alpha=alpha, beta=beta, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=0.5,
+                                fused_smoother=fused)
+        op = mg.defineOperatorFactory(grid, fa, fb, prm).AMRnewOp()
+        op.relax(fu, fr, nsweeps)
+        outs.append(fu.download(0))
+    assert np.array_equal(outs[0], outs[1])
+    o = oracle.OracleMG([dom], dom, dx, alpha=alpha, beta=beta, bc_lo=bc_lo, bc_hi=bc_hi,
+                        bc_value=0.5, nlevels=1)
+    o.set(0, oracle.ACOEF, 0, a)
+    o.set(0, oracle.BCOEF, 0, b)
+    o.set(0, oracle.RHS, 0, rhs)
+    o.set(0, oracle.PHI, 0, u0)
+    o.setup()
+    o.relax(0, oracle.PHI, oracle.RHS, nsweeps)
+    assert np.array_equal(outs[0], o.get(0, oracle.PHI, 0))
+
+
 # ------------------------------------------------- outer solve
 @pytest.mark.parametrize("parts", [(1, 1, 1), (2, 1, 2)])
 def test_mg_preconditioner_bitwise(comm, rng, parts):
@@ -660,15 +706,17 @@ print("two-sweep OK")
 """
 
 
-def test_two_sweep_kernel_vcycle_bitwise():
-    # the temporally blocked two-sweep kernel (MGIC_SWEEPS_PER_LAUNCH=2, read
-    # once per process: a child process), odd and even sweep counts, ragged
-    # mixed-BC box and a cube, against the oracle bit for bit
+@pytest.mark.parametrize("spl", ["4", "2"])
+def test_two_sweep_kernel_vcycle_bitwise(spl):
+    # the two-sweep kernels (MGIC_SWEEPS_PER_LAUNCH, read once per process: a
+    # child process): 4 = round 1's 128x16 kernel, 2 = smoother_tb.hip (the
+    # default); odd and even sweep counts, ragged mixed-BC box and a cube,
+    # against the oracle bit for bit
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MGIC_SWEEPS_PER_LAUNCH="2")
+    env = dict(os.environ, MGIC_SWEEPS_PER_LAUNCH=spl)
     r = subprocess.run([sys.executable, "-c", _TWO_SWEEPS_CHILD, root], env=env,
                        capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -676,7 +724,7 @@ def test_two_sweep_kernel_vcycle_bitwise():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_post", [1, 3])
+@pytest.mark.parametrize("n_post", [1, 2, 3, 4])
 @pytest.mark.parametrize("bvar", [False, True])
 def test_streaming_vcycle_post_sweeps_bitwise(rng, comm, n_post, bvar):
     # z-streaming kernels at every level, an odd number of post-smoothing

@@ -1,0 +1,103 @@
+// tb2_probe.hip -- diagnostic harness for the two-sweep kernel
+// (smoother_tb.hip): launches k_gsrb_tb2 directly on an n^3 box and reports
+// its time by HIP events and, with -DSTAMPS, s_memtime stamps taken by wave 0
+// of a few workgroups at fixed points of each pipeline step (per-phase cycle
+// breakdown).  Not part of the library; built by tools/build_probe.sh.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#ifdef STAMPS
+__device__ unsigned long long g_stamps[4][64][12];
+__device__ int g_probe_blocks[4];
+#define TB2_STAMP(id, p)                                                              \
+  do {                                                                                \
+    if (threadIdx.x == 0) {                                                           \
+      for (int w_ = 0; w_ < 4; ++w_)                                                  \
+        if ((int)blockIdx.x == g_probe_blocks[w_] && (p) >= z0 + 40 && (p) < z0 + 104) \
+          g_stamps[w_][(p) - z0 - 40][id] = __builtin_amdgcn_s_memtime();             \
+    }                                                                                 \
+  } while (0)
+#endif
+
+#include "../mg_ic_code_amd/csrc/smoother_tb.hip"
+
+using namespace mgic;
+
+int main(int argc, char **argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 512;
+  const int zin = argc > 2 ? atoi(argv[2]) : 0;
+  FabGeom geo = FabGeom::make(Box{{0, 0, 0}, {n - 1, n - 1, n - 1}});
+  BoxArgs g{};
+  g.nx = g.ny = g.nz = n;
+  g.sy = geo.sy;
+  g.sz = geo.sz;
+  for (int f = 0; f < 6; ++f) {
+    g.bcm[f] = kBcDirichlet;
+    g.bcc[f] = 0.0;
+  }
+  StencilCoefs s{};
+  s.alpha = 1.0;
+  s.beta = -1.0;
+  s.dx = 100.0 / n;
+  s.dxinv = 1.0 / (s.dx * s.dx);
+  s.lamshift = (2 * 3) * s.beta / (s.dx * s.dx);
+  s.bconst = 1;
+  s.bval = 1.0;
+  std::vector<double *> f(4);
+  std::vector<double> h(geo.total);
+  for (int k = 0; k < 4; ++k) {
+    MGIC_HIP(hipMalloc(&f[k], geo.total * sizeof(double)));
+    for (long i = 0; i < geo.total; ++i)
+      h[i] = k == 2 ? -1.0 - 0.5 * ((i * 2654435761u) % 1000) / 1000.0
+                    : ((i * 40503u + k) % 2001) / 1000.0 - 1.0;
+    MGIC_HIP(hipMemcpy(f[k], h.data(), geo.total * sizeof(double), hipMemcpyHostToDevice));
+  }
+  double *u_in = f[0] + geo.origin, *rhs = f[1] + geo.origin, *a = f[2] + geo.origin,
+         *u_out = f[3] + geo.origin;
+#ifdef STAMPS
+  int blocks[4] = {0, 37, 300, 600};
+  MGIC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_probe_blocks), blocks, sizeof(blocks)));
+#endif
+  hipEvent_t e0, e1;
+  MGIC_HIP(hipEventCreate(&e0));
+  MGIC_HIP(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w)
+    kern::gsrb_sweep_tb2(u_out, u_in, rhs, a, g, s, zin, nullptr, nullptr);
+  const int reps = 10;
+  MGIC_HIP(hipEventRecord(e0, nullptr));
+  for (int r = 0; r < reps; ++r)
+    kern::gsrb_sweep_tb2(u_out, u_in, rhs, a, g, s, zin, nullptr, nullptr);
+  MGIC_HIP(hipEventRecord(e1, nullptr));
+  MGIC_HIP(hipEventSynchronize(e1));
+  float ms = 0;
+  MGIC_HIP(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  const double cells = (double)n * n * n;
+  printf("{\"n\": %d, \"zin\": %d, \"ms_per_launch\": %.4f, \"compulsory_GBps\": %.1f}\n", n, zin,
+         ms, (zin ? 24.0 : 32.0) * cells / (ms * 1e-3) / 1e9);
+#ifdef STAMPS
+  static unsigned long long st[4][64][12];
+  MGIC_HIP(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
+  for (int w = 0; w < 4; ++w) {
+    double acc[12] = {0};
+    int cnt = 0;
+    for (int p = 0; p < 63; ++p) {
+      if (!st[w][p][0] || !st[w][p + 1][0]) continue;
+      for (int i = 0; i < 11; ++i) acc[i] += (double)(st[w][p][i + 1] - st[w][p][i]);
+      acc[11] += (double)(st[w][p + 1][0] - st[w][p][11]);
+      ++cnt;
+    }
+    printf("block %d: %d steps; memtime ticks per step by phase:", blocks[w], cnt);
+    double tot = 0;
+    for (int i = 0; i < 12; ++i) {
+      printf(" %.0f", cnt ? acc[i] / cnt : 0.0);
+      tot += cnt ? acc[i] / cnt : 0.0;
+    }
+    printf("  total %.0f\n", tot);
+  }
+#endif
+  return 0;
+}
