@@ -129,8 +129,8 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
                                          const StencilCoefs &s, const TB2Ghosts &gg, int x0,
                                          int y0, int z0, int z1) {
   using F = TB2<TX, TY, NT>;
-  static_assert(F::NP == 1, "one update pair per thread");
-  constexpr int PW = F::PW, CP = F::CP, SS = F::SS, UW = F::UW, NRP = F::NRP, NL = F::NL;
+  constexpr int PW = F::PW, CP = F::CP, SS = F::SS, UW = F::UW, NRP = F::NRP, NL = F::NL,
+                NP = F::NP;
   const int nx = g.nx, ny = g.ny, nz = g.nz;
   const int tid = threadIdx.x;
   const long sy = g.sy, sz = g.sz;
@@ -170,13 +170,12 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // rule), so every ghost enters the ring as the value ParseBC writes before
   // the first colour pass (SetBCs.cpp:49-131)
   unsigned loff[2][NL];
-  int lbc[NL], ldst[NL];
+  int lbc[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int c = tid + i * NT;
     const int r = c / PW, m = c - r * PW;
     const int gy = y0 - 4 + r;
-    ldst[i] = c < CP ? c : F::PAD;
     int bits = 0;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -205,47 +204,52 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     }
     lbc[i] = bits;
   }
-  // ---- the update pair: c -> row rr (y0-3+rr), pair m = 1 + c % UW --------
-  // per parity t: roff (global byte offset of the pair), yzo (LDS index
-  // offset of the red element's y / z neighbours: s - 1; the black one's is
-  // s), wra (LDS write index of the red element, low 16 bits, and the black
-  // one: the pair, or PAD for an element never updated -- ring level > 3 or
-  // outside the updatable cells; an element updated at ring W keeps a value
-  // no later pass reads once W falls below its level, so no pass needs a
-  // select), rinf (bits 0-3 / 4-7: domain faces the red / black element
-  // borders; 8-9: store mask of the red / black element)
-  unsigned roff[2], wra[2];
-  int yzo[2], rinf[2];
-  const int c0 = tid;
-  const int rr = c0 / UW, m0 = 1 + c0 - rr * UW;
-  const int gyr = y0 - 3 + rr;
-  const bool row_ok = c0 < NRP;
-  const int ci = row_ok ? (rr + 1) * PW + m0 : F::PAD;
-  {
-    const int dy = gyr < y0 ? y0 - gyr : (gyr > ty1 ? gyr - ty1 : 0);
-    const bool yok = row_ok && gyr >= uylo && gyr <= uyhi;
+  // ---- update pairs: c = tid + i * NT -> row rr (y0-3+rr), pair m ---------
+  // Lanes 32q .. 32q+31 take pairs 1..32 of row q (one row per 32-lane LDS
+  // bank group: conflict-free reads); the rows' last UW-32 pairs go to the
+  // lanes after them.  Per parity t: roff (global byte offset of the pair),
+  // yzo (LDS index offset of the red element's y / z neighbours: s - 1; the
+  // black one's is s), rinf (bits 0-3 / 4-7: domain faces the red / black
+  // element borders; 8-9: store mask of the red / black element; 10-11: the
+  // red / black element is ever updated -- ring level <= 3 and an updatable
+  // cell).  A pass writes every lane's new value except for elements never
+  // updated, which keep theirs: an element updated at ring W holds a value no
+  // later pass reads once W falls below its level, so no pass needs the ring
+  // test.
+  static_assert(UW >= 32, "a row must fill a 32-lane group");
+  constexpr int NR = TY + 6, MAIN = 32 * NR;
+  unsigned roff[2][NP];
+  int yzo[2][NP], rinf[2][NP], ci[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int c = tid + i * NT, jt = c - MAIN;
+    const int rr = c < MAIN ? c >> 5 : jt / (UW - 32);
+    const int m = c < MAIN ? 1 + (c & 31) : 33 + jt - (jt / (UW - 32)) * (UW - 32);
+    const int gy = y0 - 3 + rr;
+    const bool row_ok = c < NRP;
+    ci[i] = row_ok ? (rr + 1) * PW + m : F::PAD;
+    const int dy = gy < y0 ? y0 - gy : (gy > ty1 ? gy - ty1 : 0);
+    const bool yok = row_ok && gy >= uylo && gy <= uyhi;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int sh = (gsum + gyr + t) & 1;
-      const int X = x0 - 6 + 2 * m0 + sh;
-      roff[t] = row_ok ? boff(clampi(X, -6, nx + 3), clampi(gyr, -4, ny + 3)) : 0u;
-      yzo[t] = sh - 1;
+      const int sh = (gsum + gy + t) & 1;
+      const int X = x0 - 6 + 2 * m + sh;
+      roff[t][i] = row_ok ? boff(clampi(X, -6, nx + 3), clampi(gy, -4, ny + 3)) : 0u;
+      yzo[t][i] = sh - 1;
       int bits = 0;
-      unsigned w = 0;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int gx = X + e;
         const int dx = gx < x0 ? x0 - gx : (gx > tx1 ? gx - tx1 : 0);
         const bool upd_ok = yok && gx >= uxlo && gx <= uxhi && max(dx, dy) <= 3;
-        w |= (unsigned)(upd_ok ? ci : F::PAD) << (16 * e);
+        bits |= (upd_ok ? 1 : 0) << (10 + e);
         const int f = ((g.bcm[0] && gx == 0) ? 1 : 0) | ((g.bcm[1] && gx == nx - 1) ? 2 : 0) |
-                      ((g.bcm[2] && gyr == 0) ? 4 : 0) | ((g.bcm[3] && gyr == ny - 1) ? 8 : 0);
+                      ((g.bcm[2] && gy == 0) ? 4 : 0) | ((g.bcm[3] && gy == ny - 1) ? 8 : 0);
         bits |= (upd_ok ? f : 0) << (4 * e);
-        const bool st = row_ok && gyr >= y0 && gyr <= ty1 && gx >= x0 && gx <= tx1;
+        const bool st = row_ok && gy >= y0 && gy <= ty1 && gx >= x0 && gx <= tx1;
         bits |= (st ? 1 : 0) << (8 + e);
       }
-      rinf[t] = bits;
-      wra[t] = w;
+      rinf[t][i] = bits;
     }
   }
   // z extent of each pass: the chunk grown by the pass's ring width,
@@ -253,35 +257,31 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   auto klo = [&](int w) { return zdl ? max(z0 - w, 0) : z0 - w; };
   auto khi = [&](int w) { return zdh ? min(z1 - 1 + w, nz - 1) : z1 - 1 + w; };
 
-  double pu0[NL], pu1[NL];           // u pairs of plane p+2 in flight
-  double nr0, nr1, na0, na1;         // rhs / aCoef pair of plane p+1 in flight
+  double pu0[NL], pu1[NL];                    // u pairs of plane p+2 in flight
+  double nr0[NP], nr1[NP], na0[NP], na1[NP];  // rhs / aCoef pairs of plane p+1 in flight
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
   // later), black of planes p-1 .. p-4 (made one step later from rb / ab);
   // moved down one plane at the end of every step
-  double R0r, R0a, R0l, R1r, R1a, R1l, R2r, R2a, R2l, R3r, R3a, R3l;
-  double B0r, B0a, B0l, B1r, B1a, B1l, B2r, B2a, B2l, B3r, B3a, B3l;
-  double rb = 0.0, ab = 0.0;
-  double ac0 = 0.0, ac1 = 0.0, an0 = 0.0, an1 = 0.0;  // ACC: acc pair of planes p-4 / p-3
-  R0r = R0a = R0l = R1r = R1a = R1l = R2r = R2a = R2l = R3r = R3a = R3l = 0.0;
-  B0r = B0a = B0l = B1r = B1a = B1l = B2r = B2a = B2l = B3r = B3a = B3l = 0.0;
+  double Rr[4][NP], Ra[4][NP], Rl[4][NP], Br[4][NP], Ba[4][NP], Bl[4][NP];
+  double rb[NP], ab[NP];
+  double ac0[NP], ac1[NP], an0[NP], an1[NP];  // ACC: acc pairs of planes p-4 / p-3
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    rb[i] = ab[i] = ac0[i] = ac1[i] = an0[i] = an1[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Rr[j][i] = Ra[j][i] = Rl[j][i] = Br[j][i] = Ba[j][i] = Bl[j][i] = 0.0;
+  }
 
-  // CHK = false: a step of the steady range (below), where every pass is
-  // active, no pass or load touches a z face plane and every plane is inside
-  // the allocation -- no checks, unclamped plane pointers from pz = p * sz
-  auto planec = [&](const double *f, bool chk, int p, long pz) {
-    return chk ? plane(f, p) : reinterpret_cast<const char *>(f + corner + pz);
-  };
-  auto fetch_u = [&](int t, bool chk, int p, long pz) {
+  auto fetch_u = [&](int t, int p) {
     // a z ghost plane of a domain face loads the plane it images
-    const char *pl = chk ? plane(ui, (zdl && p == -1) ? 0 : (zdh && p == nz) ? nz - 1 : p)
-                         : planec(ui, false, p, pz);
+    const char *pl = plane(ui, (zdl && p == -1) ? 0 : (zdh && p == nz) ? nz - 1 : p);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (ZIN || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
         pu0[i] = 0.0;
         pu1[i] = 0.0;
-      } else {
+      } else if (NL * NT <= CP || tid + i * NT < CP) {  // (whole waves past the plane skip)
         const double2 v = at2(pl, loff[t][i]);
         pu0[i] = v.x;
         pu1[i] = v.y;
@@ -290,7 +290,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   };
   // ghost pairs of the fetched plane p -> ParseBC's images (ghosts of two
   // faces, never read, get garbage)
-  auto image = [&](int t, bool chk, int p) {
+  auto image = [&](int t, int p) {
     if (EDGE) {
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
@@ -310,7 +310,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
         pu1[i] = u1;
       }
     }
-    if (chk && ((zdl && p == -1) || (zdh && p == nz))) {
+    if ((zdl && p == -1) || (zdh && p == nz)) {
       const int zf = p == -1 ? 4 : 5;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
@@ -323,24 +323,29 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     double *Rs = R + sl * SS, *Bs = B + sl * SS;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      Rs[ldst[i]] = pu0[i];
-      Bs[ldst[i]] = pu1[i];
+      if (NL * NT > CP && tid + i * NT >= CP) continue;  // whole waves past the plane
+      Rs[tid + i * NT] = pu0[i];
+      Bs[tid + i * NT] = pu1[i];
     }
   };
-  auto fetch_c = [&](int t, bool chk, int p, long pz) {
-    if (TB2_PROBE_SKIP & 1) {
-      nr0 = 0.5;
-      nr1 = 0.25;
-      na0 = -1.5;
-      na1 = -1.25;
-      return;
+  auto fetch_c = [&](int t, int p) {
+    const char *pr = plane(rhs, p), *pa = plane(a, p);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      if (TB2_PROBE_SKIP & 1) {
+        nr0[i] = 0.5;
+        nr1[i] = 0.25;
+        na0[i] = -1.5;
+        na1[i] = -1.25;
+        continue;
+      }
+      const double2 vr = at2(pr, roff[t][i]);
+      const double2 va = at2(pa, roff[t][i]);
+      nr0[i] = vr.x;
+      nr1[i] = vr.y;
+      na0[i] = va.x;
+      na1[i] = va.y;
     }
-    const double2 vr = at2(planec(rhs, chk, p, pz), roff[t]);
-    const double2 va = at2(planec(a, chk, p, pz), roff[t]);
-    nr0 = vr.x;
-    nr1 = vr.y;
-    na0 = va.x;
-    na1 = va.y;
   };
   auto lam = [&](double aa) { return 1.0 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
   auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
@@ -358,82 +363,81 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     }
     return uc - lm * (lofdpsi - rv);  // .ChF:127-128
   };
-  // One colour pass on plane k (ring slot sl, parity t) over the ring of
-  // width W, split into its LDS reads (gather), update chain and writes
-  // (scatter), so that a phase runs two passes' reads, then their chains,
-  // then their writes: the compiler cannot move one update's LDS accesses
-  // across another's.  A ghost is read only by the cell it images, so a face
+  // One colour pass on plane k (ring slot sl, parity t, coefficient set j)
+  // over the ring of width W: every pair's LDS reads, then the update chains,
+  // then the writes (the compiler cannot move one update's LDS accesses across
+  // another's).  A ghost is read only by the cell it images, so a face
   // cell's update rewrites its ghosts (in the other colour's array, at
   // positions no pass updates) with the image of its new value: what ParseBC
   // writes before the next colour pass that reads them.
-  struct Pass {
-    bool on, chk;
-    int sl, t, k;
-    double uc, xm, xp, ym, yp, zm, zp, v;
-  };
-  auto gather = [&](Pass &P, bool red, int W, int sl, int t, bool chk, int k) {
-    P.on = (!chk || (k >= klo(W) && k <= khi(W))) && !(TB2_PROBE_SKIP & 2);  // uniform
-    P.sl = sl;
-    P.t = t;
-    P.k = k;
-    P.chk = chk;
-    if (!P.on) return;
-    const double *X = (red ? R : B) + sl * SS;
-    const double *N = (red ? B : R) + sl * SS;
-    const double *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
-    const double *Np = (red ? B : R) + ((sl + 1) & 7) * SS;
-    const int o = yzo[t] + (red ? 0 : 1);  // y / z neighbours: pair m-1+s (red), m+s (black)
-    P.uc = X[ci];
-    P.xm = N[ci - (red ? 1 : 0)];
-    P.xp = N[ci + (red ? 0 : 1)];
-    P.ym = N[ci + o - PW];
-    P.yp = N[ci + o + PW];
-    P.zm = Nm[ci + o];
-    P.zp = Np[ci + o];
-  };
-  auto scatter = [&](Pass &P, bool red) {
-    if (!P.on) return;
-    const int sl = P.sl, t = P.t;
+  auto pass = [&](bool red, int W, int sl, int t, int k, const double (&cr)[NP],
+                  const double (&ca)[NP], const double (&cl)[NP]) {
+    if (k < klo(W) || k > khi(W) || (TB2_PROBE_SKIP & 2)) return;  // uniform
     double *X = (red ? R : B) + sl * SS;
-    const unsigned w = red ? (wra[t] & 0xffffu) : (wra[t] >> 16);
-    X[w] = P.v;
+    double *N = (red ? B : R) + sl * SS;
+    double *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
+    double *Np = (red ? B : R) + ((sl + 1) & 7) * SS;
+    double uc[NP], xm[NP], xp[NP], ym[NP], yp[NP], zm[NP], zp[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int c = ci[i];
+      const int o = yzo[t][i] + (red ? 0 : 1);  // y / z neighbours: pair m-1+s (red), m+s (black)
+      uc[i] = X[c];
+      xm[i] = N[c - (red ? 1 : 0)];
+      xp[i] = N[c + (red ? 0 : 1)];
+      ym[i] = N[c + o - PW];
+      yp[i] = N[c + o + PW];
+      zm[i] = Nm[c + o];
+      zp[i] = Np[c + o];
+    }
+    double v[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) v[i] = upd(uc[i], xm[i], xp[i], ym[i], yp[i], zm[i], zp[i], cr[i], ca[i], cl[i]);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> (red ? 10 : 11)) & 1 ? v[i] : uc[i];
     if (EDGE) {
-      const int f = (rinf[t] >> (red ? 0 : 4)) & 15;
-      if (f) {
-        double *N = (red ? B : R) + sl * SS;
-        const int o = yzo[t] + (red ? 0 : 1);
-        if (f & 1) N[ci - (red ? 1 : 0)] = ghost(gg, 0, P.v);
-        if (f & 2) N[ci + (red ? 0 : 1)] = ghost(gg, 1, P.v);
-        if (f & 4) N[ci + o - PW] = ghost(gg, 2, P.v);
-        if (f & 8) N[ci + o + PW] = ghost(gg, 3, P.v);
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int f = (rinf[t][i] >> (red ? 0 : 4)) & 15;
+        if (!f) continue;
+        const int c = ci[i], o = yzo[t][i] + (red ? 0 : 1);
+        if (f & 1) N[c - (red ? 1 : 0)] = ghost(gg, 0, v[i]);
+        if (f & 2) N[c + (red ? 0 : 1)] = ghost(gg, 1, v[i]);
+        if (f & 4) N[c + o - PW] = ghost(gg, 2, v[i]);
+        if (f & 8) N[c + o + PW] = ghost(gg, 3, v[i]);
       }
     }
-    const bool zl = P.chk && zdl && P.k == 0, zh = P.chk && zdh && P.k == nz - 1;
+    const bool zl = zdl && k == 0, zh = zdh && k == nz - 1;
     if (zl || zh) {  // z ghosts of the face plane (every lane: an element
                      // never updated owns its ghost alone)
-      double *Nz = (red ? B : R) + ((zl ? sl + 7 : sl + 1) & 7) * SS;
+      double *Nz = zl ? Nm : Np;
       const int zf = zl ? 4 : 5;
-      Nz[ci + yzo[t] + (red ? 0 : 1)] = ghost(gg, zf, P.v);
+#pragma unroll
+      for (int i = 0; i < NP; ++i) Nz[ci[i] + yzo[t][i] + (red ? 0 : 1)] = ghost(gg, zf, v[i]);
     }
   };
   // plane k's tile cells -> u_out (or acc += them), from ring slot sl
-  auto store = [&](int sl, int t, bool chk, int k, long kz) {
-    if ((chk && (k < z0 || k >= z1)) || (TB2_PROBE_SKIP & 4)) return;
-    const int st = (rinf[t] >> 8) & 3;
-    if (!st) return;
-    double2 w;
-    w.x = R[sl * SS + ci];
-    w.y = B[sl * SS + ci];
-    if (ACC) {  // phi += e (incr, scale 1) in the same pass
-      w.x = ac0 + w.x;
-      w.y = ac1 + w.y;
+  auto store = [&](int sl, int t, int k) {
+    if (k < z0 || k >= z1 || (TB2_PROBE_SKIP & 4)) return;
+    char *dst = reinterpret_cast<char *>((ACC ? acc : uo) + corner + (long)k * sz);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int st = (rinf[t][i] >> 8) & 3;
+      if (!st) continue;
+      double2 w;
+      w.x = R[sl * SS + ci[i]];
+      w.y = B[sl * SS + ci[i]];
+      if (ACC) {  // phi += e (incr, scale 1) in the same pass
+        w.x = ac0[i] + w.x;
+        w.y = ac1[i] + w.y;
+      }
+      unsigned off = roff[t][i];
+      asm volatile("" : "+v"(off));
+      char *d = dst + off;
+      if (st == 3) *reinterpret_cast<double2 *>(d) = w;
+      else if (st == 1) *reinterpret_cast<double *>(d) = w.x;
+      else *reinterpret_cast<double *>(d + 8) = w.y;
     }
-    unsigned off = roff[t];
-    asm volatile("" : "+v"(off));
-    char *d = reinterpret_cast<char *>((ACC ? acc : uo) + corner + (chk ? (long)k * sz : kz)) + off;
-    if (st == 3) *reinterpret_cast<double2 *>(d) = w;
-    else if (st == 1) *reinterpret_cast<double *>(d) = w.x;
-    else *reinterpret_cast<double *>(d + 8) = w.y;
   };
   // One pipeline step at plane p (t: its parity relative to pstart; slot
   // sl = p & 7), two barriers:
@@ -443,90 +447,81 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // The two passes of a phase touch disjoint planes; phase A reads black
   // cells only, phase B red ones.  Live ring planes p+1 .. p-5; plane p+1 is
   // written over plane p-7.
-  auto step = [&](auto tc, auto cc, int p, long pz) {
+  auto step = [&](auto tc, int p) {
     constexpr int T = decltype(tc)::value, U = T ^ 1;  // parity of p, of p +- 1
-    constexpr bool CHK = decltype(cc)::value != 0;
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
     const int sl = p & 7;
     TB2_STAMP(0, p);
     // coefficient sets: black of plane p-1 from the raw black element, red
     // of plane p from its pair fetched last step (alpha * a, .ChF:107)
-    B0r = rb;
-    B0a = FAST ? ab : s.alpha * ab;
-    B0l = lam(B0a);
-    R0r = nr0;
-    R0a = FAST ? na0 : s.alpha * na0;
-    R0l = lam(R0a);
-    rb = nr1;
-    ab = na1;
-    image(U, CHK, p + 1);
-    put((sl + 1) & 7);
-    fetch_c(U, CHK, p + 1, pz + sz);
-    if (ACC) {
-      ac0 = an0;
-      ac1 = an1;
-      const double2 v = at2(planec(acc, CHK, p - 3, pz - 3 * sz), roff[U]);
-      an0 = v.x;
-      an1 = v.y;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      Br[0][i] = rb[i];
+      Ba[0][i] = FAST ? ab[i] : s.alpha * ab[i];
+      Bl[0][i] = lam(Ba[0][i]);
+      Rr[0][i] = nr0[i];
+      Ra[0][i] = FAST ? na0[i] : s.alpha * na0[i];
+      Rl[0][i] = lam(Ra[0][i]);
+      rb[i] = nr1[i];
+      ab[i] = na1[i];
     }
-    fetch_u(T, CHK, p + 2, pz + 2 * sz);
+    image(U, p + 1);
+    put((sl + 1) & 7);
+    fetch_c(U, p + 1);
+    if (ACC) {
+      const char *pl = plane(acc, p - 3);
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        ac0[i] = an0[i];
+        ac1[i] = an1[i];
+        const double2 v = at2(pl, roff[U][i]);
+        an0[i] = v.x;
+        an1[i] = v.y;
+      }
+    }
+    fetch_u(T, p + 2);
     TB2_STAMP(1, p);
     __syncthreads();
     TB2_STAMP(2, p);
-    {
-      Pass A;
-      gather(A, true, 3, sl, T, CHK, p);
-      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, R0r, R0a, R0l);
-      scatter(A, true);
-      gather(A, true, 1, (sl + 5) & 7, U, CHK, p - 3);
-      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, R3r, R3a, R3l);
-      scatter(A, true);
-    }
+    pass(true, 3, sl, T, p, Rr[0], Ra[0], Rl[0]);
+    pass(true, 1, (sl + 5) & 7, U, p - 3, Rr[3], Ra[3], Rl[3]);
     TB2_STAMP(3, p);
     __syncthreads();
     TB2_STAMP(4, p);
-    {
-      Pass A;
-      gather(A, false, 2, (sl + 7) & 7, U, CHK, p - 1);
-      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, B0r, B0a, B0l);
-      scatter(A, false);
-      gather(A, false, 0, (sl + 4) & 7, T, CHK, p - 4);
-      if (A.on) A.v = upd(A.uc, A.xm, A.xp, A.ym, A.yp, A.zm, A.zp, B3r, B3a, B3l);
-      scatter(A, false);
-    }
+    pass(false, 2, (sl + 7) & 7, U, p - 1, Br[0], Ba[0], Bl[0]);
+    pass(false, 0, (sl + 4) & 7, T, p - 4, Br[3], Ba[3], Bl[3]);
     TB2_STAMP(5, p);
-    store((sl + 4) & 7, T, CHK, p - 4, pz - 4 * sz);
+    store((sl + 4) & 7, T, p - 4);
     TB2_STAMP(6, p);
     // every set moves down one plane
-    R3r = R2r; R3a = R2a; R3l = R2l;
-    R2r = R1r; R2a = R1a; R2l = R1l;
-    R1r = R0r; R1a = R0a; R1l = R0l;
-    B3r = B2r; B3a = B2a; B3l = B2l;
-    B2r = B1r; B2a = B1a; B2l = B1l;
-    B1r = B0r; B1a = B0a; B1l = B0l;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+#pragma unroll
+      for (int j = 3; j > 0; --j) {
+        Rr[j][i] = Rr[j - 1][i];
+        Ra[j][i] = Ra[j - 1][i];
+        Rl[j][i] = Rl[j - 1][i];
+        Br[j][i] = Br[j - 1][i];
+        Ba[j][i] = Ba[j - 1][i];
+        Bl[j][i] = Bl[j - 1][i];
+      }
+    }
   };
 
-  fetch_u(1, true, pstart - 1, 0);
-  image(1, true, pstart - 1);
+  fetch_u(1, pstart - 1);
+  image(1, pstart - 1);
   put((pstart - 1) & 7);
-  fetch_u(0, true, pstart, 0);
-  image(0, true, pstart);
+  fetch_u(0, pstart);
+  image(0, pstart);
   put(pstart & 7);
-  fetch_u(1, true, pstart + 1, 0);
-  fetch_c(0, true, pstart, 0);
-  // the steady range [pA, pB]: every pass active, no pass touching a z face
-  // plane (k = 0 .. 4 at a lower, k >= nz - 4 at an upper domain face) and
-  // every load and the store inside the allocation / the chunk
-  int pA = max(max(klo(3), klo(2) + 1), max(klo(1) + 3, klo(0) + 4));
-  pA = max(max(pA, z0 + 4), zdl ? 5 : -1);
-  int pB = min(min(khi(3), khi(2) + 1), min(khi(1) + 3, khi(0) + 4));
-  pB = min(min(pB, z1 + 3), zdh ? nz - 3 : nz + 1);
-  int p = pstart;
-  for (; p <= pend; p += 2) {
-    step(IC<0>{}, IC<1>{}, p, 0);
-    step(IC<1>{}, IC<1>{}, p + 1, 0);
+  fetch_u(1, pstart + 1);
+  fetch_c(0, pstart);
+  for (int p = pstart; p <= pend; p += 2) {
+    step(IC<0>{}, p);
+    step(IC<1>{}, p + 1);
   }
 }
+
 
 template <int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST>
 __global__ __launch_bounds__(NT) void k_gsrb_tb2(double *__restrict__ uo,
@@ -635,7 +630,9 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
 // tile shape (MGIC_TB2_VARIANT, measurement): a thread owns one x pair of
 // the update region ((TX/2 + 4) x (TY + 6) pairs <= NT) and carries its
 // coefficient sets in registers; 1024 threads = four waves per SIMD at 128
-// VGPRs.  0: 64 x 22 (1008 pairs, 148 KB LDS), 1: 64 x 16 (792 pairs)
+// VGPRs.  0: 64 x 22 with 1024 threads (one pair each, 148 KB LDS),
+// 1: the same tile with 512 threads and two pairs each (measured 1.79 vs
+// 1.53 ms per 512^3 launch: fewer waves hide less of the pass latency)
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
                     hipStream_t st) {
@@ -643,7 +640,7 @@ void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const 
     const char *e = getenv("MGIC_TB2_VARIANT");
     return e ? atoi(e) : 0;
   }();
-  if (v == 1) launch_tb2<64, 16, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+  if (v == 1) launch_tb2<64, 22, 512>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
   else launch_tb2<64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
 }
 
