@@ -154,13 +154,17 @@ def main():
     # colour pass), 2 (fused sweep) or 4 (two fused sweeps per launch)
     passes_per_launch = passes / launches if launches else 0.0
     fused = passes_per_launch >= 2
-    bytes_per_launch = 48.0 * fine_cells * passes_per_launch  # 48 B/cell/pass
-    # compulsory traffic of one launch: u, rhs, a read once (+ b unless it is
-    # one value everywhere -- bCoef = 1 here, which the operator detects and
-    # does not load) + u written once, however many colour passes it performs
+    # SURVEY §8(d)'s per-pass credit (48 B/cell/colour pass: u, rhs, a, b in,
+    # u out, every pass): an effective bandwidth, reported beside the roofline
+    credit_per_launch = 48.0 * fine_cells * passes_per_launch
+    # algorithmic (compulsory) bytes of one launch: u, rhs, a read once (+ b
+    # unless it is one value everywhere -- bCoef = 1 here, which the operator
+    # detects and does not load) + u written once, however many colour passes
+    # it performs: the HBM roofline's numerator, so frac <= 1
     compulsory = 32.0 * fine_cells
     avg_launch_ms = smooth_ms / launches if launches else float("nan")
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if launches else None
+    achieved = compulsory / (avg_launch_ms * 1e-3) / 1e9 if launches else None
+    effective = credit_per_launch / (avg_launch_ms * 1e-3) / 1e9 if launches else None
     traffic = None
     tj = args.traffic_json
     if os.path.exists(tj):
@@ -215,14 +219,13 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "traffic_GBps": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and launches else None,
-                "compulsory_bytes_per_launch": compulsory,
-                "compulsory_GBps": round(compulsory / (avg_launch_ms * 1e-3) / 1e9, 1) if launches else None,
-                "note": "achieved/frac use SURVEY 8(d)'s 48 B/cell/colour-pass credit (an effective "
-                        "bandwidth: the fused launch does two passes reading each array once and "
-                        "bCoef = 1 is not loaded, so frac can exceed 1); compulsory = 32 B/cell "
-                        "(u, rhs, aCoef in, u out); traffic = PMC HBM bytes per launch "
-                        "(profiles/traffic_smoother.json)",
-                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_bytes_per_launch": compulsory,
+                "effective_GBps": round(effective, 1) if effective else None,
+                "note": "achieved/frac = algorithmic bytes per launch (32 B/cell: u, rhs, aCoef in, "
+                        "u out, once per launch whatever its colour passes) / average launch time; "
+                        "effective_GBps = SURVEY 8(d)'s 48 B/cell/colour-pass credit over the same "
+                        "time (exceeds the peak once a launch fuses passes); traffic = PMC HBM "
+                        "bytes per launch (profiles/traffic_smoother.json)",
                 "avg_launch_ms": round(avg_launch_ms, 5) if launches else None,
                 "timing": ("off" if args.no_roofline_events else
                            "HIP events on the operator stream, one pair per relax call "

@@ -469,9 +469,12 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     }
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
-  // two sweeps per launch (temporal blocking) on boxes with only domain faces
+  // two sweeps per launch (temporal blocking): on boxes with only domain
+  // faces, or with exchanged faces in deep-halo mode (the kernel's rings run
+  // onto the 4-deep shell, exchanged before every pair; rhs / coefficient
+  // shells are 4 deep there too)
   const int spl = sweeps_per_launch();
-  bool two = !halo && !cfl && spl >= 2 && n >= 2;
+  bool two = (!halo || (deep_ok && spl == 2)) && !cfl && spl >= 2 && n >= 2;
   for (int b = 0; two && b < grid->nlocal(); ++b)
     two = spl == 3 ||
           (spl == 4 ? kern::gsrb_sweep_fused2s_applies(args_hom_[b], s, prm.fused_smoother)
@@ -526,7 +529,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
         vd = kDeepDepth;
       }
     } else if (halo && !zin && (!(overlap || split) || it == 0)) {
-      src->exchange_shell(st);
+      src->exchange_shell(st, k == 2 ? kDeepDepth : 2);
     }
     // deep: sweep the grown box when the shell allows it and the result's
     // ghosts are wanted (a later sweep, or the caller's face ghosts)

@@ -81,10 +81,12 @@ def main():
     k = max(keys, key=lambda kk: sum(fetch[kk]["_dur"]))
     fb = sum(fetch[k]["FETCH_SIZE"]) / len(fetch[k]["FETCH_SIZE"]) * 1024 * 2
     wb = sum(write[k]["WRITE_SIZE"]) / len(write[k]["WRITE_SIZE"]) * 1024
-    fused = "fused" in k[0] or "block" in k[0]
+    # the key bench.py looks up: colour passes per launch of that kernel
+    kind = ("fused2x" if "tb2" in k[0] or "fused2s" in k[0] else
+            "fused" if "fused" in k[0] or "block" in k[0] else "pass")
     out_path = os.path.join(ROOT, "profiles", "traffic_smoother.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    data[f"n{args.n}_w{args.world}_{'fused' if fused else 'pass'}"] = {
+    data[f"n{args.n}_w{args.world}_{kind}"] = {
         "kernel": k[0], "grid": k[1], "tag": args.tag,
         "read_bytes_per_launch": fb, "write_bytes_per_launch": wb,
         "hbm_bytes_per_launch": fb + wb,
