@@ -66,7 +66,9 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #define TB2_STAMP(id, p) ((void)0)
 #endif
 // diagnostic builds of tools/tb2_probe.hip only: bit 0 skips the global
-// loads, bit 1 the colour passes, bit 2 the stores (wrong results, timing)
+// loads, bit 1 the colour passes, bit 2 the stores, bit 3 the red (phase A)
+// passes, bit 4 the black (phase B) passes, bit 5 replaces the update chain
+// by six adds of its inputs, bit 6 the divisions (wrong results, timing)
 #ifndef TB2_PROBE_SKIP
 #define TB2_PROBE_SKIP 0
 #endif
@@ -349,9 +351,10 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
       na1[i] = va.y;
     }
   };
-  auto lam = [&](double aa) { return 1.0 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
+  auto lam = [&](double aa) { return (TB2_PROBE_SKIP & 64) ? aa + s.lamshift : 1.0 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
   auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
                  double rv, double aa, double lm) -> double {
+    if (TB2_PROBE_SKIP & 32) return ((uc + xm) + (xp + ym)) + ((yp + zm) + zp);
     const double tx = (xp + xm) - 2.0 * uc;
     const double ty = (yp + ym) - 2.0 * uc;
     const double tz = (zp + zm) - 2.0 * uc;
@@ -375,6 +378,8 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   auto pass = [&](bool red, int W, int sl, int t, int k, const double (&cr)[NP],
                   const double (&ca)[NP], const double (&cl)[NP]) {
     if (k < klo(W) || k > khi(W) || (TB2_PROBE_SKIP & 2)) return;  // uniform
+    if ((TB2_PROBE_SKIP & 8) && red) return;
+    if ((TB2_PROBE_SKIP & 16) && !red) return;
     double *X = (red ? R : B) + sl * SS;
     double *N = (red ? B : R) + sl * SS;
     double *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
@@ -645,7 +650,9 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
 // coefficient sets in registers; 1024 threads = four waves per SIMD at 128
 // VGPRs.  0: 64 x 22 with 1024 threads (one pair each, 148 KB LDS),
 // 1: the same tile with 512 threads and two pairs each (measured 1.79 vs
-// 1.53 ms per 512^3 launch: fewer waves hide less of the pass latency)
+// 1.53 ms per 512^3 launch: fewer waves hide less of the pass latency).
+// 58 x 22 (one u load per lane, 924 busy lanes) measured 1.53 vs 1.36 ms:
+// a step costs about the same whatever the tile, so wide tiles win
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
                     hipStream_t st) {
