@@ -58,8 +58,6 @@ using sweep::bsel;
 
 template <int N>
 using IC = std::integral_constant<int, N>;
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 // in-kernel time stamps for tools/tb2_probe.hip (diagnostic builds only)
 #ifndef TB2_STAMP
@@ -424,19 +422,17 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     }
   };
   // plane k's tile cells -> u_out (or acc += them), from ring slot sl
-  // Raw buffer stores: a lane's elements outside the tile (or a plane
-  // outside the chunk) get an offset past the buffer's range and the store
-  // is dropped, so every step issues exactly NP * 2 store instructions with
-  // no branch around them.  vmcnt counts loads and stores together in issue
-  // order; with a static store count the next step's wait for the loads
-  // issued before these stores is vmcnt(stores) instead of vmcnt(0), which
-  // would also wait for the stores' completion.
+  // Stores with a static instruction count (sweep::bstore): a lane's
+  // elements outside the tile (or a plane outside the chunk) are dropped by
+  // an out-of-range offset, so every step issues exactly NP * 2 stores with
+  // no branch around them and the next step waits vmcnt(2) for its loads
+  // instead of vmcnt(0), which would also wait for these stores.
   auto store = [&](int sl, int t, int k) {
     if (TB2_PROBE_SKIP & 4) return;
     const bool kin = k >= z0 && k < z1;  // uniform
     char *dst = reinterpret_cast<char *>((ACC ? acc : uo) + corner + (long)clampi(k, z0, z1 - 1) * sz);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7fffffff, 0x00020000);
-    constexpr unsigned kDrop = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t rs = sweep::store_rsrc(dst);
+    constexpr unsigned kDrop = sweep::kDrop;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int st = kin ? (rinf[t][i] >> 8) & 3 : 0;
@@ -453,8 +449,8 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
       const unsigned o4 = st == 3 ? off : kDrop;
       const unsigned o2 = st == 1 ? off : (st == 2 ? off + 8 : kDrop);
       const double e = st == 1 ? w.x : w.y;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w), rs, o4, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, e), rs, o2, 0, 0);
+      sweep::bstore(rs, w, o4);
+      sweep::bstore(rs, e, o2);
     }
   };
   // One pipeline step at plane p (t: its parity relative to pstart; slot

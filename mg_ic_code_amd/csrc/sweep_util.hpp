@@ -34,6 +34,31 @@ __device__ __forceinline__ float bsel(int q, float x, float y) {
   return __uint_as_float((__float_as_uint(x) & m) | (__float_as_uint(y) & ~m));
 }
 
+// Stores whose instruction count does not depend on the lane: raw buffer
+// stores through a resource over `base`, where a lane that must not store
+// passes kDrop as its byte offset (past the range: the hardware drops it).
+// vmcnt counts loads and stores together in issue order, so with a static
+// store count a later wait for loads issued BEFORE the stores is vmcnt(n
+// stores) instead of vmcnt(0) -- which would also wait for the stores.
+constexpr unsigned kDrop = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t store_rsrc(void *base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+}
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, double2 v, unsigned off) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, double v, unsigned off) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float2 v, unsigned off) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, unsigned off) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+
 // XCD-aware workgroup -> tile order: blocks are dealt round-robin over the
 // 8 XCDs, so give each XCD a contiguous range of tiles (neighbouring tiles
 // share halo lines in that XCD's L2)
