@@ -167,44 +167,19 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   };
 
   // ---- loads of u (slot c = LDS pair index), per plane parity t ----------
-  // A pair holding a ghost of an x / y domain face loads the cells the ghost
-  // images and transforms them (image(); lbc bits per t: 0-2 x rule, 3-4 y
-  // rule), so every ghost enters the ring as the value ParseBC writes before
-  // the first colour pass (SetBCs.cpp:49-131)
+  // (ghost pairs of x / y domain faces load whatever the ghost cells hold:
+  // no pass reads them, see pass)
   unsigned loff[2][NL];
-  int lbc[NL];
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int c = tid + i * NT;
     const int r = c / PW, m = c - r * PW;
     const int gy = y0 - 4 + r;
-    int bits = 0;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int X = x0 - 6 + 2 * m + ((gsum + gy + t) & 1);
-      int gx = clampi(X, -6, nx + 3), bx = 0, ly = clampi(gy, -4, ny + 3), by = 0;
-      if (g.bcm[0] && X == -1) {  // (-1, 0): element 0 <- image of element 1
-        bx = 1;
-      } else if (g.bcm[0] && X == -2) {  // (-2, -1) <- image of 0: load (0, 1)
-        gx = 0;
-        bx = 2;
-      } else if (g.bcm[1] && X == nx - 1) {  // (nx-1, nx): element 1 <- image of element 0
-        bx = 3;
-      } else if (g.bcm[1] && X == nx) {  // (nx, nx+1) <- image of nx-1: load (nx-2, nx-1)
-        gx = nx - 2;
-        bx = 4;
-      }
-      if (g.bcm[2] && gy == -1) {
-        ly = 0;
-        by = 1;
-      } else if (g.bcm[3] && gy == ny) {
-        ly = ny - 1;
-        by = 2;
-      }
-      loff[t][i] = c < CP ? boff(gx, ly) : 0u;
-      bits |= (c < CP ? bx | (by << 3) : 0) << (5 * t);
+      loff[t][i] = c < CP ? boff(clampi(X, -6, nx + 3), clampi(gy, -4, ny + 3)) : 0u;
     }
-    lbc[i] = bits;
   }
   // ---- update pairs: c = tid + i * NT -> row rr (y0-3+rr), pair m ---------
   // Lanes 32q .. 32q+31 take pairs 1..32 of row q (one row per 32-lane LDS
@@ -290,28 +265,9 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
       }
     }
   };
-  // ghost pairs of the fetched plane p -> ParseBC's images (ghosts of two
-  // faces, never read, get garbage)
+  // a z ghost plane of a domain face, fetched as the plane it images ->
+  // ParseBC's images.  (x / y ghosts are never stored: see pass.)
   auto image = [&](int t, int p) {
-    if (EDGE) {
-#pragma unroll
-      for (int i = 0; i < NL; ++i) {
-        const int bits = lbc[i] >> (5 * t), bx = bits & 7, by = (bits >> 3) & 3;
-        if (!(bx | by)) continue;
-        double u0 = pu0[i], u1 = pu1[i];
-        if (by) {
-          const int yf = by == 1 ? 2 : 3;
-          u0 = ghost(gg, yf, u0);
-          u1 = ghost(gg, yf, u1);
-        }
-        if (bx == 1) u0 = ghost(gg, 0, u1);
-        else if (bx == 2) u1 = ghost(gg, 0, u0);
-        else if (bx == 3) u1 = ghost(gg, 1, u0);
-        else if (bx == 4) u0 = ghost(gg, 1, u1);
-        pu0[i] = u0;
-        pu1[i] = u1;
-      }
-    }
     if ((zdl && p == -1) || (zdh && p == nz)) {
       const int zf = p == -1 ? 4 : 5;
 #pragma unroll
@@ -369,10 +325,12 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // One colour pass on plane k (ring slot sl, parity t, coefficient set j)
   // over the ring of width W: every pair's LDS reads, then the update chains,
   // then the writes (the compiler cannot move one update's LDS accesses across
-  // another's).  A ghost is read only by the cell it images, so a face
-  // cell's update rewrites its ghosts (in the other colour's array, at
-  // positions no pass updates) with the image of its new value: what ParseBC
-  // writes before the next colour pass that reads them.
+  // another's).  A ghost is read only by the cell it images, and ParseBC
+  // fills it from that cell's value before every colour pass
+  // (SetBCs.cpp:49-131), i.e. from the value the update starts from: an x / y
+  // face cell takes its ghost neighbour as ghost(its own value) in registers
+  // (branch-free selects), so x / y ghosts are never stored or loaded.  z
+  // ghosts (face planes of z chunks only) are still written into the ring.
   auto pass = [&](bool red, int W, int sl, int t, int k, const double (&cr)[NP],
                   const double (&ca)[NP], const double (&cl)[NP]) {
     if (k < klo(W) || k > khi(W) || (TB2_PROBE_SKIP & 2)) return;  // uniform
@@ -395,23 +353,21 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
       zm[i] = Nm[c + o];
       zp[i] = Np[c + o];
     }
+    if (EDGE) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int f = (rinf[t][i] >> (red ? 0 : 4)) & 15;
+        xm[i] = (f & 1) ? ghost(gg, 0, uc[i]) : xm[i];
+        xp[i] = (f & 2) ? ghost(gg, 1, uc[i]) : xp[i];
+        ym[i] = (f & 4) ? ghost(gg, 2, uc[i]) : ym[i];
+        yp[i] = (f & 8) ? ghost(gg, 3, uc[i]) : yp[i];
+      }
+    }
     double v[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) v[i] = upd(uc[i], xm[i], xp[i], ym[i], yp[i], zm[i], zp[i], cr[i], ca[i], cl[i]);
 #pragma unroll
     for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> (red ? 10 : 11)) & 1 ? v[i] : uc[i];
-    if (EDGE) {
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int f = (rinf[t][i] >> (red ? 0 : 4)) & 15;
-        if (!f) continue;
-        const int c = ci[i], o = yzo[t][i] + (red ? 0 : 1);
-        if (f & 1) N[c - (red ? 1 : 0)] = ghost(gg, 0, v[i]);
-        if (f & 2) N[c + (red ? 0 : 1)] = ghost(gg, 1, v[i]);
-        if (f & 4) N[c + o - PW] = ghost(gg, 2, v[i]);
-        if (f & 8) N[c + o + PW] = ghost(gg, 3, v[i]);
-      }
-    }
     const bool zl = zdl && k == 0, zh = zdh && k == nz - 1;
     if (zl || zh) {  // z ghosts of the face plane (every lane: an element
                      // never updated owns its ghost alone)

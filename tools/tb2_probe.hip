@@ -35,7 +35,7 @@ int main(int argc, char **argv) {
   g.sy = geo.sy;
   g.sz = geo.sz;
   for (int f = 0; f < 6; ++f) {
-    g.bcm[f] = kBcDirichlet;
+    g.bcm[f] = argc > 3 && atoi(argv[3]) ? kBcMemory : kBcDirichlet;
     g.bcc[f] = 0.0;
   }
   StencilCoefs s{};
