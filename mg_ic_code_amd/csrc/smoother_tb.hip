@@ -129,7 +129,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
                                          const double *__restrict__ rhs,
                                          const double *__restrict__ a, const BoxArgs &g,
                                          const StencilCoefs &s, const TB2Ghosts &gg, int x0,
-                                         int y0, int z0, int z1) {
+                                         int y0, int z0, int z1, int ef) {
   using F = TB2<TX, TY, NT>;
   constexpr int PW = F::PW, CP = F::CP, SS = F::SS, UW = F::UW, NRP = F::NRP, NL = F::NL,
                 NP = F::NP;
@@ -357,10 +357,11 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const int f = (rinf[t][i] >> (red ? 0 : 4)) & 15;
-        xm[i] = (f & 1) ? ghost(gg, 0, uc[i]) : xm[i];
-        xp[i] = (f & 2) ? ghost(gg, 1, uc[i]) : xp[i];
-        ym[i] = (f & 4) ? ghost(gg, 2, uc[i]) : ym[i];
-        yp[i] = (f & 8) ? ghost(gg, 3, uc[i]) : yp[i];
+        // ef: the domain faces this tile's rings reach (uniform)
+        if (ef & 1) xm[i] = (f & 1) ? ghost(gg, 0, uc[i]) : xm[i];
+        if (ef & 2) xp[i] = (f & 2) ? ghost(gg, 1, uc[i]) : xp[i];
+        if (ef & 4) ym[i] = (f & 4) ? ghost(gg, 2, uc[i]) : ym[i];
+        if (ef & 8) yp[i] = (f & 8) ? ghost(gg, 3, uc[i]) : yp[i];
       }
     }
     double v[NP];
@@ -509,15 +510,15 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(double *__restrict__ uo,
   const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
   const int z0 = (L / (ntx * nty)) * kc;
   const int z1 = min(z0 + kc, g.nz);
-  // uniform: do the tile's rings (3 cells) reach an x / y domain face?
-  const bool edge = (g.bcm[0] && x0 <= 3) || (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx) ||
-                    (g.bcm[2] && y0 <= 3) || (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny);
-  if (edge)
+  // uniform: the x / y domain faces the tile's rings (3 cells) reach
+  const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
+                 (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
+  if (ef)
     tb2_tile<TX, TY, NT, ZIN, ACC, FAST, true>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
-                                               z1);
+                                               z1, ef);
   else
     tb2_tile<TX, TY, NT, ZIN, ACC, FAST, false>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
-                                                z1);
+                                                z1, 0);
 }
 
 template <int TX, int TY, int NT>
