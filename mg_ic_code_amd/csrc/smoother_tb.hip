@@ -233,6 +233,16 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // clipped to the box at a domain face
   auto klo = [&](int w) { return zdl ? max(z0 - w, 0) : z0 - w; };
   auto khi = [&](int w) { return zdh ? min(z1 - 1 + w, nz - 1) : z1 - 1 + w; };
+  int kl[4];
+  unsigned kw[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    kl[w] = klo(w);
+    kw[w] = (unsigned)(khi(w) - klo(w));
+  }
+  constexpr int kNone = -(1 << 28);
+  const int zfl = zdl ? 0 : kNone, zfh = zdh ? nz - 1 : kNone;
+  const int zgl = zdl ? -1 : kNone, zgh = zdh ? nz : kNone;
 
   double pu0[NL], pu1[NL];                    // u pairs of plane p+2 in flight
   double nr0[NP], nr1[NP], na0[NP], na1[NP];  // rhs / aCoef pairs of plane p+1 in flight
@@ -252,7 +262,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
 
   auto fetch_u = [&](int t, int p) {
     // a z ghost plane of a domain face loads the plane it images
-    const char *pl = plane(ui, (zdl && p == -1) ? 0 : (zdh && p == nz) ? nz - 1 : p);
+    const char *pl = plane(ui, p == zgl ? 0 : p == zgh ? nz - 1 : p);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (ZIN || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
@@ -268,7 +278,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // a z ghost plane of a domain face, fetched as the plane it images ->
   // ParseBC's images.  (x / y ghosts are never stored: see pass.)
   auto image = [&](int t, int p) {
-    if ((zdl && p == -1) || (zdh && p == nz)) {
+    if (p == zgl || p == zgh) {
       const int zf = p == -1 ? 4 : 5;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
@@ -333,7 +343,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // ghosts (face planes of z chunks only) are still written into the ring.
   auto pass = [&](bool red, int W, int sl, int t, int k, const double (&cr)[NP],
                   const double (&ca)[NP], const double (&cl)[NP]) {
-    if (k < klo(W) || k > khi(W) || (TB2_PROBE_SKIP & 2)) return;  // uniform
+    if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
     if ((TB2_PROBE_SKIP & 8) && red) return;
     if ((TB2_PROBE_SKIP & 16) && !red) return;
     double *X = (red ? R : B) + sl * SS;
@@ -369,7 +379,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     for (int i = 0; i < NP; ++i) v[i] = upd(uc[i], xm[i], xp[i], ym[i], yp[i], zm[i], zp[i], cr[i], ca[i], cl[i]);
 #pragma unroll
     for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> (red ? 10 : 11)) & 1 ? v[i] : uc[i];
-    const bool zl = zdl && k == 0, zh = zdh && k == nz - 1;
+    const bool zl = k == zfl, zh = k == zfh;
     if (zl || zh) {  // z ghosts of the face plane (every lane: an element
                      // never updated owns its ghost alone)
       double *Nz = zl ? Nm : Np;
