@@ -70,6 +70,23 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_PROBE_SKIP
 #define TB2_PROBE_SKIP 0
 #endif
+// measurement switches (A/B builds): TB2_ROT 1 = coefficient sets moved down
+// one register set per step in a 2-step loop (round 2's first form);
+// TB2_NO_READ2 1 = x-neighbour pairs as two ds_read_b64
+#ifndef TB2_ROT
+#define TB2_ROT 0
+#endif
+#ifndef TB2_NO_READ2
+#define TB2_NO_READ2 0
+#endif
+// TB2_PF2 1 = loads two steps ahead (plain / ZIN variants); TB2_STORE_CPOL =
+// cache-policy bits of the u_out stores (16 = sc1: drop the line from L2)
+#ifndef TB2_PF2
+#define TB2_PF2 1
+#endif
+#ifndef TB2_STORE_CPOL
+#define TB2_STORE_CPOL 0
+#endif
 
 // Geometry.  Rows of the LDS ring are SHIFTED pairings: in row y of plane k
 // pair m holds cells (X, X+1) with X = x0 - 6 + 2m + s, s = (x0 + y + k +
@@ -244,8 +261,12 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   const int zfl = zdl ? 0 : kNone, zfh = zdh ? nz - 1 : kNone;
   const int zgl = zdl ? -1 : kNone, zgh = zdh ? nz : kNone;
 
-  double pu0[NL], pu1[NL];                    // u pairs of plane p+2 in flight
-  double nr0[NP], nr1[NP], na0[NP], na1[NP];  // rhs / aCoef pairs of plane p+1 in flight
+  // loads in flight, PF steps ahead (PF 1: u plane p+2 and rhs / aCoef of
+  // plane p+1 while step p runs; PF 2: planes p+3 / p+2, one register set
+  // per step parity)
+  constexpr int PF = (TB2_PF2 && !ACC) ? 2 : 1;
+  double pu0[PF][NL], pu1[PF][NL];
+  double nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
   // later), black of planes p-1 .. p-4 (made one step later from rb / ab);
@@ -260,59 +281,63 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     for (int j = 0; j < 4; ++j) Rr[j][i] = Ra[j][i] = Rl[j][i] = Br[j][i] = Ba[j][i] = Bl[j][i] = 0.0;
   }
 
-  auto fetch_u = [&](int t, int p) {
+  auto fetch_u = [&](int t, int p, auto bc) {
+    constexpr int b = decltype(bc)::value;
     // a z ghost plane of a domain face loads the plane it images
     const char *pl = plane(ui, p == zgl ? 0 : p == zgh ? nz - 1 : p);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (ZIN || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
-        pu0[i] = 0.0;
-        pu1[i] = 0.0;
+        pu0[b][i] = 0.0;
+        pu1[b][i] = 0.0;
       } else if (NL * NT <= CP || tid + i * NT < CP) {  // (whole waves past the plane skip)
         const double2 v = at2(pl, loff[t][i]);
-        pu0[i] = v.x;
-        pu1[i] = v.y;
+        pu0[b][i] = v.x;
+        pu1[b][i] = v.y;
       }
     }
   };
   // a z ghost plane of a domain face, fetched as the plane it images ->
   // ParseBC's images.  (x / y ghosts are never stored: see pass.)
-  auto image = [&](int t, int p) {
+  auto image = [&](int p, auto bc) {
+    constexpr int b = decltype(bc)::value;
     if (p == zgl || p == zgh) {
       const int zf = p == -1 ? 4 : 5;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
-        pu0[i] = ghost(gg, zf, pu0[i]);
-        pu1[i] = ghost(gg, zf, pu1[i]);
+        pu0[b][i] = ghost(gg, zf, pu0[b][i]);
+        pu1[b][i] = ghost(gg, zf, pu1[b][i]);
       }
     }
   };
-  auto put = [&](int sl) {  // into ring slot sl: red element -> R, black -> B
+  auto put = [&](int sl, auto bc) {  // into ring slot sl: red element -> R, black -> B
+    constexpr int b = decltype(bc)::value;
     double *Rs = R + sl * SS, *Bs = B + sl * SS;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (NL * NT > CP && tid + i * NT >= CP) continue;  // whole waves past the plane
-      Rs[tid + i * NT] = pu0[i];
-      Bs[tid + i * NT] = pu1[i];
+      Rs[tid + i * NT] = pu0[b][i];
+      Bs[tid + i * NT] = pu1[b][i];
     }
   };
-  auto fetch_c = [&](int t, int p) {
+  auto fetch_c = [&](int t, int p, auto bc) {
+    constexpr int b = decltype(bc)::value;
     const char *pr = plane(rhs, p), *pa = plane(a, p);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       if (TB2_PROBE_SKIP & 1) {
-        nr0[i] = 0.5;
-        nr1[i] = 0.25;
-        na0[i] = -1.5;
-        na1[i] = -1.25;
+        nr0[b][i] = 0.5;
+        nr1[b][i] = 0.25;
+        na0[b][i] = -1.5;
+        na1[b][i] = -1.25;
         continue;
       }
       const double2 vr = at2(pr, roff[t][i]);
       const double2 va = at2(pa, roff[t][i]);
-      nr0[i] = vr.x;
-      nr1[i] = vr.y;
-      na0[i] = va.x;
-      na1[i] = va.y;
+      nr0[b][i] = vr.x;
+      nr1[b][i] = vr.y;
+      na0[b][i] = va.x;
+      na1[b][i] = va.y;
     }
   };
   auto lam = [&](double aa) { return (TB2_PROBE_SKIP & 64) ? aa + s.lamshift : 1.0 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
@@ -356,8 +381,17 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
       const int c = ci[i];
       const int o = yzo[t][i] + (red ? 0 : 1);  // y / z neighbours: pair m-1+s (red), m+s (black)
       uc[i] = X[c];
+#if TB2_NO_READ2
+      // separate ds_read_b64s: a ds_read2_b64 of the adjacent pair costs 8
+      // LDS cycles against 2 x 2
+      int cx = c + (red ? 0 : 1);
+      asm volatile("" : "+v"(cx));
+      xm[i] = N[c - (red ? 1 : 0)];
+      xp[i] = N[cx];
+#else
       xm[i] = N[c - (red ? 1 : 0)];
       xp[i] = N[c + (red ? 0 : 1)];
+#endif
       ym[i] = N[c + o - PW];
       yp[i] = N[c + o + PW];
       zm[i] = Nm[c + o];
@@ -416,8 +450,8 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
       const unsigned o4 = st == 3 ? off : kDrop;
       const unsigned o2 = st == 1 ? off : (st == 2 ? off + 8 : kDrop);
       const double e = st == 1 ? w.x : w.y;
-      sweep::bstore(rs, w, o4);
-      sweep::bstore(rs, e, o2);
+      sweep::bstore<TB2_STORE_CPOL>(rs, w, o4);
+      sweep::bstore<TB2_STORE_CPOL>(rs, e, o2);
     }
   };
   // One pipeline step at plane p (t: its parity relative to pstart; slot
@@ -429,7 +463,13 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // cells only, phase B red ones.  Live ring planes p+1 .. p-5; plane p+1 is
   // written over plane p-7.
   auto step = [&](auto tc, int p) {
-    constexpr int T = decltype(tc)::value, U = T ^ 1;  // parity of p, of p +- 1
+    // J: position in the 4-step unrolled loop; T / U: parity of p / of p +- 1;
+    // coefficient sets live in slot J (made this step) .. slot J3 (made
+    // three steps ago, last use), so no register moves between steps
+    constexpr int J = decltype(tc)::value, T = J & 1, U = T ^ 1;
+    constexpr int J0 = TB2_ROT ? 0 : J, J3 = TB2_ROT ? 3 : (J + 1) & 3;
+    constexpr int FB = PF == 2 ? (J & 1) : 0;  // in-flight register set consumed / refilled
+    using ICF = IC<FB>;
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
     const int sl = p & 7;
     TB2_STAMP(0, p);
@@ -437,18 +477,19 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     // of plane p from its pair fetched last step (alpha * a, .ChF:107)
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      Br[0][i] = rb[i];
-      Ba[0][i] = FAST ? ab[i] : s.alpha * ab[i];
-      Bl[0][i] = lam(Ba[0][i]);
-      Rr[0][i] = nr0[i];
-      Ra[0][i] = FAST ? na0[i] : s.alpha * na0[i];
-      Rl[0][i] = lam(Ra[0][i]);
-      rb[i] = nr1[i];
-      ab[i] = na1[i];
+      Br[J0][i] = rb[i];
+      Ba[J0][i] = FAST ? ab[i] : s.alpha * ab[i];
+      Bl[J0][i] = lam(Ba[J0][i]);
+      Rr[J0][i] = nr0[FB][i];
+      Ra[J0][i] = FAST ? na0[FB][i] : s.alpha * na0[FB][i];
+      Rl[J0][i] = lam(Ra[J0][i]);
+      rb[i] = nr1[FB][i];
+      ab[i] = na1[FB][i];
     }
-    image(U, p + 1);
-    put((sl + 1) & 7);
-    fetch_c(U, p + 1);
+    image(p + 1, ICF{});
+    put((sl + 1) & 7, ICF{});
+    if (PF == 2) fetch_c(T, p + 2, ICF{});
+    else fetch_c(U, p + 1, ICF{});
     if (ACC) {
       const char *pl = plane(acc, p - 3);
 #pragma unroll
@@ -460,23 +501,24 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
         an1[i] = v.y;
       }
     }
-    fetch_u(T, p + 2);
+    if (PF == 2) fetch_u(U, p + 3, ICF{});
+    else fetch_u(T, p + 2, ICF{});
     TB2_STAMP(1, p);
     __syncthreads();
     TB2_STAMP(2, p);
-    pass(true, 3, sl, T, p, Rr[0], Ra[0], Rl[0]);
-    pass(true, 1, (sl + 5) & 7, U, p - 3, Rr[3], Ra[3], Rl[3]);
+    pass(true, 3, sl, T, p, Rr[J0], Ra[J0], Rl[J0]);
+    pass(true, 1, (sl + 5) & 7, U, p - 3, Rr[J3], Ra[J3], Rl[J3]);
     TB2_STAMP(3, p);
     __syncthreads();
     TB2_STAMP(4, p);
-    pass(false, 2, (sl + 7) & 7, U, p - 1, Br[0], Ba[0], Bl[0]);
-    pass(false, 0, (sl + 4) & 7, T, p - 4, Br[3], Ba[3], Bl[3]);
+    pass(false, 2, (sl + 7) & 7, U, p - 1, Br[J0], Ba[J0], Bl[J0]);
+    pass(false, 0, (sl + 4) & 7, T, p - 4, Br[J3], Ba[J3], Bl[J3]);
     TB2_STAMP(5, p);
     store((sl + 4) & 7, T, p - 4);
     TB2_STAMP(6, p);
-    // every set moves down one plane
+    // TB2_ROT (the round-1 form): every set moves down one plane
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
+    for (int i = 0; i < NP && TB2_ROT; ++i) {
 #pragma unroll
       for (int j = 3; j > 0; --j) {
         Rr[j][i] = Rr[j - 1][i];
@@ -489,18 +531,33 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     }
   };
 
-  fetch_u(1, pstart - 1);
-  image(1, pstart - 1);
-  put((pstart - 1) & 7);
-  fetch_u(0, pstart);
-  image(0, pstart);
-  put(pstart & 7);
-  fetch_u(1, pstart + 1);
-  fetch_c(0, pstart);
+  fetch_u(1, pstart - 1, IC<0>{});
+  image(pstart - 1, IC<0>{});
+  put((pstart - 1) & 7, IC<0>{});
+  fetch_u(0, pstart, IC<0>{});
+  image(pstart, IC<0>{});
+  put(pstart & 7, IC<0>{});
+  fetch_u(1, pstart + 1, IC<0>{});
+  fetch_c(0, pstart, IC<0>{});
+  if (PF == 2) {
+    fetch_u(0, pstart + 2, IC<PF - 1>{});
+    fetch_c(1, pstart + 1, IC<PF - 1>{});
+  }
+#if TB2_ROT
   for (int p = pstart; p <= pend; p += 2) {
     step(IC<0>{}, p);
     step(IC<1>{}, p + 1);
   }
+#else
+  // (up to three steps past pend: their passes and stores fall outside every
+  // range test, their loads are clamped)
+  for (int p = pstart; p <= pend; p += 4) {
+    step(IC<0>{}, p);
+    step(IC<1>{}, p + 1);
+    step(IC<2>{}, p + 2);
+    step(IC<3>{}, p + 3);
+  }
+#endif
 }
 
 

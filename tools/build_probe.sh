@@ -7,7 +7,8 @@ cd "$(dirname "$0")"
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I../mg_ic_code_amd/csrc"
 S=../mg_ic_code_amd/csrc/smoother.hip
-$H $F -o tb2_probe tb2_probe.hip $S &
-$H $F -DSTAMPS -o tb2_probe_st tb2_probe.hip $S &
+D=${DEFS:-}
+$H $F $D -o tb2_probe tb2_probe.hip $S &
+$H $F $D -DSTAMPS -o tb2_probe_st tb2_probe.hip $S &
 for k in ${SKIPS:-1 2 4}; do $H $F -DTB2_PROBE_SKIP=$k -o tb2_probe_s$k tb2_probe.hip $S & done
 wait

@@ -79,6 +79,7 @@ int main(int argc, char **argv) {
   printf("{\"n\": %d, \"zin\": %d, \"ms_per_launch\": %.4f, \"compulsory_GBps\": %.1f}\n", n, zin,
          ms, (zin ? 24.0 : 32.0) * cells / (ms * 1e-3) / 1e9);
 #ifdef STAMPS
+  constexpr int kStamps = 7;  // TB2_STAMP ids 0..6 per step (smoother_tb.hip)
   static unsigned long long st[4][64][12];
   MGIC_HIP(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
   for (int w = 0; w < 4; ++w) {
@@ -86,13 +87,13 @@ int main(int argc, char **argv) {
     int cnt = 0;
     for (int p = 0; p < 63; ++p) {
       if (!st[w][p][0] || !st[w][p + 1][0]) continue;
-      for (int i = 0; i < 11; ++i) acc[i] += (double)(st[w][p][i + 1] - st[w][p][i]);
-      acc[11] += (double)(st[w][p + 1][0] - st[w][p][11]);
+      for (int i = 0; i < kStamps - 1; ++i) acc[i] += (double)(st[w][p][i + 1] - st[w][p][i]);
+      acc[kStamps - 1] += (double)(st[w][p + 1][0] - st[w][p][kStamps - 1]);
       ++cnt;
     }
     printf("block %d: %d steps; memtime ticks per step by phase:", blocks[w], cnt);
     double tot = 0;
-    for (int i = 0; i < 12; ++i) {
+    for (int i = 0; i < kStamps; ++i) {
       printf(" %.0f", cnt ? acc[i] / cnt : 0.0);
       tot += cnt ? acc[i] / cnt : 0.0;
     }
