@@ -199,9 +199,11 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     }
   }
   // ---- update pairs: c = tid + i * NT -> row rr (y0-3+rr), pair m ---------
-  // Lanes 32q .. 32q+31 take pairs 1..32 of row q (one row per 32-lane LDS
-  // bank group: conflict-free reads); the rows' last UW-32 pairs go to the
-  // lanes after them.  Per parity t: roff (global byte offset of the pair),
+  // Each 32-lane half of a wave takes pairs 1..32 of one row (one row per
+  // 32-lane LDS bank group: conflict-free reads); wave w holds rows w and
+  // NR-1-w, so the inner rings' passes skip the waves of the outer rows
+  // whole.  The rows' last UW-32 pairs go to the lanes after them.  Per
+  // parity t: roff (global byte offset of the pair),
   // yzo (LDS index offset of the red element's y / z neighbours: s - 1; the
   // black one's is s), rinf (bits 0-3 / 4-7: domain faces the red / black
   // element borders; 8-9: store mask of the red / black element; 10-11: the
@@ -212,12 +214,16 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // test.
   static_assert(UW >= 32, "a row must fill a 32-lane group");
   constexpr int NR = TY + 6, MAIN = 32 * NR;
+  static_assert(NR % 2 == 0 && MAIN <= NT * NP, "row pairing needs an even row count");
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index (uniform)
   unsigned roff[2][NP];
   int yzo[2][NP], rinf[2][NP], ci[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     const int c = tid + i * NT, jt = c - MAIN;
-    const int rr = c < MAIN ? c >> 5 : jt / (UW - 32);
+    // wave w takes rows w and NR-1-w (one per 32-lane half), so the waves
+    // of the outer rows -- idle in the inner rings' passes -- skip them whole
+    const int rr = c < MAIN ? (((c >> 5) & 1) ? NR - 1 - (c >> 6) : (c >> 6)) : jt / (UW - 32);
     const int m = c < MAIN ? 1 + (c & 31) : 33 + jt - (jt / (UW - 32)) * (UW - 32);
     const int gy = y0 - 3 + rr;
     const bool row_ok = c < NRP;
@@ -369,6 +375,9 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   auto pass = [&](bool red, int W, int sl, int t, int k, const double (&cr)[NP],
                   const double (&ca)[NP], const double (&cl)[NP]) {
     if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
+    // rows beyond ring W (distance > W from the tile) are never read once
+    // this pass is done, so waves holding only such rows skip it
+    if (W < 3 && wv < 3 - W) return;
     if ((TB2_PROBE_SKIP & 8) && red) return;
     if ((TB2_PROBE_SKIP & 16) && !red) return;
     double *X = (red ? R : B) + sl * SS;

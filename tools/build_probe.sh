@@ -10,5 +10,6 @@ S=../mg_ic_code_amd/csrc/smoother.hip
 D=${DEFS:-}
 $H $F $D -o tb2_probe tb2_probe.hip $S &
 $H $F $D -DSTAMPS -o tb2_probe_st tb2_probe.hip $S &
+$H $F $D -DDRIFT -o tb2_probe_drift tb2_probe.hip $S &
 for k in ${SKIPS:-1 2 4}; do $H $F -DTB2_PROBE_SKIP=$k -o tb2_probe_s$k tb2_probe.hip $S & done
 wait

@@ -22,6 +22,21 @@ __device__ int g_probe_blocks[4];
   } while (0)
 #endif
 
+#ifdef DRIFT
+// per-block progress: thread 0 stamps step p = z0 + 32k (k < 16) and the
+// tile origin, so the host can see how far neighbouring tiles drift apart
+__device__ unsigned long long g_drift[2048][16];
+__device__ int g_tile[2048][2];
+#define TB2_STAMP(id, p)                                                              \
+  do {                                                                                \
+    if (id == 0 && threadIdx.x == 0 && (p) >= z0 && (p) < z0 + 512 && (((p) - z0) & 31) == 0) { \
+      g_drift[blockIdx.x][((p) - z0) >> 5] = __builtin_amdgcn_s_memrealtime();           \
+      g_tile[blockIdx.x][0] = x0;                                                     \
+      g_tile[blockIdx.x][1] = y0;                                                     \
+    }                                                                                 \
+  } while (0)
+#endif
+
 #include "../mg_ic_code_amd/csrc/smoother_tb.hip"
 
 using namespace mgic;
@@ -98,6 +113,34 @@ int main(int argc, char **argv) {
       tot += cnt ? acc[i] / cnt : 0.0;
     }
     printf("  total %.0f\n", tot);
+  }
+#endif
+#ifdef DRIFT
+  static unsigned long long dr[2048][16];
+  static int tl[2048][2];
+  MGIC_HIP(hipMemcpyFromSymbol(dr, HIP_SYMBOL(g_drift), sizeof(dr)));
+  MGIC_HIP(hipMemcpyFromSymbol(tl, HIP_SYMBOL(g_tile), sizeof(tl)));
+  // blocks of the last launch: those with a stamp at k = 0
+  std::vector<int> bs;
+  for (int b = 0; b < 2048; ++b)
+    if (dr[b][0]) bs.push_back(b);
+  for (int k = 0; k < 16; ++k) {
+    unsigned long long lo = ~0ull, hi = 0;
+    double nb = 0;
+    int nn = 0;
+    for (int b : bs) {
+      if (!dr[b][k]) continue;
+      lo = dr[b][k] < lo ? dr[b][k] : lo;
+      hi = dr[b][k] > hi ? dr[b][k] : hi;
+      for (int c : bs)  // x neighbour (same y0, x0 + 64)
+        if (tl[c][1] == tl[b][1] && tl[c][0] == tl[b][0] + 64 && dr[c][k]) {
+          nb += dr[c][k] > dr[b][k] ? (double)(dr[c][k] - dr[b][k]) : (double)(dr[b][k] - dr[c][k]);
+          ++nn;
+        }
+    }
+    if (!hi) continue;
+    printf("plane z0+%3d: %zu blocks, spread %llu x10ns, mean |x-neighbour lag| %.0f x10ns\n", 32 * k,
+           bs.size(), hi - lo, nn ? nb / nn : 0.0);
   }
 #endif
   return 0;
