@@ -124,6 +124,18 @@ int main(int argc, char **argv) {
   std::vector<int> bs;
   for (int b = 0; b < 2048; ++b)
     if (dr[b][0]) bs.push_back(b);
+  {  // time over the first 128 steps, interior vs edge tiles
+    double ti = 0, te = 0;
+    int ni = 0, ne = 0;
+    for (int b : bs) {
+      if (!dr[b][4]) continue;
+      const double d = (double)(dr[b][4] - dr[b][0]);
+      const bool edge = tl[b][0] <= 3 || tl[b][0] + 64 + 3 >= n || tl[b][1] <= 3 || tl[b][1] + 22 + 3 >= n;
+      if (edge) { te += d; ++ne; } else { ti += d; ++ni; }
+    }
+    printf("128 steps: interior tiles %.0f x10ns (%d), edge tiles %.0f x10ns (%d)\n", ni ? ti / ni : 0.0, ni,
+           ne ? te / ne : 0.0, ne);
+  }
   for (int k = 0; k < 16; ++k) {
     unsigned long long lo = ~0ull, hi = 0;
     double nb = 0;
