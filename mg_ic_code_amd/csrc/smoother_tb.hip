@@ -10,14 +10,15 @@
 // fused sweep.
 //
 // Pipeline.  A workgroup owns a TX x TY (x, y) tile and streams a chunk of
-// z planes through a 6-plane LDS ring (red and black element of every x pair
+// z planes through an 8-slot LDS ring (red and black element of every x pair
 // in separate arrays, so every LDS access is stride 1).  At step p it runs
 // four colour passes on four planes, each on the tile grown by the cells the
 // later passes read:
 //     sweep-1 red   plane p     tile + 3
 //     sweep-1 black plane p-1   tile + 2
-//     sweep-2 red   plane p-2   tile + 1
-//     sweep-2 black plane p-3   tile        -> stored
+//     sweep-2 red   plane p-3   tile + 1
+//     sweep-2 black plane p-4   tile        -> stored
+// (two barriers per step: the red passes, then the black ones)
 // Every pass updates the ring array in place (red and black cells are
 // disjoint), so one copy of each plane suffices.
 //
@@ -70,12 +71,8 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_PROBE_SKIP
 #define TB2_PROBE_SKIP 0
 #endif
-// measurement switches (A/B builds): TB2_ROT 1 = coefficient sets moved down
-// one register set per step in a 2-step loop (round 2's first form);
-// TB2_NO_READ2 1 = x-neighbour pairs as two ds_read_b64
-#ifndef TB2_ROT
-#define TB2_ROT 0
-#endif
+// measurement switches (A/B builds): TB2_NO_READ2 1 = x-neighbour pairs as
+// two ds_read_b64
 #ifndef TB2_NO_READ2
 #define TB2_NO_READ2 0
 #endif
@@ -276,7 +273,8 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
   // later), black of planes p-1 .. p-4 (made one step later from rb / ab);
-  // moved down one plane at the end of every step
+  // set J of the 4-step unrolled loop is made at step J and last used at
+  // step J + 3
   double Rr[4][NP], Ra[4][NP], Rl[4][NP], Br[4][NP], Ba[4][NP], Bl[4][NP];
   double rb[NP], ab[NP];
   double ac0[NP], ac1[NP], an0[NP], an1[NP];  // ACC: acc pairs of planes p-4 / p-3
@@ -476,7 +474,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     // coefficient sets live in slot J (made this step) .. slot J3 (made
     // three steps ago, last use), so no register moves between steps
     constexpr int J = decltype(tc)::value, T = J & 1, U = T ^ 1;
-    constexpr int J0 = TB2_ROT ? 0 : J, J3 = TB2_ROT ? 3 : (J + 1) & 3;
+    constexpr int J0 = J, J3 = (J + 1) & 3;
     constexpr int FB = PF == 2 ? (J & 1) : 0;  // in-flight register set consumed / refilled
     using ICF = IC<FB>;
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
@@ -525,19 +523,6 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     TB2_STAMP(5, p);
     store((sl + 4) & 7, T, p - 4);
     TB2_STAMP(6, p);
-    // TB2_ROT (the round-1 form): every set moves down one plane
-#pragma unroll
-    for (int i = 0; i < NP && TB2_ROT; ++i) {
-#pragma unroll
-      for (int j = 3; j > 0; --j) {
-        Rr[j][i] = Rr[j - 1][i];
-        Ra[j][i] = Ra[j - 1][i];
-        Rl[j][i] = Rl[j - 1][i];
-        Br[j][i] = Br[j - 1][i];
-        Ba[j][i] = Ba[j - 1][i];
-        Bl[j][i] = Bl[j - 1][i];
-      }
-    }
   };
 
   fetch_u(1, pstart - 1, IC<0>{});
@@ -552,12 +537,6 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     fetch_u(0, pstart + 2, IC<PF - 1>{});
     fetch_c(1, pstart + 1, IC<PF - 1>{});
   }
-#if TB2_ROT
-  for (int p = pstart; p <= pend; p += 2) {
-    step(IC<0>{}, p);
-    step(IC<1>{}, p + 1);
-  }
-#else
   // (up to three steps past pend: their passes and stores fall outside every
   // range test, their loads are clamped)
   for (int p = pstart; p <= pend; p += 4) {
@@ -566,7 +545,6 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     step(IC<2>{}, p + 2);
     step(IC<3>{}, p + 3);
   }
-#endif
 }
 
 
