@@ -1199,10 +1199,22 @@ void bicg_p(double *p, const double *v, const double *r, double beta, double c, 
   check_launch();
 }
 
+// Blocks per item (grid.y = item): sized for the largest item at
+// copy_ept() elements per thread, so the many small items (edges, corners of
+// a ghost shell) do not each launch the largest item's share of empty blocks
+int copy_ept() {
+  static const int ept = [] {
+    const char *e = getenv("MGIC_COPY_EPT");
+    const int v = e ? atoi(e) : 4;
+    return v > 0 ? v : 1;
+  }();
+  return ept;
+}
 void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *const *src_tab,
                 const double *src_buf, double *const *dst_tab, double *dst_buf, hipStream_t st) {
   if (nitems <= 0 || max_cells <= 0) return;
-  long bx = (max_cells + 255) / 256;
+  const long per = 256L * copy_ept();
+  long bx = (max_cells + per - 1) / per;
   if (bx > 1024) bx = 1024;
   k_copy_items<double><<<dim3((unsigned)bx, (unsigned)nitems), dim3(256), 0, st>>>(
       d_items, src_tab, src_buf, dst_tab, dst_buf);
@@ -1314,7 +1326,8 @@ void prolong_f(float *uf, const BoxArgs &fg, const float *ec, const BoxArgs &cg,
 void copy_items_f(const CopyItem *d_items, int nitems, long max_cells, float *const *src_tab,
                   const float *src_buf, float *const *dst_tab, float *dst_buf, hipStream_t st) {
   if (nitems <= 0 || max_cells <= 0) return;
-  long bx = (max_cells + 255) / 256;
+  const long per = 256L * copy_ept();
+  long bx = (max_cells + per - 1) / per;
   if (bx > 1024) bx = 1024;
   k_copy_items<float><<<dim3((unsigned)bx, (unsigned)nitems), dim3(256), 0, st>>>(
       d_items, src_tab, src_buf, dst_tab, dst_buf);
