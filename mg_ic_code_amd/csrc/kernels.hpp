@@ -61,6 +61,9 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
                     hipStream_t st);
+// the same two-sweep launch on fp32 fields (no phi += e)
+void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
+                      const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st);
 long gsrb_block_max_cells();
 // two red+black sweeps u_in -> u_out in one z-streaming launch (128x16
 // tiles, 6-plane LDS ring, coefficients carried in registers): boxes whose

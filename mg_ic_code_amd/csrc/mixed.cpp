@@ -85,19 +85,32 @@ void MixedMultiGrid::relax(int d, LevelDataF &e, const LevelDataF &r, int n, boo
     }
     return;
   }
-  for (int it = 0; it < n; ++it) {
+  // two sweeps per launch (the temporally blocked kernel, smoother_tb.hip)
+  // on levels without exchanged faces; a last sweep that folds phi += e
+  // into fp64 stays a single sweep
+  bool two = !L.halo && n >= 2;
+  for (int b = 0; two && b < op.grid->nlocal(); ++b)
+    two = kern::gsrb_sweep_tb2_applies(op.boxArgs(b, true), L.s, kind);
+  for (int it = 0; it < n;) {
     const bool zin = zero_in && it == 0;
-    const bool last = it == n - 1;
+    const int left = n - it;
+    const int k = two && (left >= 3 || (left == 2 && !acc)) ? 2 : 1;
+    const bool last = it + k == n;
     if (L.halo && !zin) src->exchange_shell(st);
     for (int b = 0; b < op.grid->nlocal(); ++b) {
       const long nc = op.grid->geom[b].valid.ncells();
-      prof_mark(st, nc, true, 2);
-      kern::gsrb_sweep_fused_f(dst->p[b], src->p[b], r.p[b], L.a->p[b], L.b->p[b],
-                               op.boxArgs(b, true), L.s, zin, last && acc ? acc->p[b] : nullptr,
-                               kind, st);
-      prof_mark(st, nc, false, 2);
+      prof_mark(st, nc, true, 2 * k);
+      if (k == 2)
+        kern::gsrb_sweep_tb2_f(dst->p[b], src->p[b], r.p[b], L.a->p[b], op.boxArgs(b, true), L.s,
+                               zin, st);
+      else
+        kern::gsrb_sweep_fused_f(dst->p[b], src->p[b], r.p[b], L.a->p[b], L.b->p[b],
+                                 op.boxArgs(b, true), L.s, zin, last && acc ? acc->p[b] : nullptr,
+                                 kind, st);
+      prof_mark(st, nc, false, 2 * k);
     }
     std::swap(src, dst);
+    it += k;
   }
   if (acc) return;
   if (src != &e)

@@ -115,36 +115,57 @@ struct TB2 {
 // exactly (c - v == c + (-v); v + (-0.0) == v for every v, signed zeros
 // included), with sign/gc per domain face
 // (built on the host, one per face, so the kernel holds no BC-mode logic)
+template <class T>
 struct TB2Ghosts {
-  double c[6];
-  unsigned sgn[6];  // 0x80000000: negate v (Dirichlet)
+  T c[6];
+  unsigned sgn[6];  // 0x80000000: negate v (Dirichlet; the sign bit of T's top word)
 };
-TB2Ghosts make_ghosts(const BoxArgs &g) {
-  TB2Ghosts r{};
+template <class T>
+TB2Ghosts<T> make_ghosts(const BoxArgs &g) {
+  TB2Ghosts<T> r{};
   for (int f = 0; f < 6; ++f) {
     const int mode = g.bcm[f];
     r.sgn[f] = mode == kBcDirichlet ? 0x80000000u : 0u;
-    r.c[f] = mode == kBcNeumannHom ? -0.0 : g.bcc[f];
+    r.c[f] = mode == kBcNeumannHom ? (T)-0.0 : (T)g.bcc[f];
   }
   return r;
 }
-__device__ __forceinline__ double ghost(const TB2Ghosts &gg, int f, double v) {
+__device__ __forceinline__ double ghost(const TB2Ghosts<double> &gg, int f, double v) {
   const long long b = __double_as_longlong(v) ^ ((long long)gg.sgn[f] << 32);
   return __longlong_as_double(b) + gg.c[f];
 }
+__device__ __forceinline__ float ghost(const TB2Ghosts<float> &gg, int f, float v) {
+  return __uint_as_float(__float_as_uint(v) ^ gg.sgn[f]) + gg.c[f];
+}
+
+// the stencil constants rounded to T once (identity for double), as the
+// single-sweep kernels' SC<T> (smoother.hip) and oracle/mixed.py do
+template <class T>
+struct TB2Coefs {
+  T alpha, beta, dxinv, lamshift, bval;
+  __device__ explicit TB2Coefs(const StencilCoefs &s)
+      : alpha((T)s.alpha), beta((T)s.beta), dxinv((T)s.dxinv), lamshift((T)s.lamshift),
+        bval((T)s.bval) {}
+};
+template <class T> struct TB2Vec;
+template <> struct TB2Vec<double> { using type = double2; };
+template <> struct TB2Vec<float> { using type = float2; };
 
 // One tile (x0, y0) of the box, planes [z0, z1).  FAST: alpha == 1, beta ==
 // -1, bval == 1 (exact specialisation, see above); EDGE: the tile's rings
 // reach an x / y domain face (BC code compiled in).
-template <int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE>
-__device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restrict__ B,
-                                         double *__restrict__ uo, double *__restrict__ acc,
-                                         const double *__restrict__ ui,
-                                         const double *__restrict__ rhs,
-                                         const double *__restrict__ a, const BoxArgs &g,
-                                         const StencilCoefs &s, const TB2Ghosts &gg, int x0,
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE>
+__device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
+                                         T *__restrict__ uo, double *__restrict__ acc,
+                                         const T *__restrict__ ui,
+                                         const T *__restrict__ rhs,
+                                         const T *__restrict__ a, const BoxArgs &g,
+                                         const StencilCoefs &s64, const TB2Ghosts<T> &gg, int x0,
                                          int y0, int z0, int z1, int ef) {
+  static_assert(!ACC || std::is_same<T, double>::value, "phi += e is folded into fp64 sweeps only");
   using F = TB2<TX, TY, NT>;
+  using V = typename TB2Vec<T>::type;
+  const TB2Coefs<T> s(s64);
   constexpr int PW = F::PW, CP = F::CP, SS = F::SS, UW = F::UW, NRP = F::NRP, NL = F::NL,
                 NP = F::NP;
   const int nx = g.nx, ny = g.ny, nz = g.nz;
@@ -165,7 +186,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // a uniform 64-bit plane base + a 32-bit lane offset
   const long corner = -16 - 4 * sy;
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
-  auto plane = [&](const double *f, int p) {  // corner of (clamped) plane p
+  auto plane = [&](const T *f, int p) {  // corner of (clamped) plane p
     return reinterpret_cast<const char *>(f + corner + (long)clampi(p, -4, nz + 3) * sz);
   };
   // the lane offset is laundered per access: otherwise the compiler hoists
@@ -174,10 +195,10 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // uniform plane base + 32-bit offset form
   auto at2 = [](const char *base, unsigned off) {
     asm volatile("" : "+v"(off));
-    return *reinterpret_cast<const double2 *>(base + off);
+    return *reinterpret_cast<const V *>(base + off);
   };
   auto boff = [&](int x, int y) {  // byte offset of cell (x, y) from the corner
-    return (unsigned)(8 * (16 + x + (long)(y + 4) * sy));
+    return (unsigned)(sizeof(T) * (16 + x + (long)(y + 4) * sy));
   };
 
   // ---- loads of u (slot c = LDS pair index), per plane parity t ----------
@@ -268,15 +289,15 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // plane p+1 while step p runs; PF 2: planes p+3 / p+2, one register set
   // per step parity)
   constexpr int PF = (TB2_PF2 && !ACC) ? 2 : 1;
-  double pu0[PF][NL], pu1[PF][NL];
-  double nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
+  T pu0[PF][NL], pu1[PF][NL];
+  T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
   // later), black of planes p-1 .. p-4 (made one step later from rb / ab);
   // set J of the 4-step unrolled loop is made at step J and last used at
   // step J + 3
-  double Rr[4][NP], Ra[4][NP], Rl[4][NP], Br[4][NP], Ba[4][NP], Bl[4][NP];
-  double rb[NP], ab[NP];
+  T Rr[4][NP], Ra[4][NP], Rl[4][NP], Br[4][NP], Ba[4][NP], Bl[4][NP];
+  T rb[NP], ab[NP];
   double ac0[NP], ac1[NP], an0[NP], an1[NP];  // ACC: acc pairs of planes p-4 / p-3
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
@@ -295,7 +316,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
         pu0[b][i] = 0.0;
         pu1[b][i] = 0.0;
       } else if (NL * NT <= CP || tid + i * NT < CP) {  // (whole waves past the plane skip)
-        const double2 v = at2(pl, loff[t][i]);
+        const V v = at2(pl, loff[t][i]);
         pu0[b][i] = v.x;
         pu1[b][i] = v.y;
       }
@@ -316,7 +337,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   };
   auto put = [&](int sl, auto bc) {  // into ring slot sl: red element -> R, black -> B
     constexpr int b = decltype(bc)::value;
-    double *Rs = R + sl * SS, *Bs = B + sl * SS;
+    T *Rs = R + sl * SS, *Bs = B + sl * SS;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (NL * NT > CP && tid + i * NT >= CP) continue;  // whole waves past the plane
@@ -336,27 +357,27 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
         na1[b][i] = -1.25;
         continue;
       }
-      const double2 vr = at2(pr, roff[t][i]);
-      const double2 va = at2(pa, roff[t][i]);
+      const V vr = at2(pr, roff[t][i]);
+      const V va = at2(pa, roff[t][i]);
       nr0[b][i] = vr.x;
       nr1[b][i] = vr.y;
       na0[b][i] = va.x;
       na1[b][i] = va.y;
     }
   };
-  auto lam = [&](double aa) { return (TB2_PROBE_SKIP & 64) ? aa + s.lamshift : 1.0 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
-  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
-                 double rv, double aa, double lm) -> double {
+  auto lam = [&](T aa) { return (TB2_PROBE_SKIP & 64) ? aa + s.lamshift : (T)1 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
+  auto upd = [&](T uc, T xm, T xp, T ym, T yp, T zm, T zp,
+                 T rv, T aa, T lm) -> T {
     if (TB2_PROBE_SKIP & 32) return ((uc + xm) + (xp + ym)) + ((yp + zm) + zp);
-    const double tx = (xp + xm) - 2.0 * uc;
-    const double ty = (yp + ym) - 2.0 * uc;
-    const double tz = (zp + zm) - 2.0 * uc;
-    const double lap = (tx + ty) + tz;  // .ChF:111-120
-    double lofdpsi = aa * uc;           // .ChF:107-108
+    const T tx = (xp + xm) - (T)2 * uc;
+    const T ty = (yp + ym) - (T)2 * uc;
+    const T tz = (zp + zm) - (T)2 * uc;
+    const T lap = (tx + ty) + tz;  // .ChF:111-120
+    T lofdpsi = aa * uc;           // .ChF:107-108
     if (FAST) {
       lofdpsi = lofdpsi + lap * s.dxinv;  // .ChF:122-124 with bCoef 1, beta -1
     } else {
-      const double ldpsi = lap * s.dxinv * s.bval;  // .ChF:122
+      const T ldpsi = lap * s.dxinv * s.bval;  // .ChF:122
       lofdpsi = lofdpsi - s.beta * ldpsi;           // .ChF:124
     }
     return uc - lm * (lofdpsi - rv);  // .ChF:127-128
@@ -370,19 +391,19 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   // face cell takes its ghost neighbour as ghost(its own value) in registers
   // (branch-free selects), so x / y ghosts are never stored or loaded.  z
   // ghosts (face planes of z chunks only) are still written into the ring.
-  auto pass = [&](bool red, int W, int sl, int t, int k, const double (&cr)[NP],
-                  const double (&ca)[NP], const double (&cl)[NP]) {
+  auto pass = [&](bool red, int W, int sl, int t, int k, const T (&cr)[NP],
+                  const T (&ca)[NP], const T (&cl)[NP]) {
     if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
     // rows beyond ring W (distance > W from the tile) are never read once
     // this pass is done, so waves holding only such rows skip it
     if (W < 3 && wv < 3 - W) return;
     if ((TB2_PROBE_SKIP & 8) && red) return;
     if ((TB2_PROBE_SKIP & 16) && !red) return;
-    double *X = (red ? R : B) + sl * SS;
-    double *N = (red ? B : R) + sl * SS;
-    double *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
-    double *Np = (red ? B : R) + ((sl + 1) & 7) * SS;
-    double uc[NP], xm[NP], xp[NP], ym[NP], yp[NP], zm[NP], zp[NP];
+    T *X = (red ? R : B) + sl * SS;
+    T *N = (red ? B : R) + sl * SS;
+    T *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
+    T *Np = (red ? B : R) + ((sl + 1) & 7) * SS;
+    T uc[NP], xm[NP], xp[NP], ym[NP], yp[NP], zm[NP], zp[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int c = ci[i];
@@ -415,7 +436,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
         if (ef & 8) yp[i] = (f & 8) ? ghost(gg, 3, uc[i]) : yp[i];
       }
     }
-    double v[NP];
+    T v[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) v[i] = upd(uc[i], xm[i], xp[i], ym[i], yp[i], zm[i], zp[i], cr[i], ca[i], cl[i]);
 #pragma unroll
@@ -423,7 +444,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     const bool zl = k == zfl, zh = k == zfh;
     if (zl || zh) {  // z ghosts of the face plane (every lane: an element
                      // never updated owns its ghost alone)
-      double *Nz = zl ? Nm : Np;
+      T *Nz = zl ? Nm : Np;
       const int zf = zl ? 4 : 5;
 #pragma unroll
       for (int i = 0; i < NP; ++i) Nz[ci[i] + yzo[t][i] + (red ? 0 : 1)] = ghost(gg, zf, v[i]);
@@ -438,27 +459,28 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
   auto store = [&](int sl, int t, int k) {
     if (TB2_PROBE_SKIP & 4) return;
     const bool kin = k >= z0 && k < z1;  // uniform
-    char *dst = reinterpret_cast<char *>((ACC ? acc : uo) + corner + (long)clampi(k, z0, z1 - 1) * sz);
+    char *dst = ACC ? reinterpret_cast<char *>(acc + corner + (long)clampi(k, z0, z1 - 1) * sz)
+                    : reinterpret_cast<char *>(uo + corner + (long)clampi(k, z0, z1 - 1) * sz);
     const __amdgpu_buffer_rsrc_t rs = sweep::store_rsrc(dst);
     constexpr unsigned kDrop = sweep::kDrop;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int st = kin ? (rinf[t][i] >> 8) & 3 : 0;
-      double2 w;
+      V w;
       w.x = R[sl * SS + ci[i]];
       w.y = B[sl * SS + ci[i]];
-      if (ACC) {  // phi += e (incr, scale 1) in the same pass
+      if constexpr (ACC) {  // phi += e (incr, scale 1) in the same pass
         w.x = ac0[i] + w.x;
         w.y = ac1[i] + w.y;
       }
       const unsigned off = roff[t][i];
-      // both elements (st 3) as one 16-B store; a single one (st 1 / 2, the
-      // tile's x edges) as an 8-B store
+      // both elements (st 3) as one pair store; a single one (st 1 / 2, the
+      // tile's x edges) as an element store
       const unsigned o4 = st == 3 ? off : kDrop;
-      const unsigned o2 = st == 1 ? off : (st == 2 ? off + 8 : kDrop);
-      const double e = st == 1 ? w.x : w.y;
-      sweep::bstore<TB2_STORE_CPOL>(rs, w, o4);
-      sweep::bstore<TB2_STORE_CPOL>(rs, e, o2);
+      const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
+      const T e = st == 1 ? w.x : w.y;
+      sweep::bstore(rs, w, o4);
+      sweep::bstore(rs, e, o2);
     }
   };
   // One pipeline step at plane p (t: its parity relative to pstart; slot
@@ -473,7 +495,7 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     // J: position in the 4-step unrolled loop; T / U: parity of p / of p +- 1;
     // coefficient sets live in slot J (made this step) .. slot J3 (made
     // three steps ago, last use), so no register moves between steps
-    constexpr int J = decltype(tc)::value, T = J & 1, U = T ^ 1;
+    constexpr int J = decltype(tc)::value, PT = J & 1, PU = PT ^ 1;
     constexpr int J0 = J, J3 = (J + 1) & 3;
     constexpr int FB = PF == 2 ? (J & 1) : 0;  // in-flight register set consumed / refilled
     using ICF = IC<FB>;
@@ -495,33 +517,33 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
     }
     image(p + 1, ICF{});
     put((sl + 1) & 7, ICF{});
-    if (PF == 2) fetch_c(T, p + 2, ICF{});
-    else fetch_c(U, p + 1, ICF{});
-    if (ACC) {
+    if (PF == 2) fetch_c(PT, p + 2, ICF{});
+    else fetch_c(PU, p + 1, ICF{});
+    if constexpr (ACC) {
       const char *pl = plane(acc, p - 3);
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         ac0[i] = an0[i];
         ac1[i] = an1[i];
-        const double2 v = at2(pl, roff[U][i]);
+        const double2 v = at2(pl, roff[PU][i]);
         an0[i] = v.x;
         an1[i] = v.y;
       }
     }
-    if (PF == 2) fetch_u(U, p + 3, ICF{});
-    else fetch_u(T, p + 2, ICF{});
+    if (PF == 2) fetch_u(PU, p + 3, ICF{});
+    else fetch_u(PT, p + 2, ICF{});
     TB2_STAMP(1, p);
     __syncthreads();
     TB2_STAMP(2, p);
-    pass(true, 3, sl, T, p, Rr[J0], Ra[J0], Rl[J0]);
-    pass(true, 1, (sl + 5) & 7, U, p - 3, Rr[J3], Ra[J3], Rl[J3]);
+    pass(true, 3, sl, PT, p, Rr[J0], Ra[J0], Rl[J0]);
+    pass(true, 1, (sl + 5) & 7, PU, p - 3, Rr[J3], Ra[J3], Rl[J3]);
     TB2_STAMP(3, p);
     __syncthreads();
     TB2_STAMP(4, p);
-    pass(false, 2, (sl + 7) & 7, U, p - 1, Br[J0], Ba[J0], Bl[J0]);
-    pass(false, 0, (sl + 4) & 7, T, p - 4, Br[J3], Ba[J3], Bl[J3]);
+    pass(false, 2, (sl + 7) & 7, PU, p - 1, Br[J0], Ba[J0], Bl[J0]);
+    pass(false, 0, (sl + 4) & 7, PT, p - 4, Br[J3], Ba[J3], Bl[J3]);
     TB2_STAMP(5, p);
-    store((sl + 4) & 7, T, p - 4);
+    store((sl + 4) & 7, PT, p - 4);
     TB2_STAMP(6, p);
   };
 
@@ -548,18 +570,18 @@ __device__ __forceinline__ void tb2_tile(double *__restrict__ R, double *__restr
 }
 
 
-template <int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST>
-__global__ __launch_bounds__(NT) void k_gsrb_tb2(double *__restrict__ uo,
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST>
+__global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  double *__restrict__ acc,
-                                                 const double *__restrict__ ui,
-                                                 const double *__restrict__ rhs,
-                                                 const double *__restrict__ a,
+                                                 const T *__restrict__ ui,
+                                                 const T *__restrict__ rhs,
+                                                 const T *__restrict__ a,
                                                  const BoxArgs g, const StencilCoefs s,
-                                                 const TB2Ghosts gg, int kc, int ntx, int nty,
+                                                 const TB2Ghosts<T> gg, int kc, int ntx, int nty,
                                                  int nblocks) {
   using F = TB2<TX, TY, NT>;
-  __shared__ double R[F::NS * F::SS];  // red element of every pair, 8 plane slots
-  __shared__ double B[F::NS * F::SS];  // black element
+  __shared__ T R[F::NS * F::SS];  // red element of every pair, 8 plane slots
+  __shared__ T B[F::NS * F::SS];  // black element
   const int L = sweep::xcd_tile(blockIdx.x, nblocks);
   const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
   const int z0 = (L / (ntx * nty)) * kc;
@@ -568,21 +590,21 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(double *__restrict__ uo,
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
   if (ef)
-    tb2_tile<TX, TY, NT, ZIN, ACC, FAST, true>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
                                                z1, ef);
   else
-    tb2_tile<TX, TY, NT, ZIN, ACC, FAST, false>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
                                                 z1, 0);
 }
 
-template <int TX, int TY, int NT>
+template <class T, int TX, int TY, int NT>
 int tb2_resident_slots() {
   static const int slots = [] {
     int dev = 0, ncu = 0, per = 0;
     MGIC_HIP(hipGetDevice(&dev));
     MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     MGIC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per, k_gsrb_tb2<TX, TY, NT, false, false, true>, NT, 0));
+        &per, k_gsrb_tb2<T, TX, TY, NT, false, false, true>, NT, 0));
     return (per > 0 ? per : 1) * (ncu > 0 ? ncu : 1);
   }();
   return slots;
@@ -605,29 +627,32 @@ int tb2_choose_kc(int tiles, int nz, int slots) {
   return best;
 }
 
-template <int TX, int TY, int NT>
-void launch_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
-                const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
-                hipStream_t st) {
+template <class T, int TX, int TY, int NT>
+void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs &g,
+                const StencilCoefs &s, bool zero_in, double *acc, hipStream_t st) {
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
   static const int kc_env = [] {
     const char *e = getenv("MGIC_TB2_KC");
     return e ? atoi(e) : 0;
   }();
   int kc = kc_env >= 8 ? (kc_env < g.nz ? kc_env : g.nz)
-                       : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<TX, TY, NT>());
+                       : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<T, TX, TY, NT>());
   const int ntz = (g.nz + kc - 1) / kc;
   const int nblocks = ntx * nty * ntz;
   const dim3 grid((unsigned)nblocks), block(NT);
   const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0;
-  const TB2Ghosts gg = make_ghosts(g);
-#define MGIC_TB2(Z, A, FA)                                                                     \
-  k_gsrb_tb2<TX, TY, NT, Z, A, FA><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, g, s, gg, \
-                                                           kc, ntx, nty, nblocks)
+  const TB2Ghosts<T> gg = make_ghosts<T>(g);
+#define MGIC_TB2(Z, A, FA)                                                                        \
+  k_gsrb_tb2<T, TX, TY, NT, Z, A, FA><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, g, s, gg, \
+                                                              kc, ntx, nty, nblocks)
   if (acc) {
-    if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
-    if (fast) MGIC_TB2(false, true, true);
-    else MGIC_TB2(false, true, false);
+    if constexpr (std::is_same<T, double>::value) {
+      if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
+      if (fast) MGIC_TB2(false, true, true);
+      else MGIC_TB2(false, true, false);
+    } else {
+      throw Error(kBadArg, "two-sweep launch: phi += e is folded into fp64 sweeps only");
+    }
   } else if (zero_in) {
     if (fast) MGIC_TB2(true, false, true);
     else MGIC_TB2(true, false, false);
@@ -667,8 +692,17 @@ void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const 
     const char *e = getenv("MGIC_TB2_VARIANT");
     return e ? atoi(e) : 0;
   }();
-  if (v == 1) launch_tb2<64, 22, 512>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
-  else launch_tb2<64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+  if (v == 1) launch_tb2<double, 64, 22, 512>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+  else launch_tb2<double, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+}
+
+// fp32 (the mixed-precision V-cycle's smoother, BASELINE config C5): the same
+// kernel on floats with the stencil constants rounded to float once, as the
+// single-sweep fp32 kernel and oracle/mixed.py compute them (phi += e stays a
+// separate fp64 sweep there)
+void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
+                      const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st) {
+  launch_tb2<float, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, nullptr, st);
 }
 
 }  // namespace kern
