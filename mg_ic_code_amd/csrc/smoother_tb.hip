@@ -241,6 +241,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     const int c = tid + i * NT, jt = c - MAIN;
     // wave w takes rows w and NR-1-w (one per 32-lane half), so the waves
     // of the outer rows -- idle in the inner rings' passes -- skip them whole
+    // (with one pair per lane; NP > 1 keeps the mapping, not the skipping)
     const int rr = c < MAIN ? (((c >> 5) & 1) ? NR - 1 - (c >> 6) : (c >> 6)) : jt / (UW - 32);
     const int m = c < MAIN ? 1 + (c & 31) : 33 + jt - (jt / (UW - 32)) * (UW - 32);
     const int gy = y0 - 3 + rr;
@@ -396,7 +397,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
     // rows beyond ring W (distance > W from the tile) are never read once
     // this pass is done, so waves holding only such rows skip it
-    if (W < 3 && wv < 3 - W) return;
+    if (NP == 1 && W < 3 && wv < 3 - W) return;  // (one pair per lane only)
     if ((TB2_PROBE_SKIP & 8) && red) return;
     if ((TB2_PROBE_SKIP & 16) && !red) return;
     T *X = (red ? R : B) + sl * SS;

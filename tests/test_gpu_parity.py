@@ -706,17 +706,18 @@ print("two-sweep OK")
 """
 
 
-@pytest.mark.parametrize("spl", ["4", "2"])
-def test_two_sweep_kernel_vcycle_bitwise(spl):
+@pytest.mark.parametrize("spl,variant", [("4", "0"), ("2", "0"), ("2", "1")])
+def test_two_sweep_kernel_vcycle_bitwise(spl, variant):
     # the two-sweep kernels (MGIC_SWEEPS_PER_LAUNCH, read once per process: a
     # child process): 4 = round 1's 128x16 kernel, 2 = smoother_tb.hip (the
-    # default); odd and even sweep counts, ragged mixed-BC box and a cube,
-    # against the oracle bit for bit
+    # default; MGIC_TB2_VARIANT 1 = its 512-thread form with two pairs per
+    # lane, where whole waves never skip a pass); odd and even sweep counts,
+    # ragged mixed-BC box and a cube, against the oracle bit for bit
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MGIC_SWEEPS_PER_LAUNCH=spl)
+    env = dict(os.environ, MGIC_SWEEPS_PER_LAUNCH=spl, MGIC_TB2_VARIANT=variant)
     r = subprocess.run([sys.executable, "-c", _TWO_SWEEPS_CHILD, root], env=env,
                        capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
