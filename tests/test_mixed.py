@@ -162,6 +162,34 @@ def test_mixed_streaming_multi_tile_bitwise(comm):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_pre,n_post", [(1, 1), (2, 3), (3, 2), (5, 4)])
+def test_mixed_sweep_counts_bitwise(comm, n_pre, n_post):
+    # the fp32 relax in pairs through the two-sweep kernel (fused_smoother =
+    # 2: streaming at every depth) with odd and even counts: single sweeps
+    # for the odd remainder and for the last post-sweep that folds phi += e
+    # into fp64, against the float32 restatement bit for bit
+    import mg_ic_code_amd as mg
+    rng = np.random.default_rng(12)
+    shape = (72, 48, 40)
+    lo = (8, -16, 0)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    dx = 0.3
+    bc_lo, bc_hi, bcv = (1, 0, 0), (0, 0, 1), -0.5
+    a, b, rhs = _problem(rng, shape, False)
+    S = _gpu(comm, dom, [dom], dx, a, b, rhs, 2, 2, bc_lo, bc_hi, bcv)
+    sp = mg.SolverParams(max_depth=1, bottom_solver=0, n_pre=n_pre, n_post=n_post,
+                         n_bottom=n_pre + n_post)
+    mm = mg.MixedMultiGrid(S["fac"], sp)
+    m = MixedOracle(_oracle(dom, dx, a, b, rhs, 2, bc_lo, bc_hi, bcv), 1.0, -1.0, bc_lo, bc_hi,
+                    n_pre=n_pre, n_post=n_post, n_bottom=n_pre + n_post)
+    assert mm.init_residual(S["fphi"], S["frhs"], S["fres"], 0) == \
+        np.abs(m.init_residual(np.zeros(shape[::-1]))).max()
+    for _ in range(2):
+        assert mm.iteration(S["fphi"], S["frhs"], S["fres"], 0) == np.abs(m.iteration()).max()
+    assert np.array_equal(_phi(S), m.phi)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rccl", [False, True])
 def test_mixed_multibox_matches_single_box(rccl):
     import mg_ic_code_amd as mg
