@@ -84,6 +84,10 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_STORE_CPOL
 #define TB2_STORE_CPOL 0
 #endif
+// TB2_ZIN_SHORT 0 = ZIN launches run sweep 1 through the generic passes
+#ifndef TB2_ZIN_SHORT
+#define TB2_ZIN_SHORT 1
+#endif
 
 // Geometry.  Rows of the LDS ring are SHIFTED pairings: in row y of plane k
 // pair m holds cells (X, X+1) with X = x0 - 6 + 2m + s, s = (x0 + y + k +
@@ -392,8 +396,17 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // face cell takes its ghost neighbour as ghost(its own value) in registers
   // (branch-free selects), so x / y ghosts are never stored or loaded.  z
   // ghosts (face planes of z chunks only) are still written into the ring.
-  auto pass = [&](bool red, int W, int sl, int t, int k, const T (&cr)[NP],
+  // zc (ZIN launches only): 1 = sweep-1 red, 2 = sweep-1 black.  On a zero
+  // input under homogeneous BCs (launch_tb2 checks) sweep-1 red sees u = 0
+  // and six neighbours that are +-0 (loaded zeros, ParseBC's images of
+  // them), so .ChF:107-128 reduce exactly to 0 - lam * (0 - rhs): lofdpsi
+  // is +-0, (+-0 - rhs) == -rhs for rhs != 0 and +-0 otherwise, which gives
+  // +0 either way.  Sweep-1 black starts from its own u = 0 (the constant
+  // lets x - 2*0 fold to x, exact).  Both skip the LDS reads they no longer
+  // need.
+  auto pass = [&](auto zc, bool red, int W, int sl, int t, int k, const T (&cr)[NP],
                   const T (&ca)[NP], const T (&cl)[NP]) {
+    constexpr int ZC = decltype(zc)::value;
     if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
     // rows beyond ring W (distance > W from the tile) are never read once
     // this pass is done, so waves holding only such rows skip it
@@ -404,12 +417,27 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     T *N = (red ? B : R) + sl * SS;
     T *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
     T *Np = (red ? B : R) + ((sl + 1) & 7) * SS;
+    if constexpr (ZC == 1) {
+      T v[NP];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) v[i] = (T)0 - cl[i] * ((T)0 - cr[i]);
+#pragma unroll
+      for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> 10) & 1 ? v[i] : (T)0;
+      const bool zl = k == zfl, zh = k == zfh;
+      if (zl || zh) {
+        T *Nz = zl ? Nm : Np;
+        const int zf = zl ? 4 : 5;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) Nz[ci[i] + yzo[t][i]] = ghost(gg, zf, v[i]);
+      }
+      return;
+    }
     T uc[NP], xm[NP], xp[NP], ym[NP], yp[NP], zm[NP], zp[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int c = ci[i];
       const int o = yzo[t][i] + (red ? 0 : 1);  // y / z neighbours: pair m-1+s (red), m+s (black)
-      uc[i] = X[c];
+      uc[i] = ZC == 2 ? (T)0 : X[c];
 #if TB2_NO_READ2
       // separate ds_read_b64s: a ds_read2_b64 of the adjacent pair costs 8
       // LDS cycles against 2 x 2
@@ -536,13 +564,13 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     TB2_STAMP(1, p);
     __syncthreads();
     TB2_STAMP(2, p);
-    pass(true, 3, sl, PT, p, Rr[J0], Ra[J0], Rl[J0]);
-    pass(true, 1, (sl + 5) & 7, PU, p - 3, Rr[J3], Ra[J3], Rl[J3]);
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, true, 3, sl, PT, p, Rr[J0], Ra[J0], Rl[J0]);
+    pass(IC<0>{}, true, 1, (sl + 5) & 7, PU, p - 3, Rr[J3], Ra[J3], Rl[J3]);
     TB2_STAMP(3, p);
     __syncthreads();
     TB2_STAMP(4, p);
-    pass(false, 2, (sl + 7) & 7, PU, p - 1, Br[J0], Ba[J0], Bl[J0]);
-    pass(false, 0, (sl + 4) & 7, PT, p - 4, Br[J3], Ba[J3], Bl[J3]);
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, false, 2, (sl + 7) & 7, PU, p - 1, Br[J0], Ba[J0], Bl[J0]);
+    pass(IC<0>{}, false, 0, (sl + 4) & 7, PT, p - 4, Br[J3], Ba[J3], Bl[J3]);
     TB2_STAMP(5, p);
     store((sl + 4) & 7, PT, p - 4);
     TB2_STAMP(6, p);
@@ -643,6 +671,10 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   const dim3 grid((unsigned)nblocks), block(NT);
   const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0;
   const TB2Ghosts<T> gg = make_ghosts<T>(g);
+  if (zero_in)  // the ZIN passes assume every ghost of a zero input is +-0
+    for (int f = 0; f < 6; ++f)
+      if (g.bcm[f] != kBcMemory && gg.c[f] != (T)0)
+        throw Error(kBadArg, "two-sweep launch: zero input under an inhomogeneous BC");
 #define MGIC_TB2(Z, A, FA)                                                                        \
   k_gsrb_tb2<T, TX, TY, NT, Z, A, FA><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, g, s, gg, \
                                                               kc, ntx, nty, nblocks)
