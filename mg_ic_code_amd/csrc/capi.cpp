@@ -1041,11 +1041,9 @@ MGIC_API int mgic_grid_create_patches(mgic_comm c, const int domain[6], const in
     const Box dom = Box::make(domain);
     std::vector<Box> bx;
     std::vector<int> own;
-    long vol = 0;
     for (int b = 0; b < nbox; ++b) {
       bx.push_back(Box::make(boxes + 6 * b));
       MGIC_CHECK(!bx.back().empty() && dom.contains(bx.back()), "patch boxes must lie in the domain");
-      vol += bx.back().ncells();
       own.push_back(owners ? owners[b] : 0);
     }
     for (int a = 0; a < nbox; ++a)
