@@ -1342,7 +1342,13 @@ void residual_to_f(float *r, const double *u, const double *rhs, const double *a
   const int kc = 16 < g.nz ? 16 : g.nz;
   dim3 grid = grid_cells((g.nx + 1) / 2, g.ny, g.nz);
   grid.z = (unsigned)((g.nz + kc - 1) / kc);
-  if (s.bconst) k_residual_z2<true, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  static const int nt = [] {  // as residual(): MGIC_RESIDUAL_NT, default 3
+    const char *e = getenv("MGIC_RESIDUAL_NT");
+    return e ? atoi(e) : 3;
+  }();
+  if (s.bconst && nt == 3)
+    k_residual_z2<true, float, 3><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  else if (s.bconst) k_residual_z2<true, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
   else k_residual_z2<false, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
   check_launch();
 }
@@ -1351,7 +1357,14 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
                          const float *a, const float *b, const BoxArgs &fg, const StencilCoefs &s,
                          hipStream_t st) {
   if (cg.nx <= 0 || cg.ny <= 0 || cg.nz <= 0) return;
-  if (s.bconst)
+  static const int nt = [] {  // as restrict_residual(): MGIC_RESTRICT_NT, default 1
+    const char *e = getenv("MGIC_RESTRICT_NT");
+    return e ? atoi(e) : 1;
+  }();
+  if (s.bconst && (nt & 1))
+    k_restrict<float, true, 1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(
+        rc, cg, u, rhs, a, b, fg, s, 0);
+  else if (s.bconst)
     k_restrict<float, true><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b,
                                                                                fg, s, 0);
   else
