@@ -50,15 +50,30 @@ def parse():
                     help="4-deep ghost shells, two sweeps per exchange: 0 off, 1 every level, "
                          "2 levels of boxes <= 128^3; default 1 for N > 1 (RCCL exchanges: "
                          "fewer, larger messages), 0 on one GPU (local copies are cheap)")
+    ap.add_argument("--transport", choices=("auto", "ipc", "rccl"), default="auto",
+                    help="N > 1 halo transport: peer-mapped buffers + device flags (ipc), RCCL "
+                         "send/recv (rccl), or ipc with an RCCL fallback (auto, default)")
+    ap.add_argument("--agglomerate-below", type=int, default=0,
+                    help="gather MG depths whose boxes have a side below this to one box on "
+                         "rank 0 (the coarsest levels solved on rank 0); 0 off")
     ap.add_argument("--roofline-events", choices=("relax", "launch"), default="relax",
                     help="HIP events for the smoother roofline: one pair per relax call "
                          "(default; time / launches) or one pair per launch")
     ap.add_argument("--no-roofline-events", action="store_true",
                     help="no events in the timed region (roofline fields null)")
+    ap.add_argument("--norm-type", type=int, default=0,
+                    help="per-iteration residual norm of AMRMultiGrid's stop test (params.txt:37-38, "
+                         "m_normType 0 = max norm; -1 skips it)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=10)
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads for the all-cores CPU baseline (0: the CPUs this process may run "
+                         "on, capped by OMP_NUM_THREADS when that is set)")
+    ap.add_argument("--cpu-1core-iters", type=int, default=1,
+                    help="V-cycle iterations of the 1-thread CPU baseline (0 skips it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_smoother.json"))
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the in-run PMC passes (rocprofv3 FETCH_SIZE / WRITE_SIZE of the "
+                         "smoother launches, two child runs of this script)")
     return ap.parse_args()
 
 
@@ -74,8 +89,6 @@ def main():
     import torch
 
     import mg_ic_code_amd as mg
-    from mg_ic_code_amd.decomposition import decompose
-    from mg_ic_code_amd.params import read_params_file
 
     # MGIC_BENCH_DEVICE pins every rank to one device (rehearsing the
     # multi-rank path on a one-GPU machine); default: one GPU per rank
@@ -84,49 +97,34 @@ def main():
     mg.set_device(dev)
 
     dist = None
+    transport = "none"
     if world > 1:
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        uid = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            uid = torch.tensor(list(mg.Comm.unique_id()), dtype=torch.uint8)
-        dist.broadcast(uid, 0)
-        comm = mg.Comm(rank, world, unique_id=bytes(uid.tolist()))
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=300))
+        comm, transport = make_comm(mg, torch, dist, rank, world, args.transport)
     else:
         comm = mg.Comm()
 
-    prm = read_params_file(os.path.join(ROOT, "tests", "golden", "params.txt"))
-    n = args.size
-    dx = prm.L / n
-    bh = prm.bh()
-    bh["domain_length"] = dx * n
     bpr = tuple(int(v) for v in args.boxes_per_rank.split(","))
-    dom, boxes, owners = decompose((n, n, n), world, boxes_per_rank=bpr)
-    grid = mg.Grid(comm, dom, boxes, dx, owners=owners)
-    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
-    mg.set_binary_bh_coefs(fa, frhs, bh)
-    fb.set_val(1.0)
-    fphi.set_zero()
-    op_params = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
-                                  bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
-                                  coefficient_average_type=1, prolong_type=1, relax_mode=1,
-                                  fused_smoother=0 if args.no_fused else 1,
-                                  overlap_exchange=args.overlap,
-                                  deep_halo=(1 if world > 1 else 0) if args.deep_halo < 0
-                                  else args.deep_halo)
-    fac = mg.defineOperatorFactory(grid, fa, fb, op_params)
-    sp = mg.SolverParams(max_depth=args.levels - 1, n_pre=args.nsmooth, n_post=args.nsmooth,
-                         n_bottom=args.nsmooth, bottom_solver=0)
-    amg = mg.AMRMultiGrid(fac, sp)
-    assert amg.num_depths == args.levels, amg.num_depths
+    case = build_case(mg, comm, world, args.size, args.levels, args.nsmooth, bpr,
+                      fused=0 if args.no_fused else 1, overlap=args.overlap,
+                      deep_halo=(1 if world > 1 else 0) if args.deep_halo < 0 else args.deep_halo,
+                      agglomerate_below=args.agglomerate_below)
+    n = args.size
+    boxes, grid, fa, frhs, fphi, fres = (case[k] for k in ("boxes", "grid", "fa", "frhs", "fphi",
+                                                           "fres"))
+    dom, dx, amg, op_params = case["dom"], case["dx"], case["amg"], case["op_params"]
     r0 = amg.init_residual(fphi, frhs, fres, norm_type=0)
+    nt = args.norm_type
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     for _ in range(args.warmup):
-        amg.iteration(fphi, frhs, fres, norm_type=-1)
+        amg.iteration(fphi, frhs, fres, norm_type=nt)
     comm.synchronize()
 
     fine_cells = max((b[3] - b[0] + 1) * (b[4] - b[1] + 1) * (b[5] - b[2] + 1) for b in boxes)
@@ -135,8 +133,11 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    hist = []
     for _ in range(args.steps):
-        amg.iteration(fphi, frhs, fres, norm_type=-1)
+        # AMRMultiGrid::solve's iteration: the V-cycle, r = rhs - L(phi) and
+        # (norm_type >= 0) its norm for the stop test, on the host
+        hist.append(amg.iteration(fphi, frhs, fres, norm_type=nt))
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -166,20 +167,13 @@ def main():
     achieved = compulsory / (avg_launch_ms * 1e-3) / 1e9 if launches else None
     effective = credit_per_launch / (avg_launch_ms * 1e-3) / 1e9 if launches else None
     traffic = None
-    tj = args.traffic_json
-    if os.path.exists(tj):
-        try:
-            with open(tj) as f:
-                tinfo = json.load(f)
-            key = f"n{n}_w{world}_{ {1: 'pass', 2: 'fused', 4: 'fused2x'}.get(round(passes_per_launch), 'mixed')}"
-            if key in tinfo:
-                traffic = tinfo[key]["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
+    if rank == 0 and world == 1 and not args.no_traffic and launches:
+        traffic = pmc_traffic(args)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_iters > 0:
         cpu = cpu_baseline(args, grid, fa, frhs, dom, dx, np)
+    hb = traffic.get("hbm_bytes_per_launch") if traffic else None
 
     if rank == 0:
         vps = args.steps / elapsed
@@ -205,8 +199,10 @@ def main():
                 "halo": ("none (one box)" if len(boxes) == 1 else
                          "4-deep ghost shell per 2 fused sweeps (deep halo)" if op_params.deep_halo
                          else "2-deep ghost shell per fused sweep"),
-                "parallelism": f"domain-decomposition x{world} (RCCL halo exchange)" if world > 1
-                else "single GPU",
+                "parallelism": f"domain-decomposition x{world} ({transport} halo exchange)"
+                if world > 1 else "single GPU",
+                "transport": transport,
+                "agglomerate_below": args.agglomerate_below,
             },
             "roofline": {
                 "bound": "hbm",
@@ -217,15 +213,17 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": traffic,
-                "traffic_GBps": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic and launches else None,
+                "traffic": hb,
+                "traffic_GBps": round(hb / (avg_launch_ms * 1e-3) / 1e9, 1) if hb and launches else None,
+                "traffic_detail": traffic,
                 "algorithmic_bytes_per_launch": compulsory,
                 "effective_GBps": round(effective, 1) if effective else None,
                 "note": "achieved/frac = algorithmic bytes per launch (32 B/cell: u, rhs, aCoef in, "
                         "u out, once per launch whatever its colour passes) / average launch time; "
                         "effective_GBps = SURVEY 8(d)'s 48 B/cell/colour-pass credit over the same "
-                        "time (exceeds the peak once a launch fuses passes); traffic = PMC HBM "
-                        "bytes per launch (profiles/traffic_smoother.json)",
+                        "time (exceeds the peak once a launch fuses passes); traffic = HBM bytes per "
+                        "fine-level smoother launch from two rocprofv3 --pmc passes (FETCH_SIZE x2 "
+                        "gfx950 correction, WRITE_SIZE) run by this bench on the same workload",
                 "avg_launch_ms": round(avg_launch_ms, 5) if launches else None,
                 "timing": ("off" if args.no_roofline_events else
                            "HIP events on the operator stream, one pair per relax call "
@@ -235,6 +233,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "residual_max_norm": {"initial": r0, "final": r_final},
+            "norm_type_in_step": nt,
+            "residual_norm_history": hist[-3:] if nt >= 0 else None,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
@@ -242,14 +242,86 @@ def main():
         dist.destroy_process_group()
 
 
+def make_comm(mg, torch, dist, rank, world, transport):
+    """The N > 1 communicator: the peer-mapped transport ("ipc": ranks map
+    each other's receive buffers, csrc/transport.hpp; works when ranks share
+    a device) or RCCL.  "auto" tries ipc and falls back to RCCL on every rank
+    when any rank could not set it up (a collective decision)."""
+    if transport in ("ipc", "auto"):
+        comm, ok, err = None, 1, ""
+        try:
+            comm = mg.Comm(rank, world, transport="ipc")
+        except Exception as e:  # noqa: BLE001 -- decided collectively below
+            ok, err = 0, str(e)
+        t = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if int(t.item()) == 1:
+            return comm, "ipc"
+        if transport == "ipc":
+            raise SystemExit(f"rank {rank}: peer-mapped transport unavailable: {err}")
+        del comm
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        uid = torch.tensor(list(mg.Comm.unique_id()), dtype=torch.uint8)
+    dist.broadcast(uid, 0)
+    return mg.Comm(rank, world, unique_id=bytes(uid.tolist())), "rccl"
+
+
+def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fused=1, overlap=0,
+               deep_halo=0, agglomerate_below=0):
+    """The bench workload (BASELINE config C3 / C4): n^3 split over `world`
+    ranks (z first), SetBinaryBH aCoef / rhs of params.txt at psi = 1 on
+    device, bCoef = 1, phi = 0, the reference operator settings, and an
+    AMRMultiGrid of `levels` depths.  tests/mp_worker.py builds the same."""
+    from mg_ic_code_amd.decomposition import decompose
+    from mg_ic_code_amd.params import read_params_file
+    prm = read_params_file(os.path.join(ROOT, "tests", "golden", "params.txt"))
+    dx = prm.L / n
+    bh = prm.bh()
+    bh["domain_length"] = dx * n
+    dom, boxes, owners = decompose((n, n, n), world, boxes_per_rank=tuple(boxes_per_rank))
+    grid = mg.Grid(comm, dom, boxes, dx, owners=owners)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    mg.set_binary_bh_coefs(fa, frhs, bh)
+    fb.set_val(1.0)
+    fphi.set_zero()
+    op_params = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                                  bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
+                                  coefficient_average_type=1, prolong_type=1, relax_mode=1,
+                                  fused_smoother=fused, overlap_exchange=overlap,
+                                  deep_halo=deep_halo)
+    fac = mg.defineOperatorFactory(grid, fa, fb, op_params)
+    sp = mg.SolverParams(max_depth=levels - 1, n_pre=nsmooth, n_post=nsmooth, n_bottom=nsmooth,
+                         bottom_solver=0, agglomerate_below=agglomerate_below)
+    amg = mg.AMRMultiGrid(fac, sp)
+    assert amg.num_depths == levels, amg.num_depths
+    return dict(dom=dom, boxes=boxes, owners=owners, dx=dx, grid=grid, fa=fa, fb=fb, frhs=frhs,
+                fphi=fphi, fres=fres, fac=fac, amg=amg, op_params=op_params)
+
+
+def host_cpus():
+    """(CPUs this process may run on, CPUs of the machine)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return avail, os.cpu_count() or avail
+
+
 def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
-    """The oracle (C restatement, OpenMP) on the same inputs: bounded sample
-    of `cpu_baseline_iters` V-cycle iterations of the same workload."""
+    """The oracle (C restatement, OpenMP) on the same inputs: bounded samples
+    of the same workload on all the host cores this job may use and on one
+    core.  Chombo itself cannot be built here."""
     import oracle
     n = args.size
     a = fa.download(0)
     rhs = frhs.download(0)
-    oracle.set_threads(args.cpu_threads)
+    avail, machine = host_cpus()
+    threads = args.cpu_threads
+    if threads <= 0:
+        threads = avail
+        if os.environ.get("OMP_NUM_THREADS"):
+            threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
     o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, nlevels=args.levels, avg_type=1,
                         prolong_type=1, bottom_solver=0, n_pre=args.nsmooth, n_post=args.nsmooth,
                         n_bottom=args.nsmooth)
@@ -259,18 +331,89 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
     del a, rhs
     o.setup()
     o.init_residual(0)
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_baseline_iters):
-        o.iteration(0)
-    dt = time.perf_counter() - t0
-    return {
+
+    def timed(nthreads, iters):
+        oracle.set_threads(nthreads)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            o.iteration(0)
+        return time.perf_counter() - t0, oracle.get_threads()
+
+    dt, used = timed(threads, args.cpu_baseline_iters)
+    out = {
         "value": round(args.cpu_baseline_iters / dt, 6),
         "unit": "V-cycles/s",
-        "cores": oracle.get_threads(),
+        "cores": used,
         "kind": "port",
         "sample": f"{args.cpu_baseline_iters} V-cycle iteration(s) of the same {n}^3 "
                   f"{args.levels}-level workload (oracle/mgic_oracle.c, OpenMP, -O3), {dt:.1f} s",
+        "host_cpus_available": avail,
+        "host_cpus_machine": machine,
     }
+    if args.cpu_1core_iters > 0:
+        dt1, _ = timed(1, args.cpu_1core_iters)
+        out["one_core"] = {"value": round(args.cpu_1core_iters / dt1, 6), "unit": "V-cycles/s",
+                           "cores": 1,
+                           "sample": f"{args.cpu_1core_iters} V-cycle iteration(s), 1 thread, "
+                                     f"{dt1:.1f} s"}
+    oracle.set_threads(threads)
+    return out
+
+
+def pmc_traffic(args):
+    """HBM bytes per fine-level smoother launch, measured by this bench: two
+    child runs of the same workload under rocprofv3 --pmc (FETCH_SIZE, then
+    WRITE_SIZE: they do not fit one pass), each under its own time limit.
+    MI355X_MICROARCH.md 'HBM': on gfx950 FETCH_SIZE counts half the bytes of
+    a wide coalesced read (x2); WRITE_SIZE is exact for 16-B stores; KiB."""
+    import csv
+    import glob
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    work = tempfile.mkdtemp(prefix="mgic_pmc_")
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    kname = None
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(work, ctr)
+            cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "--kernel-include-regex",
+                   "k_gsrb_tb2", "-d", d, "-o", "p", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
+                   "--size", str(args.size), "--levels", str(args.levels), "--nsmooth",
+                   str(args.nsmooth), "--no-cpu-baseline", "--no-traffic",
+                   "--no-roofline-events", "--norm-type", str(args.norm_type)]
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env,
+                               timeout=200)
+            if r.returncode != 0:
+                return {"error": f"rocprofv3 --pmc {ctr} pass exited {r.returncode}"}
+            rows = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                rows += list(csv.DictReader(open(f)))
+            if not rows:
+                return {"error": f"no counter rows for {ctr}"}
+            top = max(int(x["Grid_Size"]) for x in rows)  # the fine level's launches
+            v = [float(x["Counter_Value"]) for x in rows if int(x["Grid_Size"]) == top]
+            m = re.search(r"(k_gsrb_tb2<[^(]*>)", rows[0]["Kernel_Name"])
+            kname = m.group(1) if m else rows[0]["Kernel_Name"][:80]
+            vals[ctr] = (sum(v) / len(v), len(v))
+    except Exception as e:  # the bench line never fails for want of counters
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    rd = vals["FETCH_SIZE"][0] * 1024.0 * 2.0
+    wr = vals["WRITE_SIZE"][0] * 1024.0
+    return {"hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd,
+            "write_bytes_per_launch": wr, "launches_sampled": vals["FETCH_SIZE"][1],
+            "kernel": kname,
+            "method": "this run: rocprofv3 --pmc FETCH_SIZE (x1024 x2, gfx950 half count) and "
+                      "WRITE_SIZE (x1024) in separate child passes of the same workload, averaged "
+                      "over the fine-level k_gsrb_tb2 launches (plain, ACC and ZIN variants)"}
 
 
 if __name__ == "__main__":

@@ -100,11 +100,26 @@ MGIC_API void mgic_mg_params_default(mgic_mg_params *p);
 MGIC_API int mgic_comm_unique_id(unsigned char id[MGIC_UNIQUE_ID_BYTES]);
 MGIC_API int mgic_comm_create(int rank, int size, const unsigned char *id, int force_rccl,
                               mgic_comm *out);
+/* The peer-mapped transport instead of RCCL (no RCCL communicator): every
+ * rank maps every other rank's signal page and receive arena through
+ * hipIpcOpenMemHandle, and an exchange is two kernels with device-side flags
+ * (ranks may share one device).  `allgather` is the host's own collective
+ * (MPI_Allgather in a Chombo build), called once inside this function:
+ * gather `nbytes` from every rank into out[size * nbytes], rank order, 0 on
+ * success; it may be NULL when size == 1.  arena_bytes: one message buffer
+ * (0: MGIC_IPC_ARENA_MB, default 64 MB); every rank passes the same value.
+ * Replaces the MPI transport of Chombo's Copier (exchange(),
+ * VariableCoeffPoissonOperator.cpp:48,131,301) and of its norms. */
+typedef int (*mgic_allgather_fn)(const void *in, size_t nbytes, void *out, void *user);
+MGIC_API int mgic_comm_create_ipc(int rank, int size, mgic_allgather_fn allgather, void *user,
+                                  size_t arena_bytes, mgic_comm *out);
+/* transport of a communicator: 0 none (one rank), 1 RCCL, 2 peer-mapped */
+MGIC_API int mgic_comm_transport(mgic_comm c, int *transport);
 MGIC_API int mgic_comm_destroy(mgic_comm c);
 MGIC_API int mgic_comm_set_stream(mgic_comm c, void *hip_stream); /* NULL: own stream */
 MGIC_API int mgic_comm_get_stream(mgic_comm c, void **hip_stream);
 MGIC_API int mgic_comm_set_self_messages(mgic_comm c, int on);
-MGIC_API int mgic_comm_synchronize(mgic_comm c);
+MGIC_API int mgic_comm_synchronize(mgic_comm c); /* + raises a transport timeout */
 MGIC_API int mgic_comm_rank(mgic_comm c, int *rank, int *size, int *uses_rccl);
 
 /* ---- grids (DisjointBoxLayout(boxes, procs, domain); set_grids,

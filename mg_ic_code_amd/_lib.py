@@ -90,6 +90,8 @@ SIGNATURES = {
     "mgic_mg_params_default": [POINTER(MGParams)],
     "mgic_comm_unique_id": [ctypes.c_char_p],
     "mgic_comm_create": [c_int, c_int, ctypes.c_char_p, c_int, PH],
+    "mgic_comm_create_ipc": [c_int, c_int, c_void_p, c_void_p, ctypes.c_size_t, PH],
+    "mgic_comm_transport": [H, PI],
     "mgic_comm_destroy": [H],
     "mgic_comm_set_stream": [H, c_void_p],
     "mgic_comm_get_stream": [H, PH],

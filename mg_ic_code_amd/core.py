@@ -67,20 +67,75 @@ def device_synchronize() -> None:
     call("mgic_device_synchronize")
 
 
+# mgic_allgather_fn: int (*)(const void *in, size_t nbytes, void *out, void *user)
+_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                 ctypes.c_void_p)
+
+
+def gloo_allgather(group=None):
+    """A host allgather over an initialised torch.distributed process group
+    (the control plane of the peer-mapped transport's one-time setup)."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(data: bytes) -> List[bytes]:
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(out, t, group=group)
+        return [bytes(o.numpy().tobytes()) for o in out]
+
+    return fn
+
+
 class Comm:
-    """One rank of the job (MPI process in the reference): RCCL communicator
-    (when size > 1 or forced) and the HIP stream all work is queued on."""
+    """One rank of the job (MPI process in the reference) and the HIP stream
+    all work is queued on.  transport:
+      "rccl" -- an RCCL communicator (when size > 1 or forced; needs
+                `unique_id`, one rank per device);
+      "ipc"  -- the peer-mapped transport (csrc/transport.hpp): every rank
+                maps the others' receive buffers and signal pages; ranks may
+                share a device.  `allgather(bytes) -> [bytes per rank]` is
+                the host collective for the one-time setup (default: gloo
+                over torch.distributed)."""
 
     def __init__(self, rank: int = 0, size: int = 1, unique_id: Optional[bytes] = None,
-                 force_rccl: bool = False):
+                 force_rccl: bool = False, transport: str = "rccl",
+                 allgather=None, arena_bytes: int = 0):
         h = ctypes.c_void_p()
+        self.rank, self.size = rank, size
+        if transport == "ipc":
+            if allgather is None and size > 1:
+                allgather = gloo_allgather()
+
+            def _cb(inp, nbytes, out, _user):
+                try:
+                    parts = allgather(ctypes.string_at(inp, nbytes))
+                    if len(parts) != size or any(len(x) != nbytes for x in parts):
+                        return 1
+                    ctypes.memmove(out, b"".join(parts), nbytes * size)
+                    return 0
+                except Exception:  # noqa: BLE001 -- reported as a status code
+                    return 1
+
+            cb = _ALLGATHER_FN(_cb)
+            call("mgic_comm_create_ipc", int(rank), int(size), ctypes.cast(cb, ctypes.c_void_p),
+                 None, int(arena_bytes), ctypes.byref(h))
+            self._h = h
+            return
+        if transport != "rccl":
+            raise ValueError(f"unknown transport {transport!r}")
         uid = None
         if unique_id is not None:
             assert len(unique_id) == 128
             uid = ctypes.c_char_p(bytes(unique_id))
         call("mgic_comm_create", int(rank), int(size), uid, int(bool(force_rccl)), ctypes.byref(h))
         self._h = h
-        self.rank, self.size = rank, size
+
+    @property
+    def transport(self) -> str:
+        t = ctypes.c_int()
+        call("mgic_comm_transport", self._h, ctypes.byref(t))
+        return {0: "none", 1: "rccl", 2: "ipc"}[t.value]
 
     @staticmethod
     def unique_id() -> bytes:

@@ -253,6 +253,27 @@ MGIC_API int mgic_comm_create(int rank, int size, const unsigned char *id, int f
     *out = h;
   });
 }
+MGIC_API int mgic_comm_create_ipc(int rank, int size, mgic_allgather_fn allgather, void *user,
+                                  size_t arena_bytes, mgic_comm *out) {
+  return guard([&] {
+    NEED(out);
+    auto *h = new mgic_comm_s;
+    try {
+      h->c = std::make_shared<Comm>(rank, size, allgather, user, arena_bytes);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+MGIC_API int mgic_comm_transport(mgic_comm c, int *transport) {
+  return guard([&] {
+    NEED(c);
+    NEED(transport);
+    *transport = c->c->uses_ipc() ? 2 : c->c->uses_rccl() ? 1 : 0;
+  });
+}
 MGIC_API int mgic_comm_destroy(mgic_comm c) {
   return guard([&] { delete c; });
 }
@@ -279,6 +300,7 @@ MGIC_API int mgic_comm_synchronize(mgic_comm c) {
   return guard([&] {
     NEED(c);
     MGIC_HIP(hipStreamSynchronize(c->c->stream()));
+    c->c->ipc_check();
   });
 }
 MGIC_API int mgic_comm_rank(mgic_comm c, int *rank, int *size, int *uses_rccl) {

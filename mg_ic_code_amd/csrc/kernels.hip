@@ -26,6 +26,13 @@ __device__ __forceinline__ T ghost_of(int mode, T c, T near) {
   return mode == kBcDirichlet ? (c - near) : (mode == kBcNeumannHom ? near : near + c);
 }
 
+// reduction operator: sums (KIND < 3) and maxima (KIND >= 3, also of |x|)
+template <int KIND>
+__device__ __forceinline__ double red_op(double a, double b) {
+  if constexpr (KIND >= 3) return a > b ? a : b;
+  else return a + b;
+}
+
 // element type traits for the fp32 (mixed-precision) variants: a lane pair
 // is one 16-B (double) / 8-B (float) access; the stencil constants are
 // rounded to T once (identity for double)
@@ -219,59 +226,81 @@ __device__ __forceinline__ void st2n(T *__restrict__ p, const V2<T> &w) {
   }
 }
 
-template <bool BC, class RT, int NT = 0>
+// NRM: also the block's max |r| over the cells it writes into
+// partials[linear block id] (AMRMultiGrid's per-iteration max norm, normType
+// 0, taken while r is in registers instead of a second pass over it; a max
+// is exact, so it equals the separate norm bit for bit)
+template <bool BC, class RT, int NT = 0, bool NRM = false>
 __global__ __launch_bounds__(256) void k_residual_z2(RT *__restrict__ r,
                                                      const double *__restrict__ u,
                                                      const double *__restrict__ rhs,
                                                      const double *__restrict__ a,
                                                      const double *__restrict__ b, const BoxArgs g,
-                                                     const StencilCoefs s, int kc) {
+                                                     const StencilCoefs s, int kc,
+                                                     double *__restrict__ partials = nullptr) {
   const int i = 2 * (blockIdx.x * TX + threadIdx.x);
   const int j = blockIdx.y * TY + threadIdx.y;
   const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, g.nz);
-  if (i >= g.nx || j >= g.ny) return;
-  const long col = (long)i + (long)j * g.sy;
-  const bool two = i + 1 < g.nx;
-  const bool fx0 = i == 0 && g.bcm[0];
-  const bool fx1a = i == g.nx - 1 && g.bcm[1], fx1b = i + 1 == g.nx - 1 && g.bcm[1];
-  const bool fy0 = j == 0 && g.bcm[2], fy1 = j == g.ny - 1 && g.bcm[3];
-  double2 um = ld2(u + col + (long)(k0 - 1) * g.sz);  // ghost plane -1 is allocated
-  double2 uc = ld2(u + col + (long)k0 * g.sz);
-  for (int k = k0; k < k1; ++k) {
-    const long idx = col + (long)k * g.sz;
-    const double2 up = ld2(u + idx + g.sz);  // plane nz (ghost) when k = nz - 1
-    const double xl = u[idx - 1], xr = u[idx + 2];
-    const double2 ym = ld2(u + idx - g.sy), yp = ld2(u + idx + g.sy);
-    const double2 rv = ld2n<NT & 1>(rhs + idx), av = ld2n<NT & 1>(a + idx);
-    const double2 bv = BC ? make_double2(s.bval, s.bval) : ld2n<NT & 1>(b + idx);
-    auto cell = [&](double c, double xm, double xp, double ymv, double ypv, double zm, double zp,
-                    double rr, double aa, double bb, bool bxm, bool bxp) {
-      if (bxm) xm = ghost_of(g.bcm[0], g.bcc[0], c);
-      if (bxp) xp = ghost_of(g.bcm[1], g.bcc[1], c);
-      if (fy0) ymv = ghost_of(g.bcm[2], g.bcc[2], c);
-      if (fy1) ypv = ghost_of(g.bcm[3], g.bcc[3], c);
-      if (k == 0 && g.bcm[4]) zm = ghost_of(g.bcm[4], g.bcc[4], c);
-      if (k == g.nz - 1 && g.bcm[5]) zp = ghost_of(g.bcm[5], g.bcc[5], c);
-      const double res = rr - s.alpha * aa * c;            // .ChF:314-316
-      const double tx = (xp + xm) - 2.0 * c;
-      const double ty = (ypv + ymv) - 2.0 * c;
-      const double tz = (zp + zm) - 2.0 * c;
-      double ldpsi = (tx + ty) + tz;                       // .ChF:320-329
-      ldpsi = ldpsi * s.dxinv * s.beta * bb;               // .ChF:331
-      return (RT)(res + ldpsi);                            // .ChF:333
-    };
-    const RT r0 = cell(uc.x, xl, uc.y, ym.x, yp.x, um.x, up.x, rv.x, av.x, bv.x, fx0, fx1a);
-    const RT r1 = cell(uc.y, uc.x, xr, ym.y, yp.y, um.y, up.y, rv.y, av.y, bv.y, false, fx1b);
-    if (two) {
-      V2<RT> w;
-      w.x = r0;
-      w.y = r1;
-      st2n<(NT & 2) != 0>(r + idx, w);
-    } else {
-      r[idx] = r0;
+  double nmax = 0.0;  // the identity of max |x|
+  if (i < g.nx && j < g.ny) {
+    const long col = (long)i + (long)j * g.sy;
+    const bool two = i + 1 < g.nx;
+    const bool fx0 = i == 0 && g.bcm[0];
+    const bool fx1a = i == g.nx - 1 && g.bcm[1], fx1b = i + 1 == g.nx - 1 && g.bcm[1];
+    const bool fy0 = j == 0 && g.bcm[2], fy1 = j == g.ny - 1 && g.bcm[3];
+    double2 um = ld2(u + col + (long)(k0 - 1) * g.sz);  // ghost plane -1 is allocated
+    double2 uc = ld2(u + col + (long)k0 * g.sz);
+    for (int k = k0; k < k1; ++k) {
+      const long idx = col + (long)k * g.sz;
+      const double2 up = ld2(u + idx + g.sz);  // plane nz (ghost) when k = nz - 1
+      const double xl = u[idx - 1], xr = u[idx + 2];
+      const double2 ym = ld2(u + idx - g.sy), yp = ld2(u + idx + g.sy);
+      const double2 rv = ld2n<NT & 1>(rhs + idx), av = ld2n<NT & 1>(a + idx);
+      const double2 bv = BC ? make_double2(s.bval, s.bval) : ld2n<NT & 1>(b + idx);
+      auto cell = [&](double c, double xm, double xp, double ymv, double ypv, double zm, double zp,
+                      double rr, double aa, double bb, bool bxm, bool bxp) {
+        if (bxm) xm = ghost_of(g.bcm[0], g.bcc[0], c);
+        if (bxp) xp = ghost_of(g.bcm[1], g.bcc[1], c);
+        if (fy0) ymv = ghost_of(g.bcm[2], g.bcc[2], c);
+        if (fy1) ypv = ghost_of(g.bcm[3], g.bcc[3], c);
+        if (k == 0 && g.bcm[4]) zm = ghost_of(g.bcm[4], g.bcc[4], c);
+        if (k == g.nz - 1 && g.bcm[5]) zp = ghost_of(g.bcm[5], g.bcc[5], c);
+        const double res = rr - s.alpha * aa * c;            // .ChF:314-316
+        const double tx = (xp + xm) - 2.0 * c;
+        const double ty = (ypv + ymv) - 2.0 * c;
+        const double tz = (zp + zm) - 2.0 * c;
+        double ldpsi = (tx + ty) + tz;                       // .ChF:320-329
+        ldpsi = ldpsi * s.dxinv * s.beta * bb;               // .ChF:331
+        return (RT)(res + ldpsi);                            // .ChF:333
+      };
+      const RT r0 = cell(uc.x, xl, uc.y, ym.x, yp.x, um.x, up.x, rv.x, av.x, bv.x, fx0, fx1a);
+      const RT r1 = cell(uc.y, uc.x, xr, ym.y, yp.y, um.y, up.y, rv.y, av.y, bv.y, false, fx1b);
+      if (two) {
+        V2<RT> w;
+        w.x = r0;
+        w.y = r1;
+        st2n<(NT & 2) != 0>(r + idx, w);
+      } else {
+        r[idx] = r0;
+      }
+      if constexpr (NRM) {
+        nmax = red_op<3>(nmax, fabs((double)r0));
+        if (two) nmax = red_op<3>(nmax, fabs((double)r1));
+      }
+      um = uc;
+      uc = up;
     }
-    um = uc;
-    uc = up;
+  }
+  if constexpr (NRM) {
+    __shared__ double sm[TY];
+    for (int o = 32; o > 0; o >>= 1) nmax = red_op<3>(nmax, __shfl_xor(nmax, o, 64));
+    if (threadIdx.x == 0) sm[threadIdx.y] = nmax;
+    __syncthreads();
+    if (threadIdx.x == 0 && threadIdx.y == 0) {
+      double m = sm[0];
+      for (int w = 1; w < TY; ++w) m = red_op<3>(m, sm[w]);
+      partials[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] = m;
+    }
   }
 }
 
@@ -472,11 +501,6 @@ __global__ __launch_bounds__(256) void k_blas(double *__restrict__ x, const doub
 
 constexpr int RB = 256;
 
-template <int KIND>
-__device__ __forceinline__ double red_op(double a, double b) {
-  if constexpr (KIND >= 3) return a > b ? a : b;
-  else return a + b;
-}
 // identity of the reduction: 0 for sums and max|x|, -inf for max x / max -x
 template <int KIND>
 __device__ __forceinline__ double red_init() {
@@ -1102,6 +1126,39 @@ void residual(double *r, const double *u, const double *rhs, const double *a, co
   } else {
     k_residual<false><<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(r, u, rhs, a, b, g, s);
   }
+  check_launch();
+}
+
+static int residual_kc_env() {
+  static const int mode = [] {
+    const char *e = getenv("MGIC_RESIDUAL_KC");
+    return e ? atoi(e) : 16;
+  }();
+  return mode;
+}
+
+long residual_norm_blocks(const BoxArgs &g) {
+  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return 0;
+  const int mode = residual_kc_env();
+  if (mode <= 0) return 0;
+  const int kc = mode < g.nz ? mode : g.nz;
+  const dim3 grid = grid_cells((g.nx + 1) / 2, g.ny, g.nz);
+  return (long)grid.x * grid.y * ((g.nz + kc - 1) / kc);
+}
+
+void residual_norm(double *r, const double *u, const double *rhs, const double *a, const double *b,
+                   const BoxArgs &g, const StencilCoefs &s, double *partials, hipStream_t st) {
+  if (residual_norm_blocks(g) <= 0) throw Error(kBadArg, "residual_norm: streaming residual off");
+  const int mode = residual_kc_env();
+  const int kc = mode < g.nz ? mode : g.nz;
+  dim3 grid = grid_cells((g.nx + 1) / 2, g.ny, g.nz);
+  grid.z = (unsigned)((g.nz + kc - 1) / kc);
+  // the default streams of residual() (MGIC_RESIDUAL_NT = 3: rhs / aCoef
+  // loads and r stores non-temporal)
+  if (s.bconst)
+    k_residual_z2<true, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
+  else
+    k_residual_z2<false, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
   check_launch();
 }
 

@@ -82,6 +82,12 @@ void apply_op(double *lu, const double *u, const double *a, const double *b,
 // VCCOMPUTERES3D (.ChF:283-339)
 void residual(double *r, const double *u, const double *rhs, const double *a,
               const double *b, const BoxArgs &g, const StencilCoefs &s, hipStream_t st);
+// the same residual plus one max |r| partial per block into partials[0, n)
+// (n = residual_norm_blocks(g); 0 when the streaming residual does not apply:
+// then call residual + reduce_partial instead)
+long residual_norm_blocks(const BoxArgs &g);
+void residual_norm(double *r, const double *u, const double *rhs, const double *a, const double *b,
+                   const BoxArgs &g, const StencilCoefs &s, double *partials, hipStream_t st);
 // RESTRICTRESVC3D (.ChF:379-437) incl. setVal(0) on the coarse valid box
 // accumulate=true adds into rc like the bare Fortran kernel (whose caller
 // zeroes rc first); false writes 0 + sum, i.e. setVal(0) + kernel.

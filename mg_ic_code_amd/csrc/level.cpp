@@ -2,7 +2,9 @@
 #include "level.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace mgic {
 
@@ -18,6 +20,111 @@ Comm::Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl)
   }
   MGIC_HIP(hipMalloc(&d_result_, 2 * sizeof(double)));
   MGIC_HIP(hipHostMalloc(&h_result_, 2 * sizeof(double), hipHostMallocDefault));
+}
+
+// the peer-mapped transport: signal page + receive arena per rank, mapped by
+// every other rank (transport.hpp)
+Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena_bytes)
+    : rank_(rank), size_(size) {
+  MGIC_CHECK(size >= 1 && rank >= 0 && rank < size, "bad rank/size");
+  MGIC_CHECK(size <= kern::kMaxIpcRanks, "peer-mapped transport: too many ranks");
+  MGIC_CHECK(size == 1 || allgather != nullptr, "peer-mapped transport needs a host allgather");
+  if (arena_bytes == 0) {
+    const char *e = getenv("MGIC_IPC_ARENA_MB");
+    arena_bytes = (size_t)(e ? atol(e) : 64) << 20;
+  }
+  arena_bytes_ = (arena_bytes + 255) & ~(size_t)255;
+  MGIC_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  own_stream_ = true;
+  MGIC_HIP(hipMalloc(&d_result_, 2 * sizeof(double)));
+  MGIC_HIP(hipHostMalloc(&h_result_, 2 * sizeof(double), hipHostMallocDefault));
+  MGIC_HIP(hipHostMalloc(&h_err_, sizeof(unsigned long long), hipHostMallocDefault));
+  *h_err_ = 0;
+  // counters are polled across processes / devices: uncached memory
+  MGIC_HIP(hipExtMallocWithFlags((void **)&sig_, sizeof(unsigned long long) * kern::kSigWords,
+                                 hipDeviceMallocUncached));
+  MGIC_HIP(hipMemset(sig_, 0, sizeof(unsigned long long) * kern::kSigWords));
+  MGIC_HIP(hipMalloc(&arena_, (size_t)size * 2 * arena_bytes_));
+  MGIC_HIP(hipDeviceSynchronize());
+  ipc_ = true;
+  peer_sig_.assign(size, nullptr);
+  peer_arena_.assign(size, nullptr);
+  sent_.assign(size, 0);
+  recvd_.assign(size, 0);
+  peer_sig_[rank] = sig_;
+  peer_arena_[rank] = arena_;
+  if (size > 1) {
+    struct Rec {
+      hipIpcMemHandle_t sig, arena;
+      unsigned long long arena_bytes;
+      int rank;
+    } mine{}, *all = nullptr;
+    MGIC_HIP(hipIpcGetMemHandle(&mine.sig, sig_));
+    MGIC_HIP(hipIpcGetMemHandle(&mine.arena, arena_));
+    mine.arena_bytes = arena_bytes_;
+    mine.rank = rank;
+    std::vector<Rec> recs(size);
+    all = recs.data();
+    if (allgather(&mine, sizeof(Rec), all, user) != 0)
+      throw Error(kState, "peer-mapped transport: host allgather failed");
+    for (int r = 0; r < size; ++r) {
+      MGIC_CHECK(recs[r].rank == r && recs[r].arena_bytes == arena_bytes_,
+                 "peer-mapped transport: ranks disagree on the setup");
+      if (r == rank) continue;
+      void *ps = nullptr, *pa = nullptr;
+      MGIC_HIP(hipIpcOpenMemHandle(&ps, recs[r].sig, hipIpcMemLazyEnablePeerAccess));
+      MGIC_HIP(hipIpcOpenMemHandle(&pa, recs[r].arena, hipIpcMemLazyEnablePeerAccess));
+      peer_sig_[r] = static_cast<unsigned long long *>(ps);
+      peer_arena_[r] = static_cast<char *>(pa);
+    }
+  }
+}
+
+void Comm::ipc_send(int peer, void **slot, const unsigned long long **wait,
+                    unsigned long long *wait_val, unsigned long long **flag,
+                    unsigned long long *flag_val) {
+  const unsigned long long m = sent_[peer]++;  // my message number m to peer (0-based)
+  *slot = peer_arena_[peer] + ((size_t)rank_ * 2 + (m & 1)) * arena_bytes_;
+  *wait = sig_ + kern::kSigAck + peer * kern::kSigStride;  // message m - 2 consumed
+  *wait_val = m >= 1 ? m - 1 : 0;
+  *flag = peer_sig_[peer] + kern::kSigArr + rank_ * kern::kSigStride;
+  *flag_val = m + 1;
+}
+
+void Comm::ipc_recv(int src, void **slot, const unsigned long long **wait,
+                    unsigned long long *wait_val, unsigned long long **flag,
+                    unsigned long long *flag_val) {
+  const unsigned long long m = recvd_[src]++;
+  *slot = arena_ + ((size_t)src * 2 + (m & 1)) * arena_bytes_;
+  *wait = sig_ + kern::kSigArr + src * kern::kSigStride;  // message m delivered
+  *wait_val = m + 1;
+  *flag = peer_sig_[src] + kern::kSigAck + rank_ * kern::kSigStride;
+  *flag_val = m + 1;
+}
+
+void Comm::ipc_ticket(long blocks, unsigned long long **ticket, unsigned long long *end) {
+  ticket_ += (unsigned long long)blocks;
+  *ticket = sig_ + kern::kSigTicket;
+  *end = ticket_;
+}
+
+void Comm::ipc_err_async(hipStream_t st) {
+  if (!ipc_) return;
+  MGIC_HIP(hipMemcpyAsync(h_err_, sig_ + kern::kSigErr, sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, st));
+}
+
+void Comm::ipc_err_raise() const {
+  if (ipc_ && *h_err_ != 0)
+    throw Error(kState, "peer-mapped transport: a wait for a peer timed out (peer gone or the "
+                        "ranks' exchange sequences differ)");
+}
+
+void Comm::ipc_check() {
+  if (!ipc_) return;
+  ipc_err_async(stream_);
+  MGIC_HIP(hipStreamSynchronize(stream_));
+  ipc_err_raise();
 }
 
 std::shared_ptr<Comm> Comm::host_only(int rank, int size) {
@@ -40,6 +147,17 @@ hipEvent_t Comm::event(int i) {
 
 Comm::~Comm() {
   if (nccl_) ncclCommDestroy(nccl_);
+  if (ipc_) {
+    (void)hipDeviceSynchronize();
+    for (int r = 0; r < size_; ++r) {
+      if (r == rank_) continue;
+      if (peer_sig_[r]) (void)hipIpcCloseMemHandle(peer_sig_[r]);
+      if (peer_arena_[r]) (void)hipIpcCloseMemHandle(peer_arena_[r]);
+    }
+    if (sig_) (void)hipFree(sig_);
+    if (arena_) (void)hipFree(arena_);
+    if (h_err_) (void)hipHostFree(h_err_);
+  }
   if (side_) (void)hipStreamDestroy(side_);
   for (hipEvent_t e : events_)
     if (e) (void)hipEventDestroy(e);
@@ -59,7 +177,18 @@ double *Comm::d_partials(int n) {
 }
 
 void Comm::allreduce(double *d_val, int op) {
-  if (!nccl_ || size_ == 1) return;
+  if (size_ == 1) return;
+  if (ipc_) {
+    kern::IpcReduce r{};
+    r.size = size_;
+    r.rank = rank_;
+    r.count = ++red_count_;
+    r.parity = (int)(r.count & 1);
+    for (int q = 0; q < size_; ++q) r.sig[q] = peer_sig_[q];
+    kern::ipc_allreduce(d_val, op, r, ipc_err(), stream_);
+    return;
+  }
+  if (!nccl_) return;
   MGIC_NCCL(ncclAllReduce(d_val, d_val, 1, ncclDouble, op == 1 ? ncclMax : ncclSum, nccl_, stream_));
 }
 
@@ -188,7 +317,7 @@ std::unique_ptr<CopyPlan> build_copy_plan(const Grid &src, const Grid &dst, bool
   for (int n = 0; n < dst.nlocal(); ++n) dloc[dst.local[n]] = n;
   int len[3];
   for (int d = 0; d < 3; ++d) len[d] = dst.domain.size(d);
-  const bool self_msg = dst.comm->self_messages() && dst.comm->uses_rccl();
+  const bool self_msg = dst.comm->self_messages() && dst.comm->remote_ok();
   for (size_t db = 0; db < dst.boxes.size(); ++db) {
     const Box &dv = dst.boxes[db];
     std::vector<Box> regions;
@@ -288,6 +417,8 @@ CopyPlan::~CopyPlan() {
   if (d_local_) (void)hipFree(d_local_);
   if (d_pack_) (void)hipFree(d_pack_);
   if (d_unpack_) (void)hipFree(d_unpack_);
+  if (d_ipc_pack_) (void)hipFree(d_ipc_pack_);
+  if (d_ipc_unpack_) (void)hipFree(d_ipc_unpack_);
   if (sendbuf_) (void)hipFree(sendbuf_);
   if (recvbuf_) (void)hipFree(recvbuf_);
 }
@@ -327,54 +458,122 @@ void CopyPlan::finalize() {
   d_local_ = upload_items(local_, max_local_);
   d_pack_ = upload_items(pack_, max_pack_);
   d_unpack_ = upload_items(unpack_, max_unpack_);
-  if (send_total_) MGIC_HIP(hipMalloc(&sendbuf_, sizeof(double) * (size_t)send_total_));
-  if (recv_total_) MGIC_HIP(hipMalloc(&recvbuf_, sizeof(double) * (size_t)recv_total_));
+  // the peer-mapped transport's tables: offsets within each peer's message,
+  // pad = the peer's index in send_peers_ / recv_peers_
+  if (!pack_.empty() || !unpack_.empty()) {
+    std::vector<CopyItem> ip = pack_, iu = unpack_;
+    for (auto &kv : send_cnt_) send_peers_.push_back(kv.first);
+    for (auto &kv : recv_cnt_) recv_peers_.push_back(kv.first);
+    MGIC_CHECK((int)send_peers_.size() <= kern::kMaxIpcPeers &&
+                   (int)recv_peers_.size() <= kern::kMaxIpcPeers,
+               "exchange plan: too many peers for the peer-mapped transport");
+    for (auto &it : ip) {
+      it.doff -= send_off_[it.pad];
+      it.pad = (int)(std::find(send_peers_.begin(), send_peers_.end(), it.pad) - send_peers_.begin());
+    }
+    for (auto &it : iu) {
+      it.soff -= recv_off_[it.pad];
+      it.pad = (int)(std::find(recv_peers_.begin(), recv_peers_.end(), it.pad) - recv_peers_.begin());
+    }
+    long dummy = 0;
+    d_ipc_pack_ = upload_items(ip, dummy);
+    d_ipc_unpack_ = upload_items(iu, dummy);
+  }
   final_ = true;
+}
+
+template <class T>
+void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hipStream_t st) {
+  const size_t cap = comm.ipc_arena_bytes() / sizeof(T);
+  for (auto &kv : send_cnt_)
+    MGIC_CHECK((size_t)kv.second <= cap, "exchange message exceeds the transport arena "
+                                         "(raise MGIC_IPC_ARENA_MB)");
+  if (!pack_.empty()) {
+    kern::IpcPeers pp{};
+    pp.n = (int)send_peers_.size();
+    pp.err = comm.ipc_err();
+    for (int q = 0; q < pp.n; ++q)
+      comm.ipc_send(send_peers_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q], &pp.flag[q],
+                    &pp.flag_val[q]);
+    comm.ipc_ticket((long)kern::ipc_grid_x(max_pack_) * (long)pack_.size(), &pp.ticket,
+                    &pp.ticket_end);
+    if constexpr (std::is_same<T, double>::value)
+      kern::ipc_put(d_ipc_pack_, (int)pack_.size(), max_pack_, src_tab, pp, st);
+    else
+      kern::ipc_put_f(d_ipc_pack_, (int)pack_.size(), max_pack_, src_tab, pp, st);
+  }
+  if (!unpack_.empty()) {
+    kern::IpcPeers pp{};
+    pp.n = (int)recv_peers_.size();
+    pp.err = comm.ipc_err();
+    for (int q = 0; q < pp.n; ++q)
+      comm.ipc_recv(recv_peers_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q], &pp.flag[q],
+                    &pp.flag_val[q]);
+    comm.ipc_ticket((long)kern::ipc_grid_x(max_unpack_) * (long)unpack_.size(), &pp.ticket,
+                    &pp.ticket_end);
+    if constexpr (std::is_same<T, double>::value)
+      kern::ipc_get(d_ipc_unpack_, (int)unpack_.size(), max_unpack_, dst_tab, pp, st);
+    else
+      kern::ipc_get_f(d_ipc_unpack_, (int)unpack_.size(), max_unpack_, dst_tab, pp, st);
+  }
 }
 
 void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_tab,
                        hipStream_t st) {
   if (!local_.empty())
     kern::copy_items(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
-  if (send_total_ || recv_total_) {
-    MGIC_CHECK(comm.uses_rccl(), "remote copies need an RCCL communicator");
-    if (!pack_.empty())
-      kern::copy_items(d_pack_, (int)pack_.size(), max_pack_, src_tab, nullptr, nullptr, sendbuf_, st);
-    MGIC_NCCL(ncclGroupStart());
-    for (auto &kv : send_cnt_)
-      MGIC_NCCL(ncclSend(sendbuf_ + send_off_[kv.first], (size_t)kv.second, ncclDouble, kv.first,
-                         comm.nccl(), st));
-    for (auto &kv : recv_cnt_)
-      MGIC_NCCL(ncclRecv(recvbuf_ + recv_off_[kv.first], (size_t)kv.second, ncclDouble, kv.first,
-                         comm.nccl(), st));
-    MGIC_NCCL(ncclGroupEnd());
-    if (!unpack_.empty())
-      kern::copy_items(d_unpack_, (int)unpack_.size(), max_unpack_, nullptr, recvbuf_, dst_tab,
-                       nullptr, st);
+  if (!send_total_ && !recv_total_) return;
+  MGIC_CHECK(comm.remote_ok(), "remote copies need an RCCL communicator or the peer-mapped transport");
+  if (comm.uses_ipc()) {
+    execute_ipc<double>(comm, src_tab, dst_tab, st);
+    return;
   }
+  alloc_buffers();
+  if (!pack_.empty())
+    kern::copy_items(d_pack_, (int)pack_.size(), max_pack_, src_tab, nullptr, nullptr, sendbuf_, st);
+  MGIC_NCCL(ncclGroupStart());
+  for (auto &kv : send_cnt_)
+    MGIC_NCCL(ncclSend(sendbuf_ + send_off_[kv.first], (size_t)kv.second, ncclDouble, kv.first,
+                       comm.nccl(), st));
+  for (auto &kv : recv_cnt_)
+    MGIC_NCCL(ncclRecv(recvbuf_ + recv_off_[kv.first], (size_t)kv.second, ncclDouble, kv.first,
+                       comm.nccl(), st));
+  MGIC_NCCL(ncclGroupEnd());
+  if (!unpack_.empty())
+    kern::copy_items(d_unpack_, (int)unpack_.size(), max_unpack_, nullptr, recvbuf_, dst_tab,
+                     nullptr, st);
 }
 
 void CopyPlan::execute_f(Comm &comm, float *const *src_tab, float *const *dst_tab,
                          hipStream_t st) {
-  float *sb = reinterpret_cast<float *>(sendbuf_), *rb = reinterpret_cast<float *>(recvbuf_);
   if (!local_.empty())
     kern::copy_items_f(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
-  if (send_total_ || recv_total_) {
-    MGIC_CHECK(comm.uses_rccl(), "remote copies need an RCCL communicator");
-    if (!pack_.empty())
-      kern::copy_items_f(d_pack_, (int)pack_.size(), max_pack_, src_tab, nullptr, nullptr, sb, st);
-    MGIC_NCCL(ncclGroupStart());
-    for (auto &kv : send_cnt_)
-      MGIC_NCCL(ncclSend(sb + send_off_[kv.first], (size_t)kv.second, ncclFloat, kv.first,
-                         comm.nccl(), st));
-    for (auto &kv : recv_cnt_)
-      MGIC_NCCL(ncclRecv(rb + recv_off_[kv.first], (size_t)kv.second, ncclFloat, kv.first,
-                         comm.nccl(), st));
-    MGIC_NCCL(ncclGroupEnd());
-    if (!unpack_.empty())
-      kern::copy_items_f(d_unpack_, (int)unpack_.size(), max_unpack_, nullptr, rb, dst_tab,
-                         nullptr, st);
+  if (!send_total_ && !recv_total_) return;
+  MGIC_CHECK(comm.remote_ok(), "remote copies need an RCCL communicator or the peer-mapped transport");
+  if (comm.uses_ipc()) {
+    execute_ipc<float>(comm, src_tab, dst_tab, st);
+    return;
   }
+  alloc_buffers();
+  float *sb = reinterpret_cast<float *>(sendbuf_), *rb = reinterpret_cast<float *>(recvbuf_);
+  if (!pack_.empty())
+    kern::copy_items_f(d_pack_, (int)pack_.size(), max_pack_, src_tab, nullptr, nullptr, sb, st);
+  MGIC_NCCL(ncclGroupStart());
+  for (auto &kv : send_cnt_)
+    MGIC_NCCL(ncclSend(sb + send_off_[kv.first], (size_t)kv.second, ncclFloat, kv.first,
+                       comm.nccl(), st));
+  for (auto &kv : recv_cnt_)
+    MGIC_NCCL(ncclRecv(rb + recv_off_[kv.first], (size_t)kv.second, ncclFloat, kv.first,
+                       comm.nccl(), st));
+  MGIC_NCCL(ncclGroupEnd());
+  if (!unpack_.empty())
+    kern::copy_items_f(d_unpack_, (int)unpack_.size(), max_unpack_, nullptr, rb, dst_tab,
+                       nullptr, st);
+}
+
+void CopyPlan::alloc_buffers() {  // RCCL staging buffers, on first use
+  if (send_total_ && !sendbuf_) MGIC_HIP(hipMalloc(&sendbuf_, sizeof(double) * (size_t)send_total_));
+  if (recv_total_ && !recvbuf_) MGIC_HIP(hipMalloc(&recvbuf_, sizeof(double) * (size_t)recv_total_));
 }
 
 // ------------------------------------------------------------------ LevelData

@@ -15,6 +15,7 @@
 
 #include "kernels.hpp"
 #include "mgic_core.hpp"
+#include "transport.hpp"
 
 namespace mgic {
 
@@ -26,10 +27,20 @@ namespace mgic {
                           std::string("RCCL error ") + ncclGetErrorString(r_) + " in " #x); \
   } while (0)
 
-// One process's view of the job: rank, size, RCCL communicator, stream.
+// host control plane for the peer-mapped transport's setup: gather `nbytes`
+// from every rank into out[size * nbytes] (rank order); 0 on success.  The
+// host passes its own collective (MPI_Allgather for Chombo, gloo for Python).
+typedef int (*HostAllgather)(const void *in, size_t nbytes, void *out, void *user);
+
+// One process's view of the job: rank, size, transport (RCCL communicator or
+// peer-mapped buffers, transport.hpp), stream.
 class Comm {
  public:
   Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl);
+  // peer-mapped transport: no RCCL communicator; `allgather` is called once,
+  // here (may be null when size == 1); arena_bytes: one message buffer per
+  // (sender, parity), 0 = MGIC_IPC_ARENA_MB (default 64 MB)
+  Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena_bytes);
   // rank/size only, no device resources: host-side planning (the exchange
   // plans a rank would execute) on machines without a GPU
   static std::shared_ptr<Comm> host_only(int rank, int size);
@@ -37,6 +48,8 @@ class Comm {
   int rank() const { return rank_; }
   int size() const { return size_; }
   bool uses_rccl() const { return nccl_ != nullptr; }
+  bool uses_ipc() const { return ipc_; }
+  bool remote_ok() const { return nccl_ != nullptr || ipc_; }
   // route same-rank copies through RCCL self send/recv (tests the remote
   // path on one GPU)
   bool self_messages() const { return self_messages_; }
@@ -55,6 +68,24 @@ class Comm {
   double *d_result() const { return d_result_; }
   double *h_result() const { return h_result_; }
 
+  // ---- peer-mapped transport (transport.hpp)
+  size_t ipc_arena_bytes() const { return arena_bytes_; }
+  // message slot of my next message to `peer` in its arena, the ack word to
+  // wait on and the counter to raise; then count it as sent
+  void ipc_send(int peer, void **slot, const unsigned long long **wait, unsigned long long *wait_val,
+                unsigned long long **flag, unsigned long long *flag_val);
+  void ipc_recv(int src, void **slot, const unsigned long long **wait, unsigned long long *wait_val,
+                unsigned long long **flag, unsigned long long *flag_val);
+  // the ticket words of a launch of `blocks` blocks
+  void ipc_ticket(long blocks, unsigned long long **ticket, unsigned long long *end);
+  unsigned long long *ipc_err() const { return sig_ + kern::kSigErr; }
+  // raise if a transport wait of this rank timed out (synchronizes the stream)
+  void ipc_check();
+  // the same split around a caller's own synchronize: queue the read of the
+  // error word, then (after the stream sync) raise
+  void ipc_err_async(hipStream_t st);
+  void ipc_err_raise() const;
+
  private:
   Comm() = default;
   int rank_ = 0, size_ = 1;
@@ -68,6 +99,15 @@ class Comm {
   int n_partials_ = 0;
   double *d_result_ = nullptr;
   double *h_result_ = nullptr;
+  bool ipc_ = false;
+  unsigned long long *sig_ = nullptr;            // my signal page (uncached)
+  char *arena_ = nullptr;                        // my receive arena: size x 2 x arena_bytes_
+  size_t arena_bytes_ = 0;
+  std::vector<unsigned long long *> peer_sig_;   // per rank (mine at [rank_])
+  std::vector<char *> peer_arena_;
+  std::vector<unsigned long long> sent_, recvd_; // messages per peer so far
+  unsigned long long ticket_ = 0, red_count_ = 0;
+  unsigned long long *h_err_ = nullptr;          // pinned
 };
 
 // A precomputed set of rectangular copies between two LevelData layouts
@@ -89,7 +129,14 @@ class CopyPlan {
   long send_total_ = 0, recv_total_ = 0;
 
  private:
+  template <class T>
+  void execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hipStream_t st);
+  void alloc_buffers();
   CopyItem *d_local_ = nullptr, *d_pack_ = nullptr, *d_unpack_ = nullptr;
+  // the peer-mapped transport's item tables: offsets within one peer's
+  // message, pad = index into the plan's peer list
+  CopyItem *d_ipc_pack_ = nullptr, *d_ipc_unpack_ = nullptr;
+  std::vector<int> send_peers_, recv_peers_;
   long max_local_ = 0, max_pack_ = 0, max_unpack_ = 0;
   double *sendbuf_ = nullptr, *recvbuf_ = nullptr;
   bool final_ = false, host_final_ = false;

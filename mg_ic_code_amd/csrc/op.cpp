@@ -154,6 +154,43 @@ void VariableCoeffPoissonOperator::residualI(LevelData &lhs, LevelData &dpsi,
                    s, st);
 }
 
+double VariableCoeffPoissonOperator::residualNorm(LevelData &lhs, LevelData &dpsi,
+                                                  const LevelData &rhs, bool homogeneous,
+                                                  int normType) {
+  long total = 0;
+  bool fused = normType == 0;
+  for (int n = 0; fused && n < grid->nlocal(); ++n) {
+    const long nb = kern::residual_norm_blocks(args(n, homogeneous));
+    fused = nb > 0;
+    total += nb;
+  }
+  if (!fused) {
+    residualI(lhs, dpsi, rhs, homogeneous);
+    return normType >= 0 ? norm(lhs, normType) : -1.0;
+  }
+  check_same_layout(*grid, lhs, "residual lhs");
+  check_same_layout(*grid, dpsi, "residual dpsi");
+  check_same_layout(*grid, rhs, "residual rhs");
+  Comm &c = *grid->comm;
+  const hipStream_t st = stream();
+  dpsi.exchange(st);  // .cpp:48
+  const StencilCoefs s = coefs();
+  double *parts = c.d_partials((int)std::max(1L, total));
+  long off = 0;
+  for (int n = 0; n < grid->nlocal(); ++n) {
+    const BoxArgs &a = args(n, homogeneous);
+    kern::residual_norm(lhs.p[n], dpsi.p[n], rhs.p[n], m_aCoef->p[n], m_bCoef->p[n], a, s,
+                        parts + off, st);
+    off += kern::residual_norm_blocks(a);
+  }
+  finish_reduce(3, parts, (int)total, 0);
+  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
+  c.ipc_err_async(st);
+  MGIC_HIP(hipStreamSynchronize(st));
+  c.ipc_err_raise();
+  return c.h_result()[0];
+}
+
 void VariableCoeffPoissonOperator::preCond(LevelData &cor, const LevelData &res) {
   resetLambda();  // .cpp:90
   const hipStream_t st = stream();
@@ -788,7 +825,9 @@ double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const 
     total += kern::reduce_partial(kind, x.p[n], y ? y->p[n] : nullptr, args_plain_[n], parts + total, st);
   finish_reduce(kind, parts, total, 0);
   MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
+  c.ipc_err_async(st);
   MGIC_HIP(hipStreamSynchronize(st));
+  c.ipc_err_raise();
   return c.h_result()[0];
 }
 
@@ -807,7 +846,9 @@ double VariableCoeffPoissonOperator::axpy2Norm(LevelData &s, const LevelData &r,
                                 args_plain_[n], parts + total, st);
   finish_reduce(kind, parts, total, 0);
   MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
+  c.ipc_err_async(st);
   MGIC_HIP(hipStreamSynchronize(st));
+  c.ipc_err_raise();
   const double x = c.h_result()[0];
   return kind == 2 ? std::sqrt(x) : x;
 }
@@ -833,7 +874,9 @@ void VariableCoeffPoissonOperator::dot2(const LevelData &t, const LevelData &s, 
   finish_reduce(0, parts, total, 0);
   finish_reduce(0, parts + cap, total, 1);
   MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+  c.ipc_err_async(st);
   MGIC_HIP(hipStreamSynchronize(st));
+  c.ipc_err_raise();
   ts = c.h_result()[0];
   tt = c.h_result()[1];
 }
@@ -1154,16 +1197,14 @@ double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &
                                int normType, bool homogeneous) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
   mg.oneCycleFromZeroInto(*corr_, resid, phi);  // e = 0; oneCycle(e, r); phi += e
-  op0.residual(resid, phi, rhs, homogeneous);
-  return normType >= 0 ? op0.norm(resid, normType) : -1.0;
+  return op0.residualNorm(resid, phi, rhs, homogeneous, normType);
 }
 
 double AMRMultiGrid::fmg(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
                          bool homogeneous, int ncycles) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
   mg.fmg(*corr_, resid, phi, ncycles);
-  op0.residual(resid, phi, rhs, homogeneous);
-  return normType >= 0 ? op0.norm(resid, normType) : -1.0;
+  return op0.residualNorm(resid, phi, rhs, homogeneous, normType);
 }
 
 void AMRMultiGrid::precondition(LevelData &e, const LevelData &r, int iters) {
@@ -1200,8 +1241,7 @@ int AMRMultiGrid::solve(LevelData &phi, const LevelData &rhs, const SolveParams 
 double AMRMultiGrid::initResidual(LevelData &phi, const LevelData &rhs, LevelData &resid,
                                   int normType, bool homogeneous) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
-  op0.residual(resid, phi, rhs, homogeneous);
-  return normType >= 0 ? op0.norm(resid, normType) : -1.0;
+  return op0.residualNorm(resid, phi, rhs, homogeneous, normType);
 }
 
 }  // namespace mgic

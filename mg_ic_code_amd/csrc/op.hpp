@@ -62,6 +62,10 @@ class VariableCoeffPoissonOperator {
 
   // --- AMRLevelOp / MGLevelOp overrides (VariableCoeffPoissonOperator.H:39-90)
   void residualI(LevelData &lhs, LevelData &dpsi, const LevelData &rhs, bool homogeneous);
+  // residual + norm(lhs, normType) (normType < 0: no norm, returns -1); the
+  // max norm (0) is taken inside the residual launch
+  double residualNorm(LevelData &lhs, LevelData &dpsi, const LevelData &rhs, bool homogeneous,
+                      int normType);
   void residual(LevelData &lhs, LevelData &dpsi, const LevelData &rhs, bool homogeneous) {
     residualI(lhs, dpsi, rhs, homogeneous);
   }

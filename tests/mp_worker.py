@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""One rank of a multi-process run of the bench workload (bench.build_case)
+on a GPU, for tests/test_multiprocess.py: BASELINE config C4's real form --
+separate processes, one box per rank, halo exchange through the
+peer-mapped transport (csrc/transport.hpp) -- on however many devices the
+box has (all ranks may share device 0).
+
+    mp_worker.py --rank R --world W --port P --n N --out DIR [--device D]
+Writes DIR/rank<R>.npz: this rank's phi boxes, the init + iteration
+residual max norms, the transport used.  gloo (127.0.0.1) is the control
+plane; nothing touches the GPU before the process group exists.
+"""
+import argparse
+import datetime
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--levels", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--agglomerate-below", type=int, default=0)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import mg_ic_code_amd as mg
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank,
+                            world_size=a.world, timeout=datetime.timedelta(seconds=120))
+    mg.set_device(a.device)
+    comm = mg.Comm(a.rank, a.world, transport="ipc")
+    case = bench.build_case(mg, comm, a.world, a.n, a.levels, 4, deep_halo=1,
+                            agglomerate_below=a.agglomerate_below)
+    amg, fphi, frhs, fres, grid = (case[k] for k in ("amg", "fphi", "frhs", "fres", "grid"))
+    norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
+    norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(a.iters)]
+    comm.synchronize()
+    out = {"norms": np.array(norms), "transport": np.array(comm.transport)}
+    for i in range(grid.num_local):
+        out[f"box{i}"] = np.array(grid.local_box(i))
+        out[f"phi{i}"] = fphi.download(i)
+    np.savez(os.path.join(a.out, f"rank{a.rank}.npz"), **out)
+    dist.barrier()
+    del amg, case
+    dist.destroy_process_group()
+    print(json.dumps({"rank": a.rank, "norms": norms}), flush=True)
+    del torch
+
+
+if __name__ == "__main__":
+    main()

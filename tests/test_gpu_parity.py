@@ -40,6 +40,20 @@ def comm():
     return mg.Comm()
 
 
+def remote_comm(kind, arena_mb=32):
+    """A one-rank communicator whose same-rank copies travel the remote path:
+    "rccl" -- RCCL self send/recv; "ipc" -- the peer-mapped transport's put /
+    get kernels and device flags (csrc/transport.hip) on its own arena."""
+    if kind == "rccl":
+        c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+        assert c.uses_rccl
+    else:
+        c = mg.Comm(transport="ipc", arena_bytes=arena_mb << 20)
+        assert c.transport == "ipc"
+    c.set_self_messages(True)
+    return c
+
+
 def make_fields(comm, boxes, dom, dx, periodic=(0, 0, 0), owners=None):
     grid = mg.Grid(comm, dom, boxes, dx, periodic=periodic, owners=owners)
     return grid
@@ -289,15 +303,15 @@ def test_vcycle_ragged_mixed_bc_bitwise(rng, comm, fused, bvar):
     assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
 
 
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
 @pytest.mark.parametrize("fused", [2, 3])
 @pytest.mark.parametrize("overlap", [0, 2, 4])
-def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, overlap):
-    # the RCCL pack -> send/recv -> unpack path, exercised on one GPU by
-    # routing same-rank copies through self send/recv
+def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, overlap, transport):
+    # the remote path (RCCL pack -> send/recv -> unpack, or the peer-mapped
+    # put / get kernels), exercised on one GPU by routing same-rank copies
+    # through self messages
     c_local = mg.Comm()
-    c_rccl = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
-    c_rccl.set_self_messages(True)
-    assert c_rccl.uses_rccl
+    c_rccl = remote_comm(transport)
     n = 32
     out = []
     for c in (c_local, c_rccl):
@@ -404,21 +418,24 @@ def test_overlapped_halo_large_periodic_box_bitwise(rng, rccl):
         assert np.array_equal(out[0][1], r[1])
 
 
+@pytest.mark.parametrize("bvar", [True, False])
 @pytest.mark.parametrize("nsmooth", [1, 3, 4])
 @pytest.mark.parametrize("periodic", [(0, 0, 0), (1, 0, 1)])
 @pytest.mark.parametrize("parts,n,fused", [((2, 2, 2), 32, 1), ((2, 1, 3), 48, 2), ((3, 2, 1), 48, 3)])
-def test_deep_halo_vcycle_bitwise(rng, nsmooth, periodic, parts, n, fused):
+def test_deep_halo_vcycle_bitwise(rng, nsmooth, periodic, parts, n, fused, bvar):
     # 4-deep shells, two sweeps per exchange (grown-box first sweep): the same
     # V-cycle iterates as the 2-deep schedule and the oracle, bit for bit, on
-    # local copies and RCCL self messages, down to 4-cell coarse boxes
-    for c in (mg.Comm(), None):
-        if c is None:
-            c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
-            c.set_self_messages(True)
+    # local copies, RCCL self messages and the peer-mapped transport, down to
+    # 4-cell coarse boxes.  bvar=False (bCoef = 1, detected constant) routes
+    # sweep pairs through the two-sweep kernel k_gsrb_tb2 on exchanged faces:
+    # odd counts (a pair, then a single sweep after a 2-deep shell), periodic
+    # self-exchanged faces, ragged boxes and the zero-input first pair
+    for kind in ("local", "rccl", "ipc"):
+        c = mg.Comm() if kind == "local" else remote_comm(kind)
         out = []
         for deep in (0, 1):
             S = build_pair(c, np.random.default_rng(9), n, parts, periodic=periodic, alpha=1.0,
-                           nlevels=3, bottom=0, fused=fused, overlap=0, deep=deep)
+                           nlevels=3, bottom=0, fused=fused, overlap=0, deep=deep, bvar=bvar)
             amg = mg.AMRMultiGrid(S["fac"], mg.SolverParams(max_depth=2, n_pre=nsmooth,
                                                             n_post=nsmooth, n_bottom=nsmooth,
                                                             bottom_solver=0))
@@ -867,12 +884,10 @@ def test_full_size_512_eight_boxes_rccl_deep_halo_bitwise():
     bh = prm.bh()
     bh["domain_length"] = dx * n
     out = []
-    for parts, deep in (((1, 1, 1), 0), ((2, 2, 2), 1)):
-        if parts == (1, 1, 1):
-            c = mg.Comm()
-        else:
-            c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
-            c.set_self_messages(True)
+    for parts, deep, kind in (((1, 1, 1), 0, "local"), ((2, 2, 2), 1, "rccl"),
+                              ((2, 2, 2), 1, "ipc")):
+        # one rank owns all 8 boxes: its self message carries every shell
+        c = mg.Comm() if kind == "local" else remote_comm(kind, arena_mb=256)
         dom, boxes, owners = decompose((n, n, n), 1, boxes_per_rank=parts)
         grid = mg.Grid(c, dom, boxes, dx, owners=owners)
         fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
@@ -890,5 +905,6 @@ def test_full_size_512_eight_boxes_rccl_deep_halo_bitwise():
         norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(2)]
         out.append((norms, download_global(fphi, grid, (n,) * 3)))
         del amg, fa, fb, frhs, fphi, fres, grid
-    assert out[0][0] == out[1][0]
-    assert np.array_equal(out[0][1], out[1][1])
+    for r in out[1:]:
+        assert out[0][0] == r[0]
+        assert np.array_equal(out[0][1], r[1])

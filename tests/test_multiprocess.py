@@ -1,0 +1,100 @@
+"""BASELINE config C4's real form on the GPU box: separate processes (one
+box each, bench.py's split), halo exchange between processes through the
+peer-mapped transport (csrc/transport.hpp: hipIpcOpenMemHandle-mapped
+receive arenas, device-side flags), all ranks on device 0 of the one-GPU
+box.  phi and every residual max norm must be bit-identical to the single
+box computed in this process (itself bit-identical to the oracle:
+test_gpu_parity.py::test_full_size_512_vcycle_bitwise).
+
+The workers are fresh interpreters (tests/mp_worker.py) started with
+subprocess (no fork of this GPU-initialised process, no exec).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+mg = pytest.importorskip("mg_ic_code_amd")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240):
+    port = free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONUNBUFFERED="1")
+    procs = []
+    logs = []
+    for r in range(world):
+        log = open(tmp_path / f"w{r}.log", "w")
+        logs.append(log)
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), "--rank", str(r),
+             "--world", str(world), "--port", str(port), "--n", str(n), "--levels", str(levels),
+             "--agglomerate-below", str(agglomerate_below), "--out", str(tmp_path)],
+            stdout=log, stderr=subprocess.STDOUT, env=env))
+    rcs = []
+    try:
+        for p in procs:
+            rcs.append(p.wait(timeout=timeout))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for log in logs:
+            log.close()
+    if any(rcs):
+        msg = "\n".join((tmp_path / f"w{r}.log").read_text()[-3000:] for r in range(world))
+        pytest.fail(f"workers exited {rcs}:\n{msg}")
+    out = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
+    return out
+
+
+def single_box(n, levels, iters=2):
+    import bench
+    comm = mg.Comm()
+    case = bench.build_case(mg, comm, 1, n, levels, 4)
+    amg, fphi, frhs, fres = (case[k] for k in ("amg", "fphi", "frhs", "fres"))
+    norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
+    norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(iters)]
+    return norms, fphi.download(0)
+
+
+def check(out, n, levels, iters=2):
+    norms, phi = single_box(n, levels, iters)
+    for o in out:
+        assert str(o["transport"]) == "ipc"
+        assert list(o["norms"]) == norms, (list(o["norms"]), norms)
+        i = 0
+        while f"box{i}" in o:
+            b = o[f"box{i}"]
+            assert np.array_equal(o[f"phi{i}"], phi[b[2]:b[5] + 1, b[1]:b[4] + 1, b[0]:b[3] + 1])
+            i += 1
+    assert norms[-1] < norms[0]
+
+
+def test_two_processes_bench_split_512_bitwise(tmp_path):
+    # bench.py --gpus 2's exact workload: 512^3 as two 512x512x256 z-slabs, one
+    # per process, deep halo (4-deep shells), 3 levels
+    n, levels = 512, 3
+    check(run_workers(tmp_path, 2, n, levels), n, levels)
+
+
+def test_four_processes_with_agglomeration_bitwise(tmp_path):
+    # bench.py --gpus 4's split (1x2x2) at 128^3, deep halo, the 32^3 depth
+    # gathered to rank 0 (agglomerate_below 17: its 32x16x16 boxes), so the
+    # gather / scatter plans run between processes too
+    n, levels = 128, 3
+    check(run_workers(tmp_path, 4, n, levels, agglomerate_below=17), n, levels)
