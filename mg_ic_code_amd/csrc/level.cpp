@@ -34,6 +34,8 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
     arena_bytes = (size_t)(e ? atol(e) : 64) << 20;
   }
   arena_bytes_ = (arena_bytes + 255) & ~(size_t)255;
+  MGIC_CHECK(arena_bytes_ < ((size_t)1 << 31), "transport arena buffer must stay below 2 GB "
+                                               "(32-bit buffer offsets)");
   MGIC_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   own_stream_ = true;
   MGIC_HIP(hipMalloc(&d_result_, 2 * sizeof(double)));
@@ -51,6 +53,9 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   peer_arena_.assign(size, nullptr);
   sent_.assign(size, 0);
   recvd_.assign(size, 0);
+  sent_blocks_.assign(size, 0);
+  sent_prev_.assign(size, 0);
+  recvd_blocks_.assign(size, 0);
   peer_sig_[rank] = sig_;
   peer_arena_[rank] = arena_;
   if (size > 1) {
@@ -80,32 +85,27 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   }
 }
 
-void Comm::ipc_send(int peer, void **slot, const unsigned long long **wait,
-                    unsigned long long *wait_val, unsigned long long **flag,
-                    unsigned long long *flag_val) {
+void Comm::ipc_send(int peer, long nblocks, void **slot, const unsigned long long **wait,
+                    unsigned long long *wait_val, unsigned long long **count) {
   const unsigned long long m = sent_[peer]++;  // my message number m to peer (0-based)
   *slot = peer_arena_[peer] + ((size_t)rank_ * 2 + (m & 1)) * arena_bytes_;
-  *wait = sig_ + kern::kSigAck + peer * kern::kSigStride;  // message m - 2 consumed
-  *wait_val = m >= 1 ? m - 1 : 0;
-  *flag = peer_sig_[peer] + kern::kSigArr + rank_ * kern::kSigStride;
-  *flag_val = m + 1;
+  // the slot last held message m - 2: wait until the peer has acknowledged
+  // every block up to and including it (= the blocks sent before message m - 1)
+  *wait = sig_ + kern::kSigAck + peer * kern::kSigStride;
+  *wait_val = sent_prev_[peer];
+  *count = peer_sig_[peer] + kern::kSigArr + rank_ * kern::kSigStride;
+  sent_prev_[peer] = sent_blocks_[peer];
+  sent_blocks_[peer] += (unsigned long long)nblocks;
 }
 
-void Comm::ipc_recv(int src, void **slot, const unsigned long long **wait,
-                    unsigned long long *wait_val, unsigned long long **flag,
-                    unsigned long long *flag_val) {
+void Comm::ipc_recv(int src, long nblocks, void **slot, const unsigned long long **wait,
+                    unsigned long long *wait_val, unsigned long long **count) {
   const unsigned long long m = recvd_[src]++;
   *slot = arena_ + ((size_t)src * 2 + (m & 1)) * arena_bytes_;
-  *wait = sig_ + kern::kSigArr + src * kern::kSigStride;  // message m delivered
-  *wait_val = m + 1;
-  *flag = peer_sig_[src] + kern::kSigAck + rank_ * kern::kSigStride;
-  *flag_val = m + 1;
-}
-
-void Comm::ipc_ticket(long blocks, unsigned long long **ticket, unsigned long long *end) {
-  ticket_ += (unsigned long long)blocks;
-  *ticket = sig_ + kern::kSigTicket;
-  *end = ticket_;
+  recvd_blocks_[src] += (unsigned long long)nblocks;
+  *wait = sig_ + kern::kSigArr + src * kern::kSigStride;  // every block of message m delivered
+  *wait_val = recvd_blocks_[src];
+  *count = peer_sig_[src] + kern::kSigAck + rank_ * kern::kSigStride;
 }
 
 void Comm::ipc_err_async(hipStream_t st) {
@@ -419,6 +419,8 @@ CopyPlan::~CopyPlan() {
   if (d_unpack_) (void)hipFree(d_unpack_);
   if (d_ipc_pack_) (void)hipFree(d_ipc_pack_);
   if (d_ipc_unpack_) (void)hipFree(d_ipc_unpack_);
+  if (d_put_blocks_) (void)hipFree(d_put_blocks_);
+  if (d_get_blocks_) (void)hipFree(d_get_blocks_);
   if (sendbuf_) (void)hipFree(sendbuf_);
   if (recvbuf_) (void)hipFree(recvbuf_);
 }
@@ -478,6 +480,27 @@ void CopyPlan::finalize() {
     long dummy = 0;
     d_ipc_pack_ = upload_items(ip, dummy);
     d_ipc_unpack_ = upload_items(iu, dummy);
+    // block tables: every item split into ipc_blocks(cells) blocks, the same
+    // split on the sending and the receiving side, so counts match per message
+    auto blocks = [](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> &per,
+                     int &n) {
+      std::vector<kern::IpcBlock> b;
+      per.assign(npeers, 0);
+      for (size_t i = 0; i < v.size(); ++i) {
+        const long nb = kern::ipc_blocks((long)v[i].nx * v[i].ny * v[i].nz);
+        for (long s = 0; s < nb; ++s) b.push_back({(int)i, (int)s});
+        per[v[i].pad] += nb;
+      }
+      n = (int)b.size();
+      kern::IpcBlock *d = nullptr;
+      if (!b.empty()) {
+        MGIC_HIP(hipMalloc(&d, sizeof(kern::IpcBlock) * b.size()));
+        MGIC_HIP(hipMemcpy(d, b.data(), sizeof(kern::IpcBlock) * b.size(), hipMemcpyHostToDevice));
+      }
+      return d;
+    };
+    d_put_blocks_ = blocks(ip, send_peers_.size(), send_blocks_, n_put_blocks_);
+    d_get_blocks_ = blocks(iu, recv_peers_.size(), recv_blocks_, n_get_blocks_);
   }
   final_ = true;
 }
@@ -493,28 +516,24 @@ void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hip
     pp.n = (int)send_peers_.size();
     pp.err = comm.ipc_err();
     for (int q = 0; q < pp.n; ++q)
-      comm.ipc_send(send_peers_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q], &pp.flag[q],
-                    &pp.flag_val[q]);
-    comm.ipc_ticket((long)kern::ipc_grid_x(max_pack_) * (long)pack_.size(), &pp.ticket,
-                    &pp.ticket_end);
+      comm.ipc_send(send_peers_[q], send_blocks_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q],
+                    &pp.count[q]);
     if constexpr (std::is_same<T, double>::value)
-      kern::ipc_put(d_ipc_pack_, (int)pack_.size(), max_pack_, src_tab, pp, st);
+      kern::ipc_put(d_ipc_pack_, d_put_blocks_, n_put_blocks_, src_tab, pp, st);
     else
-      kern::ipc_put_f(d_ipc_pack_, (int)pack_.size(), max_pack_, src_tab, pp, st);
+      kern::ipc_put_f(d_ipc_pack_, d_put_blocks_, n_put_blocks_, src_tab, pp, st);
   }
   if (!unpack_.empty()) {
     kern::IpcPeers pp{};
     pp.n = (int)recv_peers_.size();
     pp.err = comm.ipc_err();
     for (int q = 0; q < pp.n; ++q)
-      comm.ipc_recv(recv_peers_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q], &pp.flag[q],
-                    &pp.flag_val[q]);
-    comm.ipc_ticket((long)kern::ipc_grid_x(max_unpack_) * (long)unpack_.size(), &pp.ticket,
-                    &pp.ticket_end);
+      comm.ipc_recv(recv_peers_[q], recv_blocks_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q],
+                    &pp.count[q]);
     if constexpr (std::is_same<T, double>::value)
-      kern::ipc_get(d_ipc_unpack_, (int)unpack_.size(), max_unpack_, dst_tab, pp, st);
+      kern::ipc_get(d_ipc_unpack_, d_get_blocks_, n_get_blocks_, dst_tab, pp, st);
     else
-      kern::ipc_get_f(d_ipc_unpack_, (int)unpack_.size(), max_unpack_, dst_tab, pp, st);
+      kern::ipc_get_f(d_ipc_unpack_, d_get_blocks_, n_get_blocks_, dst_tab, pp, st);
   }
 }
 

@@ -70,14 +70,15 @@ class Comm {
 
   // ---- peer-mapped transport (transport.hpp)
   size_t ipc_arena_bytes() const { return arena_bytes_; }
-  // message slot of my next message to `peer` in its arena, the ack word to
-  // wait on and the counter to raise; then count it as sent
-  void ipc_send(int peer, void **slot, const unsigned long long **wait, unsigned long long *wait_val,
-                unsigned long long **flag, unsigned long long *flag_val);
-  void ipc_recv(int src, void **slot, const unsigned long long **wait, unsigned long long *wait_val,
-                unsigned long long **flag, unsigned long long *flag_val);
-  // the ticket words of a launch of `blocks` blocks
-  void ipc_ticket(long blocks, unsigned long long **ticket, unsigned long long *end);
+  // my next message to `peer` (nblocks put blocks): its slot in the peer's
+  // arena, the acknowledgement count to wait for (the slot's previous
+  // message consumed) and the peer's counter my blocks add to
+  void ipc_send(int peer, long nblocks, void **slot, const unsigned long long **wait,
+                unsigned long long *wait_val, unsigned long long **count);
+  // my next message from `src` (nblocks blocks): its slot in my arena, the
+  // delivered-block count that completes it, the sender's ack counter
+  void ipc_recv(int src, long nblocks, void **slot, const unsigned long long **wait,
+                unsigned long long *wait_val, unsigned long long **count);
   unsigned long long *ipc_err() const { return sig_ + kern::kSigErr; }
   // raise if a transport wait of this rank timed out (synchronizes the stream)
   void ipc_check();
@@ -105,8 +106,10 @@ class Comm {
   size_t arena_bytes_ = 0;
   std::vector<unsigned long long *> peer_sig_;   // per rank (mine at [rank_])
   std::vector<char *> peer_arena_;
-  std::vector<unsigned long long> sent_, recvd_; // messages per peer so far
-  unsigned long long ticket_ = 0, red_count_ = 0;
+  std::vector<unsigned long long> sent_, recvd_;  // messages per peer so far
+  // cumulative blocks per peer: sent (after the last message / before it), received
+  std::vector<unsigned long long> sent_blocks_, sent_prev_, recvd_blocks_;
+  unsigned long long red_count_ = 0;
   unsigned long long *h_err_ = nullptr;          // pinned
 };
 
@@ -136,7 +139,10 @@ class CopyPlan {
   // the peer-mapped transport's item tables: offsets within one peer's
   // message, pad = index into the plan's peer list
   CopyItem *d_ipc_pack_ = nullptr, *d_ipc_unpack_ = nullptr;
+  kern::IpcBlock *d_put_blocks_ = nullptr, *d_get_blocks_ = nullptr;
+  int n_put_blocks_ = 0, n_get_blocks_ = 0;
   std::vector<int> send_peers_, recv_peers_;
+  std::vector<long> send_blocks_, recv_blocks_;  // per peer of the lists above
   long max_local_ = 0, max_pack_ = 0, max_unpack_ = 0;
   double *sendbuf_ = nullptr, *recvbuf_ = nullptr;
   bool final_ = false, host_final_ = false;

@@ -1,22 +1,24 @@
 // transport.hpp -- the cross-process halo transport (peer-mapped buffers and
-// device-side flags), the second transport beside RCCL send/recv.
+// device-side counters), the second transport beside RCCL send/recv.
 //
 // Every rank maps, through hipIpcOpenMemHandle, every other rank's
-//   * signal page: 64 KB of uncached device memory holding per-peer message
-//     counters, acknowledgements, a launch ticket, an error word and the
-//     allreduce slots;
+//   * signal page: 64 KB of uncached device memory holding per-peer block
+//     counters, acknowledgements, an error word and the allreduce slots;
 //   * receive arena: size x 2 message buffers (double-buffered per sender).
 // An exchange (CopyPlan) is then two launches and no host round trip:
-//   put  -- reads my boxes' boundary regions and stores them, write-through
-//           (system-scope stores), straight into each peer's arena slot; the
-//           grid's last block raises each peer's message counter for me;
-//   get  -- each block waits for its peer's counter, acquires, copies the
-//           message into my ghost cells; the last block acknowledges the
-//           slot to each sender.
-// Counters are cumulative per (sender, receiver) pair, so no reset is ever
-// needed; every poll is bounded in time and records a timeout in the error
-// word (Comm::ipc_check raises it on the host) instead of hanging the GPU.
-// The same kernels serve a single process with self messages (tests).
+//   put  -- each block copies its share of my boundary regions, with
+//           write-through (system-scope) 16-B stores, straight into the
+//           peer's arena slot, drains them and adds 1 to the peer's counter
+//           for me;
+//   get  -- each block waits until the sender's counter covers the whole
+//           message, reads it with system-scope loads into my ghost cells and
+//           adds 1 to the sender's acknowledgement counter.
+// Both sides split an item into blocks the same way (ipc_blocks), so the
+// counters count blocks; they are cumulative per (sender, receiver) pair, so
+// nothing is ever reset, and no ticket or last-block step is needed.  Every
+// poll is bounded in time and records a timeout in the error word
+// (Comm::ipc_check raises it on the host) instead of hanging the GPU.  The
+// same kernels serve a single process with self messages (tests).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -31,9 +33,8 @@ constexpr int kMaxIpcRanks = 64;  // ranks of one job (one node: 8 GPUs)
 
 // signal page layout, in 64-bit words; every counter on its own 128-B line
 constexpr int kSigStride = 16;
-constexpr int kSigArr = 0;           // arr[r]: messages rank r has delivered to me
-constexpr int kSigAck = 1024;        // ack[r]: my messages rank r has consumed
-constexpr int kSigTicket = 2048;     // this rank's launch ticket (last-block detection)
+constexpr int kSigArr = 0;           // arr[r]: message blocks rank r has delivered to me
+constexpr int kSigAck = 1024;        // ack[r]: blocks of my messages rank r has consumed
 constexpr int kSigErr = 2064;        // timeouts observed by this rank
 constexpr int kSigRedCnt = 3072;     // red_cnt[r]: allreduce contributions of rank r
 constexpr int kSigRedVal = 4096;     // val[parity][r] at kSigRedVal + parity * 1024 + r * 16
@@ -41,16 +42,20 @@ constexpr int kSigWords = 8192;      // 64 KB
 constexpr unsigned long long kIpcTimeoutTicks = 1000000000ull;  // 10 s of the 100 MHz clock
 
 struct IpcPeers {
-  int n;                                       // peers of this launch
-  unsigned long long *ticket;                  // my ticket word
-  unsigned long long ticket_end;               // its value after this launch's last block
-  unsigned long long *err;                     // my error word
-  unsigned long long *flag[kMaxIpcPeers];      // raised by the last block (a peer's page)
-  unsigned long long flag_val[kMaxIpcPeers];
+  int n;                                         // peers of this launch
+  unsigned long long *err;                       // my error word
+  unsigned long long *count[kMaxIpcPeers];       // +1 per block when done (a peer's page)
   const unsigned long long *wait[kMaxIpcPeers];  // polled before a block copies (my page)
   unsigned long long wait_val[kMaxIpcPeers];
-  void *buf[kMaxIpcPeers];                     // message slot: put -> peer arena, get -> mine
+  void *buf[kMaxIpcPeers];                       // message slot: put -> peer arena, get -> mine
 };
+
+// one block of a put / get launch: its item and its share of the item
+struct IpcBlock {
+  int item, sub;
+};
+constexpr long kIpcBlockElems = 4096;  // elements per block (16 per thread)
+inline long ipc_blocks(long cells) { return (cells + kIpcBlockElems - 1) / kIpcBlockElems; }
 
 struct IpcReduce {
   int size, rank, parity;
@@ -58,19 +63,16 @@ struct IpcReduce {
   unsigned long long *sig[kMaxIpcRanks];       // every rank's signal page (mine at [rank])
 };
 
-// blocks of an ipc_put / ipc_get launch over `nitems` items (the ticket needs
-// the count before the launch)
-int ipc_grid_x(long max_cells);
 // put: items' src = local box, doff = element offset in the peer's message,
-// pad = index into pp's peer arrays
-void ipc_put(const CopyItem *items, int nitems, long max_cells, double *const *src_tab,
+// pad = index into pp's peer arrays; blocks: nblocks (item, sub) entries
+void ipc_put(const CopyItem *items, const IpcBlock *blocks, int nblocks, double *const *src_tab,
              const IpcPeers &pp, hipStream_t st);
-void ipc_put_f(const CopyItem *items, int nitems, long max_cells, float *const *src_tab,
+void ipc_put_f(const CopyItem *items, const IpcBlock *blocks, int nblocks, float *const *src_tab,
                const IpcPeers &pp, hipStream_t st);
 // get: items' dst = local box, soff = element offset in the sender's message
-void ipc_get(const CopyItem *items, int nitems, long max_cells, double *const *dst_tab,
+void ipc_get(const CopyItem *items, const IpcBlock *blocks, int nblocks, double *const *dst_tab,
              const IpcPeers &pp, hipStream_t st);
-void ipc_get_f(const CopyItem *items, int nitems, long max_cells, float *const *dst_tab,
+void ipc_get_f(const CopyItem *items, const IpcBlock *blocks, int nblocks, float *const *dst_tab,
                const IpcPeers &pp, hipStream_t st);
 // in-place allreduce of one device double over all ranks (op 0 sum, 1 max),
 // reduced in rank order on every rank (identical results everywhere)

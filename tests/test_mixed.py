@@ -267,3 +267,66 @@ def test_mixed_vcycle_at_scale_converges_like_fp64(comm):
     for i in (1, 2, 3):
         assert mix[i] < 1.5 * f64[i]
     assert mix[-1] < mix[-2] or mix[-1] < 1e-12 * mix[0]
+
+
+@pytest.mark.gpu
+def test_mixed_fmg_4level_multi_tile_bitwise(comm):
+    # BASELINE config C5's cycle as configs states it: a 4-level FMG (then
+    # V-cycles) in fp32 with the fp64 residual, at a multi-tile size: 272 x
+    # 144 x 80 (depths 272/136/68/34 in x; several fp64 64x22 and fp32 128x32
+    # streaming tiles per plane, ragged last tiles, several z chunks), mixed
+    # Dirichlet / Neumann faces with a boundary value, against the float32
+    # restatement bit for bit -- every depth, every FMG stage
+    import mg_ic_code_amd as mg
+    rng = np.random.default_rng(21)
+    shape = (272, 144, 80)
+    lo = (0, -16, 32)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    dx = 0.17
+    bc_lo, bc_hi, bcv = (0, 1, 0), (0, 0, 1), 0.125
+    a, b, rhs = _problem(rng, shape, False)
+    S = _gpu(comm, dom, [dom], dx, a, b, rhs, 4, 1, bc_lo, bc_hi, bcv)
+    mm = mg.MixedMultiGrid(S["fac"], S["sp"])
+    assert mm.num_depths == 4
+    m = MixedOracle(_oracle(dom, dx, a, b, rhs, 4, bc_lo, bc_hi, bcv), 1.0, -1.0, bc_lo, bc_hi)
+    assert mm.init_residual(S["fphi"], S["frhs"], S["fres"], 0) == \
+        np.abs(m.init_residual(np.zeros(shape[::-1]))).max()
+    assert mm.fmg(S["fphi"], S["frhs"], S["fres"], 0, ncycles=1) == np.abs(m.fmg(1)).max()
+    assert np.array_equal(_phi(S), m.phi)
+    for _ in range(2):
+        assert mm.iteration(S["fphi"], S["frhs"], S["fres"], 0) == np.abs(m.iteration()).max()
+    assert np.array_equal(_phi(S), m.phi)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["local", "rccl", "ipc"])
+def test_mixed_fmg_4level_multibox_matches_single_box(transport):
+    # C5's 4-level FMG on the 8-GPU split (2 x 2 x 2 boxes of 64^3 down to 8^3
+    # at depth 3), every exchange through local copies, RCCL self messages or
+    # the peer-mapped transport (fp32 messages), against the single box bit
+    # for bit
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.decomposition import split_domain
+    rng = np.random.default_rng(22)
+    n = 128
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    a, b, rhs = _problem(rng, (n, n, n), False)
+    out = []
+    for parts in ((1, 1, 1), (2, 2, 2)):
+        if parts == (1, 1, 1) or transport == "local":
+            c = mg.Comm()
+        elif transport == "rccl":
+            c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
+            c.set_self_messages(True)
+        else:
+            c = mg.Comm(transport="ipc", arena_bytes=64 << 20)
+            c.set_self_messages(True)
+        S = _gpu(c, dom, split_domain(dom, parts), 100.0 / n, a, b, rhs, 4, 1)
+        mm = mg.MixedMultiGrid(S["fac"], S["sp"])
+        assert mm.num_depths == 4
+        hist = [mm.init_residual(S["fphi"], S["frhs"], S["fres"], 0),
+                mm.fmg(S["fphi"], S["frhs"], S["fres"], 0)]
+        hist += [mm.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
+        out.append((hist, _phi(S)))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])

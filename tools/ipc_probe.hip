@@ -70,6 +70,59 @@ __global__ void k_put(double *__restrict__ peer_data, unsigned long long *peer_f
   }
 }
 
+// MODE 3: 16-B write-through buffer stores (sc0 sc1), every block drains and
+// adds 1 to the peer's counter (no fence, no ticket); the consumer polls the
+// counter up to iter * blocks and reads with 16-B sc0 sc1 buffer loads
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__global__ void k_put3(double *__restrict__ peer_data, unsigned long long *peer_flags, long n,
+                       int rank, unsigned long long iter) {
+  double *slot = peer_data + (iter & 1) * n;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(slot, (short)0, 0x7fffffff, 0x00020000);
+  const double v = (double)iter * 8.0 + rank;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; 2 * t < n; t += (long)gridDim.x * blockDim.x) {
+    double2 x;
+    x.x = v + (double)((2 * t) & 7) * 0.125;
+    x.y = v + (double)((2 * t + 1) & 7) * 0.125;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, x), rs, (unsigned)(16 * t), 0, 17);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(&peer_flags[rank], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_wait_check3(const double *__restrict__ my_data, unsigned long long *my_flags, long n,
+                              int peer, unsigned long long iter) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = wall_clock64();
+    int good = 1;
+    while (__hip_atomic_load(&my_flags[peer], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
+           iter * gridDim.x) {
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > 200000000ull) {
+        good = 0;
+        break;
+      }
+    }
+    ok = good;
+    if (!good)
+      __hip_atomic_fetch_add(&my_flags[9], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!ok) return;
+  const double *slot = my_data + (iter & 1) * n;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(slot), (short)0, 0x7fffffff, 0x00020000);
+  const double v = (double)iter * 8.0 + peer;
+  unsigned long long bad = 0;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; 2 * t < n; t += (long)gridDim.x * blockDim.x) {
+    const double2 x = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(16 * t), 0, 17));
+    bad += x.x != v + (double)((2 * t) & 7) * 0.125;
+    bad += x.y != v + (double)((2 * t + 1) & 7) * 0.125;
+  }
+  if (bad) __hip_atomic_fetch_add(&my_flags[10], bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void k_fill(double *__restrict__ d, long n, double v) {
   for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < n; t += (long)gridDim.x * blockDim.x)
     d[t] = v + (double)(t & 7) * 0.125;
@@ -166,12 +219,20 @@ int main(int argc, char **argv) {
   auto run = [&](int it0, int it1) {
     for (int it = it0; it <= it1; ++it) {
       CK(hipEventRecord(ev[0], st));
+      if (mode == 3) {
+        k_put3<<<blocks, 256, 0, st>>>(pdata, pflags, n, g_rank, (unsigned long long)it);
+        CK(hipEventRecord(ev[1], st));
+        k_wait_check3<<<blocks, 256, 0, st>>>(data, flags, n, peer, (unsigned long long)it);
+        CK(hipEventRecord(ev[2], st));
+        goto timing;
+      }
       if (mode == 0) k_put<0><<<blocks, 256, 0, st>>>(pdata, pflags, flags, n, g_rank, (unsigned long long)it);
       else if (mode == 1) k_put<1><<<blocks, 256, 0, st>>>(pdata, pflags, flags, n, g_rank, (unsigned long long)it);
       else k_put<2><<<blocks, 256, 0, st>>>(pdata, pflags, flags, n, g_rank, (unsigned long long)it);
       CK(hipEventRecord(ev[1], st));
       k_wait_check<<<blocks, 256, 0, st>>>(data, flags, n, peer, (unsigned long long)it);
       CK(hipEventRecord(ev[2], st));
+    timing:
       if (it % 16 == 0) {
         float a = 0, b = 0;
         CK(hipEventSynchronize(ev[2]));

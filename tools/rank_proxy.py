@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--levels", type=int, default=3)
     ap.add_argument("--local", action="store_true", help="local copies instead of RCCL")
+    ap.add_argument("--transport", choices=("rccl", "ipc"), default="rccl",
+                    help="self messages through RCCL send/recv or the peer-mapped transport")
     ap.add_argument("--deep", type=int, default=0, help="deep halo (two sweeps per exchange)")
     ap.add_argument("--periodic", default="1,1,1", help="periodic directions (exchanged faces)")
     ap.add_argument("--shape", default=None,
@@ -40,6 +42,9 @@ def main():
     n = args.size
     if args.local:
         comm = mg.Comm()
+    elif args.transport == "ipc":
+        comm = mg.Comm(transport="ipc", arena_bytes=64 << 20)
+        comm.set_self_messages(True)
     else:
         comm = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
         comm.set_self_messages(True)
@@ -69,7 +74,7 @@ def main():
     dt = time.perf_counter() - t0
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
     print(json.dumps({"size": n, "shape": shp, "overlap": args.overlap, "deep": args.deep, "periodic": per,
-                      "rccl": not args.local,
+                      "transport": "local" if args.local else args.transport,
                       "vcycles_per_s": round(args.steps / dt, 2),
                       "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
 
