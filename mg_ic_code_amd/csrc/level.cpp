@@ -419,8 +419,7 @@ CopyPlan::~CopyPlan() {
   if (d_unpack_) (void)hipFree(d_unpack_);
   if (d_ipc_pack_) (void)hipFree(d_ipc_pack_);
   if (d_ipc_unpack_) (void)hipFree(d_ipc_unpack_);
-  if (d_put_blocks_) (void)hipFree(d_put_blocks_);
-  if (d_get_blocks_) (void)hipFree(d_get_blocks_);
+  if (d_xblocks_) (void)hipFree(d_xblocks_);
   if (sendbuf_) (void)hipFree(sendbuf_);
   if (recvbuf_) (void)hipFree(recvbuf_);
 }
@@ -480,27 +479,27 @@ void CopyPlan::finalize() {
     long dummy = 0;
     d_ipc_pack_ = upload_items(ip, dummy);
     d_ipc_unpack_ = upload_items(iu, dummy);
-    // block tables: every item split into ipc_blocks(cells) blocks, the same
-    // split on the sending and the receiving side, so counts match per message
-    auto blocks = [](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> &per,
-                     int &n) {
-      std::vector<kern::IpcBlock> b;
-      per.assign(npeers, 0);
+    // one block table for the one-launch exchange: put blocks, then the
+    // same-rank copies, then get blocks; every item split into
+    // ipc_blocks(cells) blocks -- the same split on the sending and the
+    // receiving side, so the block counts match per message
+    std::vector<kern::IpcBlock> tab;
+    auto add = [&](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> *per) {
+      if (per) per->assign(npeers, 0);
+      const size_t n0 = tab.size();
       for (size_t i = 0; i < v.size(); ++i) {
         const long nb = kern::ipc_blocks((long)v[i].nx * v[i].ny * v[i].nz);
-        for (long s = 0; s < nb; ++s) b.push_back({(int)i, (int)s});
-        per[v[i].pad] += nb;
+        for (long b = 0; b < nb; ++b) tab.push_back({(int)i, (int)b});
+        if (per) (*per)[v[i].pad] += nb;
       }
-      n = (int)b.size();
-      kern::IpcBlock *d = nullptr;
-      if (!b.empty()) {
-        MGIC_HIP(hipMalloc(&d, sizeof(kern::IpcBlock) * b.size()));
-        MGIC_HIP(hipMemcpy(d, b.data(), sizeof(kern::IpcBlock) * b.size(), hipMemcpyHostToDevice));
-      }
-      return d;
+      return (int)(tab.size() - n0);
     };
-    d_put_blocks_ = blocks(ip, send_peers_.size(), send_blocks_, n_put_blocks_);
-    d_get_blocks_ = blocks(iu, recv_peers_.size(), recv_blocks_, n_get_blocks_);
+    n_put_blocks_ = add(ip, send_peers_.size(), &send_blocks_);
+    n_loc_blocks_ = add(local_, 0, nullptr);
+    n_get_blocks_ = add(iu, recv_peers_.size(), &recv_blocks_);
+    MGIC_HIP(hipMalloc(&d_xblocks_, sizeof(kern::IpcBlock) * tab.size()));
+    MGIC_HIP(hipMemcpy(d_xblocks_, tab.data(), sizeof(kern::IpcBlock) * tab.size(),
+                       hipMemcpyHostToDevice));
   }
   final_ = true;
 }
@@ -511,42 +510,35 @@ void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hip
   for (auto &kv : send_cnt_)
     MGIC_CHECK((size_t)kv.second <= cap, "exchange message exceeds the transport arena "
                                          "(raise MGIC_IPC_ARENA_MB)");
-  if (!pack_.empty()) {
-    kern::IpcPeers pp{};
-    pp.n = (int)send_peers_.size();
-    pp.err = comm.ipc_err();
-    for (int q = 0; q < pp.n; ++q)
-      comm.ipc_send(send_peers_[q], send_blocks_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q],
-                    &pp.count[q]);
-    if constexpr (std::is_same<T, double>::value)
-      kern::ipc_put(d_ipc_pack_, d_put_blocks_, n_put_blocks_, src_tab, pp, st);
-    else
-      kern::ipc_put_f(d_ipc_pack_, d_put_blocks_, n_put_blocks_, src_tab, pp, st);
-  }
-  if (!unpack_.empty()) {
-    kern::IpcPeers pp{};
-    pp.n = (int)recv_peers_.size();
-    pp.err = comm.ipc_err();
-    for (int q = 0; q < pp.n; ++q)
-      comm.ipc_recv(recv_peers_[q], recv_blocks_[q], &pp.buf[q], &pp.wait[q], &pp.wait_val[q],
-                    &pp.count[q]);
-    if constexpr (std::is_same<T, double>::value)
-      kern::ipc_get(d_ipc_unpack_, d_get_blocks_, n_get_blocks_, dst_tab, pp, st);
-    else
-      kern::ipc_get_f(d_ipc_unpack_, d_get_blocks_, n_get_blocks_, dst_tab, pp, st);
-  }
+  kern::IpcPeers pput{}, pget{};
+  pput.n = (int)send_peers_.size();
+  pput.err = pget.err = comm.ipc_err();
+  for (int q = 0; q < pput.n; ++q)
+    comm.ipc_send(send_peers_[q], send_blocks_[q], &pput.buf[q], &pput.wait[q], &pput.wait_val[q],
+                  &pput.count[q]);
+  pget.n = (int)recv_peers_.size();
+  for (int q = 0; q < pget.n; ++q)
+    comm.ipc_recv(recv_peers_[q], recv_blocks_[q], &pget.buf[q], &pget.wait[q], &pget.wait_val[q],
+                  &pget.count[q]);
+  if constexpr (std::is_same<T, double>::value)
+    kern::ipc_exchange(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
+                       n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget, st);
+  else
+    kern::ipc_exchange_f(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
+                         n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget, st);
 }
 
 void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_tab,
                        hipStream_t st) {
-  if (!local_.empty())
-    kern::copy_items(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
-  if (!send_total_ && !recv_total_) return;
-  MGIC_CHECK(comm.remote_ok(), "remote copies need an RCCL communicator or the peer-mapped transport");
-  if (comm.uses_ipc()) {
+  const bool remote = send_total_ || recv_total_;
+  if (remote && comm.uses_ipc()) {  // local copies included: one launch
     execute_ipc<double>(comm, src_tab, dst_tab, st);
     return;
   }
+  if (!local_.empty())
+    kern::copy_items(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
+  if (!remote) return;
+  MGIC_CHECK(comm.remote_ok(), "remote copies need an RCCL communicator or the peer-mapped transport");
   alloc_buffers();
   if (!pack_.empty())
     kern::copy_items(d_pack_, (int)pack_.size(), max_pack_, src_tab, nullptr, nullptr, sendbuf_, st);
@@ -565,14 +557,15 @@ void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_ta
 
 void CopyPlan::execute_f(Comm &comm, float *const *src_tab, float *const *dst_tab,
                          hipStream_t st) {
-  if (!local_.empty())
-    kern::copy_items_f(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
-  if (!send_total_ && !recv_total_) return;
-  MGIC_CHECK(comm.remote_ok(), "remote copies need an RCCL communicator or the peer-mapped transport");
-  if (comm.uses_ipc()) {
+  const bool remote = send_total_ || recv_total_;
+  if (remote && comm.uses_ipc()) {  // local copies included: one launch
     execute_ipc<float>(comm, src_tab, dst_tab, st);
     return;
   }
+  if (!local_.empty())
+    kern::copy_items_f(d_local_, (int)local_.size(), max_local_, src_tab, nullptr, dst_tab, nullptr, st);
+  if (!remote) return;
+  MGIC_CHECK(comm.remote_ok(), "remote copies need an RCCL communicator or the peer-mapped transport");
   alloc_buffers();
   float *sb = reinterpret_cast<float *>(sendbuf_), *rb = reinterpret_cast<float *>(recvbuf_);
   if (!pack_.empty())

@@ -139,8 +139,8 @@ class CopyPlan {
   // the peer-mapped transport's item tables: offsets within one peer's
   // message, pad = index into the plan's peer list
   CopyItem *d_ipc_pack_ = nullptr, *d_ipc_unpack_ = nullptr;
-  kern::IpcBlock *d_put_blocks_ = nullptr, *d_get_blocks_ = nullptr;
-  int n_put_blocks_ = 0, n_get_blocks_ = 0;
+  kern::IpcBlock *d_xblocks_ = nullptr;  // put, local, get blocks of the one-launch exchange
+  int n_put_blocks_ = 0, n_loc_blocks_ = 0, n_get_blocks_ = 0;
   std::vector<int> send_peers_, recv_peers_;
   std::vector<long> send_blocks_, recv_blocks_;  // per peer of the lists above
   long max_local_ = 0, max_pack_ = 0, max_unpack_ = 0;

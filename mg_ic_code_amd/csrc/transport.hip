@@ -97,12 +97,9 @@ struct Share {
   bool pairs;
   unsigned w, ny, e0, e1;
 };
-template <class T>
-__device__ __forceinline__ Share share(const CopyItem &it, int sub, const T *field, long foff,
-                                       long fsy, long fsz, long moff) {
+__device__ __forceinline__ Share share_of(const CopyItem &it, int sub, bool pairs) {
   Share s;
-  s.pairs = ((it.nx | foff | fsy | fsz | moff) & 1) == 0 &&
-            (reinterpret_cast<uintptr_t>(field) & (2 * sizeof(T) - 1)) == 0;
+  s.pairs = pairs && (it.nx & 1) == 0;
   s.w = s.pairs ? (unsigned)it.nx / 2 : (unsigned)it.nx;
   s.ny = (unsigned)it.ny;
   const unsigned n = s.w * s.ny * (unsigned)it.nz;
@@ -111,63 +108,138 @@ __device__ __forceinline__ Share share(const CopyItem &it, int sub, const T *fie
   s.e1 = min(n, s.e0 + per);
   return s;
 }
-
+// a field region whose rows all start on a 16-B (double) / 8-B (float) pair
 template <class T>
-__global__ __launch_bounds__(256) void k_ipc_put(const CopyItem *__restrict__ items,
-                                                 const IpcBlock *__restrict__ blocks,
-                                                 T *const *__restrict__ src_tab, const IpcPeers pp) {
+__device__ __forceinline__ bool pairable(const T *field, long off, long sy, long sz) {
+  return ((off | sy | sz) & 1) == 0 &&
+         (reinterpret_cast<uintptr_t>(field) & (2 * sizeof(T) - 1)) == 0;
+}
+
+// A block's share in passes of kU elements per thread, each pass issuing all
+// its loads (at clamped indices, never conditional) before its stores: a load
+// cannot move above an earlier store the compiler cannot prove disjoint, so a
+// plain load/store loop would run one memory round trip per element.
+constexpr int kU = 4;
+
+// element offset of message element / pair t in a field region (rows of w)
+struct Rows {
+  unsigned w, ny;
+  long sy, sz;
+  __device__ __forceinline__ long at(unsigned t, unsigned scale) const {
+    const unsigned q = t / w, i = t - q * w;
+    const unsigned k = q / ny, j = q - k * ny;
+    return (long)j * sy + (long)k * sz + (long)scale * i;
+  }
+};
+
+// move a block's element range: load(t) for every t of a pass, then
+// store(t, v) for the in-range ones
+template <class V, class Load, class Store>
+__device__ __forceinline__ void move_share(unsigned e0, unsigned e1, Load load, Store store) {
+  for (unsigned base = e0 + threadIdx.x; base < e1; base += 256u * kU) {
+    V v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) v[u] = load(min(base + 256u * u, e1 - 1));
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (base + 256u * u < e1) store(base + 256u * u, v[u]);
+  }
+}
+
+// put: a block's share of one item, field -> peer's message slot (rows packed:
+// pair t is message elements 2t, 2t+1)
+template <class T>
+__device__ __forceinline__ void put_share(const CopyItem &it, int sub, T *const *src_tab,
+                                          const IpcPeers &pp, int &ok) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
-  const IpcBlock b = blocks[blockIdx.x];
-  const CopyItem it = items[b.item];
-  const int p = it.pad;
-  __shared__ int ok;
+  const int p = __builtin_amdgcn_readfirstlane(it.pad);
   if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err);  // slot free
   __syncthreads();
   if (ok) {
     const T *src = src_tab[it.src] + it.soff;
-    const Share s = share(it, b.sub, src_tab[it.src], it.soff, it.ssy, it.ssz, it.doff);
+    const Share s = share_of(it, sub, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
+                                          (it.doff & 1) == 0);
+    const Rows rw{s.w, s.ny, it.ssy, it.ssz};
     const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
-    for (unsigned t = s.e0 + threadIdx.x; t < s.e1; t += blockDim.x) {
-      const unsigned q = t / s.w, i = t - q * s.w;
-      const unsigned k = q / s.ny, j = q - k * s.ny;
-      const long so = (long)j * it.ssy + (long)k * it.ssz;
-      if (s.pairs)  // message rows are packed: pair t is elements 2t, 2t+1
-        st_sys(r, (unsigned)((it.doff + 2 * (long)t) * sizeof(T)),
-               reinterpret_cast<const V *>(src + so)[i]);
-      else
-        st_sys(r, (unsigned)((it.doff + (long)t) * sizeof(T)), src[so + i]);
-    }
+    const long mo = it.doff;
+    if (s.pairs)
+      move_share<V>(s.e0, s.e1,
+                    [&](unsigned t) { return *reinterpret_cast<const V *>(src + rw.at(t, 2)); },
+                    [&](unsigned t, V v) { st_sys(r, (unsigned)((mo + 2 * (long)t) * sizeof(T)), v); });
+    else
+      move_share<T>(s.e0, s.e1, [&](unsigned t) { return src[rw.at(t, 1)]; },
+                    [&](unsigned t, T v) { st_sys(r, (unsigned)((mo + (long)t) * sizeof(T)), v); });
   }
   ipc_done(pp.count[p]);
 }
 
+// get: a block's share of one item, my message slot -> field ghosts
 template <class T>
-__global__ __launch_bounds__(256) void k_ipc_get(const CopyItem *__restrict__ items,
-                                                 const IpcBlock *__restrict__ blocks,
-                                                 T *const *__restrict__ dst_tab, const IpcPeers pp) {
+__device__ __forceinline__ void get_share(const CopyItem &it, int sub, T *const *dst_tab,
+                                          const IpcPeers &pp, int &ok) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
-  const IpcBlock b = blocks[blockIdx.x];
-  const CopyItem it = items[b.item];
-  const int p = it.pad;
-  __shared__ int ok;
+  const int p = __builtin_amdgcn_readfirstlane(it.pad);
   if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err);  // message complete
   __syncthreads();
   if (ok) {
     T *dst = dst_tab[it.dst] + it.doff;
-    const Share s = share(it, b.sub, dst_tab[it.dst], it.doff, it.dsy, it.dsz, it.soff);
+    const Share s = share_of(it, sub, pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz) &&
+                                          (it.soff & 1) == 0);
+    const Rows rw{s.w, s.ny, it.dsy, it.dsz};
     const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
-    for (unsigned t = s.e0 + threadIdx.x; t < s.e1; t += blockDim.x) {
-      const unsigned q = t / s.w, i = t - q * s.w;
-      const unsigned k = q / s.ny, j = q - k * s.ny;
-      const long d = (long)j * it.dsy + (long)k * it.dsz;
-      if (s.pairs)
-        reinterpret_cast<V *>(dst + d)[i] =
-            ld_sys<V>(r, (unsigned)((it.soff + 2 * (long)t) * sizeof(T)));
-      else
-        dst[d + i] = ld_sys<T>(r, (unsigned)((it.soff + (long)t) * sizeof(T)));
-    }
+    const long mo = it.soff;
+    if (s.pairs)
+      move_share<V>(s.e0, s.e1,
+                    [&](unsigned t) { return ld_sys<V>(r, (unsigned)((mo + 2 * (long)t) * sizeof(T))); },
+                    [&](unsigned t, V v) { *reinterpret_cast<V *>(dst + rw.at(t, 2)) = v; });
+    else
+      move_share<T>(s.e0, s.e1,
+                    [&](unsigned t) { return ld_sys<T>(r, (unsigned)((mo + (long)t) * sizeof(T))); },
+                    [&](unsigned t, T v) { dst[rw.at(t, 1)] = v; });
   }
   ipc_done(pp.count[p]);  // acknowledge to the sender
+}
+
+// local: a block's share of a same-rank copy, field -> field
+template <class T>
+__device__ __forceinline__ void local_share(const CopyItem &it, int sub, T *const *src_tab,
+                                            T *const *dst_tab) {
+  using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
+  const T *src = src_tab[it.src] + it.soff;
+  T *dst = dst_tab[it.dst] + it.doff;
+  const Share s = share_of(it, sub, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
+                                        pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz));
+  const Rows rs{s.w, s.ny, it.ssy, it.ssz}, rd{s.w, s.ny, it.dsy, it.dsz};
+  if (s.pairs)
+    move_share<V>(s.e0, s.e1,
+                  [&](unsigned t) { return *reinterpret_cast<const V *>(src + rs.at(t, 2)); },
+                  [&](unsigned t, V v) { *reinterpret_cast<V *>(dst + rd.at(t, 2)) = v; });
+  else
+    move_share<T>(s.e0, s.e1, [&](unsigned t) { return src[rs.at(t, 1)]; },
+                  [&](unsigned t, T v) { dst[rd.at(t, 1)] = v; });
+}
+
+// one exchange in one launch: blocks [0, npu) put my messages (first, so the
+// peers can start), [npu, npu + nlo) copy the same-rank regions, the rest get
+// my messages.  Blocks are dispatched in index order, so a get block that
+// waits on this launch's own put blocks (self messages) never holds back a
+// put block that has not started.
+template <class T>
+__global__ __launch_bounds__(256) void k_exchange(const CopyItem *__restrict__ put_items,
+                                                  const CopyItem *__restrict__ loc_items,
+                                                  const CopyItem *__restrict__ get_items,
+                                                  const IpcBlock *__restrict__ blocks, int npu,
+                                                  int nlo, T *const *__restrict__ src_tab,
+                                                  T *const *__restrict__ dst_tab,
+                                                  const IpcPeers pput, const IpcPeers pget) {
+  __shared__ int ok;
+  const IpcBlock b = blocks[blockIdx.x];
+  if ((int)blockIdx.x < npu)
+    put_share<T>(put_items[b.item], b.sub, src_tab, pput, ok);
+  else if ((int)blockIdx.x < npu + nlo)
+    local_share<T>(loc_items[b.item], b.sub, src_tab, dst_tab);
+  else
+    get_share<T>(get_items[b.item], b.sub, dst_tab, pget, ok);
 }
 
 __global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned long long *err) {
@@ -200,35 +272,30 @@ inline void check_launch() {
 }  // namespace
 
 template <class T>
-static void put_t(const CopyItem *items, const IpcBlock *blocks, int nblocks, T *const *src_tab,
-                  const IpcPeers &pp, hipStream_t st) {
-  if (nblocks <= 0) return;
-  k_ipc_put<T><<<dim3((unsigned)nblocks), dim3(256), 0, st>>>(items, blocks, src_tab, pp);
-  check_launch();
-}
-template <class T>
-static void get_t(const CopyItem *items, const IpcBlock *blocks, int nblocks, T *const *dst_tab,
-                  const IpcPeers &pp, hipStream_t st) {
-  if (nblocks <= 0) return;
-  k_ipc_get<T><<<dim3((unsigned)nblocks), dim3(256), 0, st>>>(items, blocks, dst_tab, pp);
+static void exchange_t(const CopyItem *put_items, const CopyItem *loc_items,
+                       const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
+                       T *const *src_tab, T *const *dst_tab, const IpcPeers &pput,
+                       const IpcPeers &pget, hipStream_t st) {
+  const int n = npu + nlo + nge;
+  if (n <= 0) return;
+  k_exchange<T><<<dim3((unsigned)n), dim3(256), 0, st>>>(put_items, loc_items, get_items, blocks,
+                                                         npu, nlo, src_tab, dst_tab, pput, pget);
   check_launch();
 }
 
-void ipc_put(const CopyItem *items, const IpcBlock *blocks, int nblocks, double *const *src_tab,
-             const IpcPeers &pp, hipStream_t st) {
-  put_t<double>(items, blocks, nblocks, src_tab, pp, st);
+void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
+                  const IpcBlock *blocks, int npu, int nlo, int nge, double *const *src_tab,
+                  double *const *dst_tab, const IpcPeers &pput, const IpcPeers &pget,
+                  hipStream_t st) {
+  exchange_t<double>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
+                     pput, pget, st);
 }
-void ipc_put_f(const CopyItem *items, const IpcBlock *blocks, int nblocks, float *const *src_tab,
-               const IpcPeers &pp, hipStream_t st) {
-  put_t<float>(items, blocks, nblocks, src_tab, pp, st);
-}
-void ipc_get(const CopyItem *items, const IpcBlock *blocks, int nblocks, double *const *dst_tab,
-             const IpcPeers &pp, hipStream_t st) {
-  get_t<double>(items, blocks, nblocks, dst_tab, pp, st);
-}
-void ipc_get_f(const CopyItem *items, const IpcBlock *blocks, int nblocks, float *const *dst_tab,
-               const IpcPeers &pp, hipStream_t st) {
-  get_t<float>(items, blocks, nblocks, dst_tab, pp, st);
+void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
+                    const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
+                    float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
+                    const IpcPeers &pget, hipStream_t st) {
+  exchange_t<float>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
+                    pput, pget, st);
 }
 
 void ipc_allreduce(double *val, int op, const IpcReduce &r, unsigned long long *err,

@@ -63,17 +63,19 @@ struct IpcReduce {
   unsigned long long *sig[kMaxIpcRanks];       // every rank's signal page (mine at [rank])
 };
 
-// put: items' src = local box, doff = element offset in the peer's message,
-// pad = index into pp's peer arrays; blocks: nblocks (item, sub) entries
-void ipc_put(const CopyItem *items, const IpcBlock *blocks, int nblocks, double *const *src_tab,
-             const IpcPeers &pp, hipStream_t st);
-void ipc_put_f(const CopyItem *items, const IpcBlock *blocks, int nblocks, float *const *src_tab,
-               const IpcPeers &pp, hipStream_t st);
-// get: items' dst = local box, soff = element offset in the sender's message
-void ipc_get(const CopyItem *items, const IpcBlock *blocks, int nblocks, double *const *dst_tab,
-             const IpcPeers &pp, hipStream_t st);
-void ipc_get_f(const CopyItem *items, const IpcBlock *blocks, int nblocks, float *const *dst_tab,
-               const IpcPeers &pp, hipStream_t st);
+// One exchange in one launch over the block table `blocks`: npu put blocks
+// (items: src = local box, doff = offset in the peer's message, pad = peer
+// index in pput), then nlo same-rank copy blocks (loc_items), then nge get
+// blocks (items: dst = local box, soff = offset in the sender's message, pad =
+// peer index in pget).  Every item is split into ipc_blocks(cells) blocks.
+void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
+                  const IpcBlock *blocks, int npu, int nlo, int nge, double *const *src_tab,
+                  double *const *dst_tab, const IpcPeers &pput, const IpcPeers &pget,
+                  hipStream_t st);
+void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
+                    const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
+                    float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
+                    const IpcPeers &pget, hipStream_t st);
 // in-place allreduce of one device double over all ranks (op 0 sum, 1 max),
 // reduced in rank order on every rank (identical results everywhere)
 void ipc_allreduce(double *val, int op, const IpcReduce &r, unsigned long long *err,
