@@ -53,9 +53,11 @@ def parse():
     ap.add_argument("--transport", choices=("auto", "ipc", "rccl"), default="auto",
                     help="N > 1 halo transport: peer-mapped buffers + device flags (ipc), RCCL "
                          "send/recv (rccl), or ipc with an RCCL fallback (auto, default)")
-    ap.add_argument("--agglomerate-below", type=int, default=0,
+    ap.add_argument("--agglomerate-below", type=int, default=-1,
                     help="gather MG depths whose boxes have a side below this to one box on "
-                         "rank 0 (the coarsest levels solved on rank 0); 0 off")
+                         "rank 0 (the coarsest levels solved on rank 0); 0 off; default 32 for "
+                         "N > 1 (DESIGN.md 6: at 3 levels the 8-GPU split's coarsest boxes are "
+                         "64^3 and stay distributed; deeper hierarchies gather from 16^3 down)")
     ap.add_argument("--roofline-events", choices=("relax", "launch"), default="relax",
                     help="HIP events for the smoother roofline: one pair per relax call "
                          "(default; time / launches) or one pair per launch")
@@ -111,7 +113,8 @@ def main():
     case = build_case(mg, comm, world, args.size, args.levels, args.nsmooth, bpr,
                       fused=0 if args.no_fused else 1, overlap=args.overlap,
                       deep_halo=(1 if world > 1 else 0) if args.deep_halo < 0 else args.deep_halo,
-                      agglomerate_below=args.agglomerate_below)
+                      agglomerate_below=(32 if world > 1 else 0) if args.agglomerate_below < 0
+                      else args.agglomerate_below)
     n = args.size
     boxes, grid, fa, frhs, fphi, fres = (case[k] for k in ("boxes", "grid", "fa", "frhs", "fphi",
                                                            "fres"))
@@ -202,7 +205,7 @@ def main():
                 "parallelism": f"domain-decomposition x{world} ({transport} halo exchange)"
                 if world > 1 else "single GPU",
                 "transport": transport,
-                "agglomerate_below": args.agglomerate_below,
+                "agglomerate_below": case["agglomerate_below"],
             },
             "roofline": {
                 "bound": "hbm",
@@ -296,7 +299,8 @@ def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fu
     amg = mg.AMRMultiGrid(fac, sp)
     assert amg.num_depths == levels, amg.num_depths
     return dict(dom=dom, boxes=boxes, owners=owners, dx=dx, grid=grid, fa=fa, fb=fb, frhs=frhs,
-                fphi=fphi, fres=fres, fac=fac, amg=amg, op_params=op_params)
+                fphi=fphi, fres=fres, fac=fac, amg=amg, op_params=op_params,
+                agglomerate_below=agglomerate_below)
 
 
 def host_cpus():

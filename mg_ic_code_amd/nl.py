@@ -106,9 +106,12 @@ def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
             res.constant_K.append(bh["constant_K"])
         set_nl_coefs(psi, a, rhs, bh)  # :155-161
         fac = defineOperatorFactory(grid, a, b, op_params)
+        # N > 1: depths whose boxes are below 32 cells a side are gathered to
+        # one box on rank 0 (the coarsest levels solved on rank 0)
         amg = AMRMultiGrid(fac, SolverParams(max_depth=depth, n_pre=prm.numMGsmooth,
                                              n_post=prm.numMGsmooth, n_bottom=prm.numMGsmooth,
-                                             bottom_solver=bottom_solver))
+                                             bottom_solver=bottom_solver,
+                                             agglomerate_below=32 if grid.comm.size > 1 else 0))
         solver = BiCGStabSolver(MultilevelLinearOp(amg, prm.numMGIterations),
                                 tolerance=prm.tolerance, max_iterations=prm.max_iterations,
                                 norm_type=0)

@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--shape", default=None,
                     help="nx,ny,nz of the rank's box (default: a --size cube); e.g. 512,512,256 "
                          "periodic 0,0,1 for one rank of the 2-GPU z-slab split")
+    ap.add_argument("--parts", default="1,1,1",
+                    help="split the box into this many boxes (all on this rank): the N-GPU "
+                         "split's exchanges and gathers on one GPU")
+    ap.add_argument("--agglomerate-below", type=int, default=0)
     args = ap.parse_args()
     import mg_ic_code_amd as mg
     from mg_ic_code_amd.params import read_params_file
@@ -51,7 +55,9 @@ def main():
     shp = tuple(int(v) for v in args.shape.split(",")) if args.shape else (n, n, n)
     dom = (0, 0, 0, shp[0] - 1, shp[1] - 1, shp[2] - 1)
     per = tuple(int(v) for v in args.periodic.split(","))
-    grid = mg.Grid(comm, dom, [dom], prm.L / n, periodic=per)
+    from mg_ic_code_amd.decomposition import split_domain
+    parts = tuple(int(v) for v in args.parts.split(","))
+    grid = mg.Grid(comm, dom, split_domain(dom, parts), prm.L / n, periodic=per)
     fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
     bh = prm.bh()
     mg.set_binary_bh_coefs(fa, frhs, bh)
@@ -62,7 +68,8 @@ def main():
                            overlap_exchange=args.overlap, deep_halo=args.deep)
     fac = mg.defineOperatorFactory(grid, fa, fb, op)
     amg = mg.AMRMultiGrid(fac, mg.SolverParams(max_depth=args.levels - 1, n_pre=4, n_post=4,
-                                               n_bottom=4, bottom_solver=0))
+                                               n_bottom=4, bottom_solver=0,
+                                               agglomerate_below=args.agglomerate_below))
     amg.init_residual(fphi, frhs, fres, norm_type=0)
     for _ in range(args.warmup):
         amg.iteration(fphi, frhs, fres, norm_type=-1)
@@ -73,7 +80,8 @@ def main():
     comm.synchronize()
     dt = time.perf_counter() - t0
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
-    print(json.dumps({"size": n, "shape": shp, "overlap": args.overlap, "deep": args.deep, "periodic": per,
+    print(json.dumps({"size": n, "shape": shp, "parts": parts,
+                      "agglomerate_below": args.agglomerate_below, "overlap": args.overlap, "deep": args.deep, "periodic": per,
                       "transport": "local" if args.local else args.transport,
                       "vcycles_per_s": round(args.steps / dt, 2),
                       "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
