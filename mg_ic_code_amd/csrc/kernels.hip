@@ -1170,15 +1170,18 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
     const char *e = getenv("MGIC_RESTRICT_NT");
     return e ? atoi(e) : 1;
   }();
+  // MGIC_RESTRICT_NT bit 0: non-temporal rhs / aCoef / bCoef loads, for
+  // every bCoef kind (the same switch in restrict_residual_f)
+  const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
+  const int accu = accumulate ? 1 : 0;
   if (s.bconst && (nt & 1))
-    k_restrict<double, true, 1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(
-        rc, cg, u, rhs, a, b, fg, s, accumulate ? 1 : 0);
+    k_restrict<double, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
   else if (s.bconst)
-    k_restrict<double, true><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(
-        rc, cg, u, rhs, a, b, fg, s, accumulate ? 1 : 0);
+    k_restrict<double, true><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
+  else if (nt & 1)
+    k_restrict<double, false, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
   else
-    k_restrict<double, false><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(
-        rc, cg, u, rhs, a, b, fg, s, accumulate ? 1 : 0);
+    k_restrict<double, false><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
   check_launch();
 }
 
@@ -1403,10 +1406,19 @@ void residual_to_f(float *r, const double *u, const double *rhs, const double *a
     const char *e = getenv("MGIC_RESIDUAL_NT");
     return e ? atoi(e) : 3;
   }();
-  if (s.bconst && nt == 3)
-    k_residual_z2<true, float, 3><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
-  else if (s.bconst) k_residual_z2<true, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
-  else k_residual_z2<false, float><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);
+  // every value of MGIC_RESIDUAL_NT & 3, for both bCoef kinds, as residual()
+#define MGIC_RZ2F(N)                                                                        \
+  do {                                                                                      \
+    if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+    else k_residual_z2<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
+  } while (0)
+  switch (nt & 3) {
+    case 1: MGIC_RZ2F(1); break;
+    case 2: MGIC_RZ2F(2); break;
+    case 3: MGIC_RZ2F(3); break;
+    default: MGIC_RZ2F(0); break;
+  }
+#undef MGIC_RZ2F
   check_launch();
 }
 
@@ -1418,15 +1430,15 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
     const char *e = getenv("MGIC_RESTRICT_NT");
     return e ? atoi(e) : 1;
   }();
+  const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
   if (s.bconst && (nt & 1))
-    k_restrict<float, true, 1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(
-        rc, cg, u, rhs, a, b, fg, s, 0);
+    k_restrict<float, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
   else if (s.bconst)
-    k_restrict<float, true><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a, b,
-                                                                               fg, s, 0);
+    k_restrict<float, true><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
+  else if (nt & 1)
+    k_restrict<float, false, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
   else
-    k_restrict<float, false><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(rc, cg, u, rhs, a,
-                                                                                b, fg, s, 0);
+    k_restrict<float, false><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
   check_launch();
 }
 

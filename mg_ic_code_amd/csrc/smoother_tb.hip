@@ -84,6 +84,15 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_STORE_CPOL
 #define TB2_STORE_CPOL 0
 #endif
+// TB2_NT_INT 1 = the waves whose loads cover only interior rows of the tile
+// (no y halo) load u / rhs / aCoef non-temporally: those lines are read by
+// this tile alone, so keeping them out of L2 leaves it to the halo lines that
+// the neighbouring tiles share.  Measured (r03, three interleaved rounds on
+// one box): 1.39 vs 1.08 ms per 512^3 launch -- the wave-uniform select
+// between the two load forms costs more than L2 gains; off
+#ifndef TB2_NT_INT
+#define TB2_NT_INT 0
+#endif
 // TB2_ZIN_SHORT 0 = ZIN launches run sweep 1 through the generic passes
 #ifndef TB2_ZIN_SHORT
 #define TB2_ZIN_SHORT 1
@@ -200,6 +209,15 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   auto at2 = [](const char *base, unsigned off) {
     asm volatile("" : "+v"(off));
     return *reinterpret_cast<const V *>(base + off);
+  };
+  typedef T VN __attribute__((ext_vector_type(2)));
+  auto at2n = [](const char *base, unsigned off) {  // non-temporal form
+    asm volatile("" : "+v"(off));
+    const VN n = __builtin_nontemporal_load(reinterpret_cast<const VN *>(base + off));
+    V v;
+    v.x = n.x;
+    v.y = n.y;
+    return v;
   };
   auto boff = [&](int x, int y) {  // byte offset of cell (x, y) from the corner
     return (unsigned)(sizeof(T) * (16 + x + (long)(y + 4) * sy));
@@ -321,7 +339,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         pu0[b][i] = 0.0;
         pu1[b][i] = 0.0;
       } else if (NL * NT <= CP || tid + i * NT < CP) {  // (whole waves past the plane skip)
-        const V v = at2(pl, loff[t][i]);
+        // interior-row waves of the first load (TB2_NT_INT): rows 4 .. TY+3
+        const bool nt = TB2_NT_INT && i == 0 && wv * 64 >= 4 * PW && wv * 64 + 63 < (TY + 4) * PW;
+        const V v = nt ? at2n(pl, loff[t][i]) : at2(pl, loff[t][i]);
         pu0[b][i] = v.x;
         pu1[b][i] = v.y;
       }
@@ -362,8 +382,11 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         na1[b][i] = -1.25;
         continue;
       }
-      const V vr = at2(pr, roff[t][i]);
-      const V va = at2(pa, roff[t][i]);
+      // interior-row waves (TB2_NT_INT): wave w holds rows w and NR-1-w, and
+      // rows 3 .. TY+2 are the tile's
+      const bool nt = TB2_NT_INT && NP == 1 && wv >= 3 && wv < NR / 2;
+      const V vr = nt ? at2n(pr, roff[t][i]) : at2(pr, roff[t][i]);
+      const V va = nt ? at2n(pa, roff[t][i]) : at2(pa, roff[t][i]);
       nr0[b][i] = vr.x;
       nr1[b][i] = vr.y;
       na0[b][i] = va.x;
@@ -660,6 +683,11 @@ template <class T, int TX, int TY, int NT>
 void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs &g,
                 const StencilCoefs &s, bool zero_in, double *acc, hipStream_t st) {
   const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
+  // the raw buffer stores address a plane with unsigned 32-bit byte offsets
+  // and drop masked lanes at kDrop = 2^31: every in-plane offset must stay
+  // below that, or valid stores would be dropped silently
+  if ((double)(g.ny + 8) * (double)g.sy * sizeof(T) >= 2147483648.0)
+    throw Error(kBadArg, "two-sweep launch: a plane exceeds the 2 GB buffer-offset range");
   static const int kc_env = [] {
     const char *e = getenv("MGIC_TB2_KC");
     return e ? atoi(e) : 0;

@@ -14,7 +14,7 @@ for spec in "$@"; do
     d=../../gpurun_ab/$name; mkdir -p $d
     $H $F $defs -c smoother_tb.hip -o $d/smoother_tb.o
     $H $F $defs -c smoother.hip -o $d/smoother.o
-    objs=""; for o in kernels level op mixed amr capi chf_dropin; do objs="$objs $o.o"; done
+    objs=""; for o in kernels transport level op mixed amr capi chf_dropin; do objs="$objs $o.o"; done
     $H -shared -fPIC --offload-arch=gfx950 -o $d/libmgic.so $objs $d/smoother_tb.o $d/smoother.o \
        -L/opt/rocm/lib -lrccl -lamdhip64 -Wl,-rpath,/opt/rocm/lib
     echo "built $d/libmgic.so ($defs)"

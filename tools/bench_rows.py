@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--nl-iters", type=int, default=3)
     args = ap.parse_args()
     import mg_ic_code_amd as mg
-    from mg_ic_code_amd.nl import poisson_solve
+    from mg_ic_code_amd.nl import NLDivergenceError, poisson_solve
     from mg_ic_code_amd.params import read_params_file
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prm = read_params_file(os.path.join(root, "tests", "golden", "params.txt"))
@@ -86,10 +86,18 @@ def main():
     gm = mg.Grid(comm, domm, [domm], L / m)
     sync()
     t0 = time.perf_counter()
-    res = poisson_solve(gm, prm, max_depth=2, bottom_solver=0, max_NL_iterations=args.nl_iters)
+    # a truncated loop (--nl-iters) can stop above the divergence threshold
+    # (Main_PoissonSolver.cpp:221-225): record the row as such
+    status = "converged"
+    try:
+        res = poisson_solve(gm, prm, max_depth=2, bottom_solver=0, max_NL_iterations=args.nl_iters)
+        if not res.converged:
+            status = "truncated"
+    except NLDivergenceError as e:
+        res, status = e.result, "diverged or truncated above the 1e-1 threshold"
     sync()
     t_nl = time.perf_counter() - t0
-    out["f2_nl_loop"] = {"config": f"{m}^3 poisson_solve (params.txt)",
+    out["f2_nl_loop"] = {"config": f"{m}^3 poisson_solve (params.txt)", "status": status,
                          "nl_iterations": len(res.dpsi_norms),
                          "linear_iterations": res.linear_iterations,
                          "dpsi_norms": res.dpsi_norms, "s_total": round(t_nl, 3),
