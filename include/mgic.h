@@ -312,6 +312,21 @@ MGIC_API int mgic_amr_init_residual(mgic_amr a, const mgic_field *phi, const mgi
 MGIC_API int mgic_amr_iteration(mgic_amr a, const mgic_field *phi, const mgic_field *rhs,
                                 int norm_type, double *norm);
 MGIC_API int mgic_amr_residual_field(mgic_amr a, int level, mgic_field *out); /* borrowed */
+/* MultilevelLinearOp over the hierarchy (Main_PoissonSolver.cpp:103-117,
+ * 169-170 with max_level > 0; [Chombo] semantics restated, see amr.hpp):
+ * lhs = AMROperator on every level, covered coarse cells zeroed; dot =
+ * sum_l dx_l^3 levelDot; norm 0 = max over levels, 1 / 2 = dx_l^3-weighted */
+MGIC_API int mgic_amr_apply_op(mgic_amr a, const mgic_field *lhs, const mgic_field *x,
+                               int homogeneous);
+MGIC_API int mgic_amr_dot(mgic_amr a, const mgic_field *x, const mgic_field *y, double *out);
+MGIC_API int mgic_amr_norm(mgic_amr a, const mgic_field *x, int ord, double *out);
+/* computeNorm / computeSum (Main_PoissonSolver.cpp:144-145,208-209): covered
+ * coarse cells masked, dx_l^3 weights (x is not modified) */
+MGIC_API int mgic_amr_composite_norm(mgic_amr a, const mgic_field *x, int ord, double *out);
+MGIC_API int mgic_amr_composite_sum(mgic_amr a, const mgic_field *x, double *out);
+/* MultilevelLinearOp::preCond: e = 0, `iters` AMR V-cycle iterations on
+ * (e, r) with homogeneous physical BCs */
+MGIC_API int mgic_amr_precondition(mgic_amr a, const mgic_field *e, const mgic_field *r, int iters);
 
 /* ---- output (WriteOutput.H).  For local box n, planes
  * [k0, k0+nk) of its valid box: the components the reference writes,
@@ -355,6 +370,10 @@ typedef struct {
 MGIC_API void mgic_solve_params_default(mgic_solve_params *p);
 MGIC_API int mgic_mg_solve(mgic_mg mg, mgic_field phi, mgic_field rhs, const mgic_solve_params *p,
                            int *iterations, double *final_norm);
+/* the same solve over an AMR hierarchy (max_level > 0): BiCGStab over
+ * mgic_amr_apply_op, preconditioned by mgic_amr_precondition */
+MGIC_API int mgic_amr_solve(mgic_amr a, const mgic_field *phi, const mgic_field *rhs,
+                            const mgic_solve_params *p, int *iterations, double *final_norm);
 
 /* ---- instrumentation: hipEvents around the smoother launches on boxes of
  * at least min_cells cells (enable 1: a pair per launch; 2: a pair per run of

@@ -180,6 +180,12 @@ SIGNATURES = {
     "mgic_amr_init_residual": [H, POINTER(H), POINTER(H), c_int, PD],
     "mgic_amr_iteration": [H, POINTER(H), POINTER(H), c_int, PD],
     "mgic_amr_residual_field": [H, c_int, PH],
+    "mgic_amr_apply_op": [H, POINTER(H), POINTER(H), c_int],
+    "mgic_amr_dot": [H, POINTER(H), POINTER(H), PD],
+    "mgic_amr_norm": [H, POINTER(H), c_int, PD],
+    "mgic_amr_composite_norm": [H, POINTER(H), c_int, PD],
+    "mgic_amr_composite_sum": [H, POINTER(H), PD],
+    "mgic_amr_precondition": [H, POINTER(H), POINTER(H), c_int],
     "mgic_mixed_create": [H, POINTER(MGParams), PH],
     "mgic_mixed_destroy": [H],
     "mgic_mixed_num_depths": [H, PI],
@@ -188,6 +194,7 @@ SIGNATURES = {
     "mgic_mixed_fmg": [H, H, H, H, c_int, c_int, PD],
     "mgic_solve_params_default": [POINTER(SolveParams)],
     "mgic_mg_solve": [H, H, H, POINTER(SolveParams), PI, PD],
+    "mgic_amr_solve": [H, POINTER(H), POINTER(H), POINTER(SolveParams), PI, PD],
     "mgic_field_grchombo_vars": [H, c_int, c_int, c_int, PD, c_void_p, c_int],
     "mgic_field_solver_vars": [H, H, H, c_int, c_int, c_int, PD, c_void_p, c_int],
     "mgic_field_layout": [H, PI, PI, PD, PI, PI, PI],

@@ -693,6 +693,10 @@ class AMRSolver:
         self._h = h
         self.num_levels = n
 
+    @property
+    def handle(self):
+        return self._h
+
     @staticmethod
     def _f(x):
         return x.handle if x is not None else None
@@ -743,6 +747,44 @@ class AMRSolver:
         call("mgic_amr_residual_field", self._h, int(level), ctypes.byref(h))
         return LevelData(self.levels[level][0], _handle=h, _owner=self)
 
+    def level_op(self, level: int) -> VariableCoeffPoissonOperator:
+        """the operator of AMR level `level` (level 0: its MultiGrid's depth 0)"""
+        h = ctypes.c_void_p()
+        call("mgic_amr_level_op", self._h, int(level), ctypes.byref(h))
+        return VariableCoeffPoissonOperator(h, self.levels[level][0], owner=self, owned=False)
+
+    # MultilevelLinearOp over the hierarchy (one LevelData per level)
+    def applyOp(self, lhs, x, homogeneous: bool = True) -> None:
+        call("mgic_amr_apply_op", self._h, self._fields(lhs), self._fields(x),
+             int(bool(homogeneous)))
+
+    def dotProduct(self, x, y) -> float:
+        out = ctypes.c_double()
+        call("mgic_amr_dot", self._h, self._fields(x), self._fields(y), ctypes.byref(out))
+        return out.value
+
+    def norm(self, x, ord: int = 0) -> float:
+        out = ctypes.c_double()
+        call("mgic_amr_norm", self._h, self._fields(x), int(ord), ctypes.byref(out))
+        return out.value
+
+    def computeNorm(self, x, ord: int = 2) -> float:
+        """computeNorm (Main_PoissonSolver.cpp:208-209): covered cells masked,
+        levels weighted by dx^3"""
+        out = ctypes.c_double()
+        call("mgic_amr_composite_norm", self._h, self._fields(x), int(ord), ctypes.byref(out))
+        return out.value
+
+    def computeSum(self, x) -> float:
+        """computeSum (Main_PoissonSolver.cpp:144-145): covered cells masked,
+        levels weighted by dx^3"""
+        out = ctypes.c_double()
+        call("mgic_amr_composite_sum", self._h, self._fields(x), ctypes.byref(out))
+        return out.value
+
+    def precondition(self, e, r, iters: int = 1) -> None:
+        call("mgic_amr_precondition", self._h, self._fields(e), self._fields(r), int(iters))
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
@@ -751,17 +793,23 @@ class AMRSolver:
 
 
 class MultilevelLinearOp:
-    """MultilevelLinearOp<FArrayBox> on one AMR level (Main_PoissonSolver.cpp:103-117,169-170):
-    the level operator plus the MG preconditioner of `num_mg_iterations` AMRMultiGrid
-    iterations (pre = post = bottom = the SolverParams smoothing counts)."""
+    """MultilevelLinearOp<FArrayBox> (Main_PoissonSolver.cpp:103-117,169-170): the
+    operator plus the MG preconditioner of `num_mg_iterations` AMRMultiGrid iterations
+    (pre = post = bottom = the SolverParams smoothing counts).  Over an AMRMultiGrid
+    (one AMR level: vectors are LevelData) or an AMRSolver (max_level > 0: vectors
+    are one LevelData per level, AMR V-cycles as the preconditioner)."""
 
-    def __init__(self, amg: "AMRMultiGrid", num_mg_iterations: int = 1):
+    def __init__(self, amg, num_mg_iterations: int = 1):
         self.amg = amg
         self.num_mg_iterations = int(num_mg_iterations)
+        self.multilevel = isinstance(amg, AMRSolver)
 
-    def preCond(self, e: LevelData, r: LevelData) -> None:
-        call("mgic_mg_precondition", self.amg.handle, e.handle, r.handle,
-             self.num_mg_iterations)
+    def preCond(self, e, r) -> None:
+        if self.multilevel:
+            self.amg.precondition(e, r, self.num_mg_iterations)
+        else:
+            call("mgic_mg_precondition", self.amg.handle, e.handle, r.handle,
+                 self.num_mg_iterations)
 
 
 class BiCGStabSolver:
@@ -778,7 +826,7 @@ class BiCGStabSolver:
         self.iterations = 0
         self.final_norm = None
 
-    def solve(self, phi: LevelData, rhs: LevelData) -> int:
+    def solve(self, phi, rhs) -> int:
         p = _lib.SolveParams()
         lib.mgic_solve_params_default(ctypes.byref(p))
         p.num_mg_iterations = self.mlop.num_mg_iterations
@@ -787,8 +835,13 @@ class BiCGStabSolver:
         p.norm_type = int(self.m_normType)
         it = ctypes.c_int()
         nrm = ctypes.c_double()
-        call("mgic_mg_solve", self.mlop.amg.handle, phi.handle, rhs.handle, ctypes.byref(p),
-             ctypes.byref(it), ctypes.byref(nrm))
+        if self.mlop.multilevel:  # phi, rhs: one LevelData per AMR level
+            a = self.mlop.amg
+            call("mgic_amr_solve", a.handle, a._fields(phi), a._fields(rhs), ctypes.byref(p),
+                 ctypes.byref(it), ctypes.byref(nrm))
+        else:
+            call("mgic_mg_solve", self.mlop.amg.handle, phi.handle, rhs.handle, ctypes.byref(p),
+                 ctypes.byref(it), ctypes.byref(nrm))
         self.iterations, self.final_norm = it.value, nrm.value
         return it.value
 

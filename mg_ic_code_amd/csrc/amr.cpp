@@ -2,6 +2,9 @@
 // operators, AMR V-cycle (see amr.hpp).
 #include "amr.hpp"
 
+#include <algorithm>
+#include <cmath>
+
 #include "kernels.hpp"
 
 namespace mgic {
@@ -228,6 +231,209 @@ double AMRSolver::iteration(std::vector<LevelData *> &phi, const std::vector<Lev
   for (int l = 0; l < n; ++l) op(l).incr(*phi[l], *L_[l].corr, 1.0);
   for (int l = n - 1; l > 0; --l) L_[l].cf->averageDown(*phi[l - 1], *phi[l], op(l).stream());
   return initResidual(phi, rhs, normType);
+}
+
+// ------------------------------------------------ MultilevelLinearOp + BiCGStab
+double AMRSolver::weight(int l) const {
+  const double dx = L_[l].grid->dx;
+  return dx * dx * dx;
+}
+
+void AMRSolver::zeroCovered(std::vector<LevelData *> &x) {
+  for (int l = 1; l < numLevels(); ++l) L_[l].cf->zeroCovered(*x[l - 1], op(l).stream());
+}
+
+void AMRSolver::applyOp(std::vector<LevelData *> &lhs, std::vector<LevelData *> &x, bool hom) {
+  const int n = numLevels();
+  MGIC_CHECK((int)lhs.size() == n && (int)x.size() == n, "AMR: one field per level");
+  for (int l = 0; l < n; ++l) AMROperator(l, *lhs[l], *x[l], l ? x[l - 1] : nullptr, hom);
+  zeroCovered(lhs);
+}
+
+void AMRSolver::residual(std::vector<LevelData *> &r, std::vector<LevelData *> &phi,
+                         const std::vector<LevelData *> &rhs, bool hom) {
+  const int n = numLevels();
+  MGIC_CHECK((int)r.size() == n && (int)phi.size() == n && (int)rhs.size() == n,
+             "AMR: one field per level");
+  for (int l = 0; l < n; ++l) AMRResidual(l, *r[l], *phi[l], l ? phi[l - 1] : nullptr, *rhs[l], hom);
+  zeroCovered(r);
+}
+
+double AMRSolver::dotProduct(const std::vector<LevelData *> &x, const std::vector<LevelData *> &y) {
+  double s = 0.0;
+  for (int l = 0; l < numLevels(); ++l) s += weight(l) * op(l).dotProduct(*x[l], *y[l]);
+  return s;
+}
+
+double AMRSolver::norm(const std::vector<LevelData *> &x, int ord) {
+  double s = 0.0;
+  for (int l = 0; l < numLevels(); ++l) {
+    const double v = op(l).norm(*x[l], ord);
+    if (ord == 0) s = std::max(s, v);
+    else if (ord == 1) s += weight(l) * v;
+    else s += weight(l) * (v * v);
+  }
+  return ord == 0 || ord == 1 ? s : std::sqrt(s);
+}
+
+std::vector<LevelData *> AMRSolver::masked(const std::vector<LevelData *> &x) {
+  const int n = numLevels();
+  MGIC_CHECK((int)x.size() == n, "AMR: one field per level");
+  if ((int)mask_.size() != n - 1) {
+    mask_.clear();
+    for (int l = 0; l + 1 < n; ++l) mask_.push_back(op(l).create());
+  }
+  std::vector<LevelData *> m(x.begin(), x.end());
+  for (int l = 0; l + 1 < n; ++l) {
+    op(l).assignLocal(*mask_[l], *x[l]);
+    L_[l + 1].cf->zeroCovered(*mask_[l], op(l).stream());
+    m[l] = mask_[l].get();
+  }
+  return m;
+}
+
+double AMRSolver::compositeNorm(const std::vector<LevelData *> &x, int ord) {
+  return norm(masked(x), ord);
+}
+
+double AMRSolver::compositeSum(const std::vector<LevelData *> &x) {
+  // computeSum: sum over the uncovered cells of every level, times dx_l^3
+  // (the level sum as a dot product with a field of ones)
+  std::vector<LevelData *> m = masked(x);
+  std::vector<LevelData *> ones = bicgVec(9);
+  double s = 0.0;
+  for (int l = 0; l < numLevels(); ++l) {
+    op(l).setVal(*ones[l], 1.0);
+    s += weight(l) * op(l).dotProduct(*m[l], *ones[l]);
+  }
+  return s;
+}
+
+std::vector<LevelData *> AMRSolver::bicgVec(int i) {
+  while ((int)bicg_.size() <= i) {
+    std::vector<std::unique_ptr<LevelData>> v;
+    for (int l = 0; l < numLevels(); ++l) v.push_back(op(l).create());
+    bicg_.push_back(std::move(v));
+  }
+  std::vector<LevelData *> out;
+  for (auto &f : bicg_[i]) out.push_back(f.get());
+  return out;
+}
+
+void AMRSolver::precondition(std::vector<LevelData *> &e, const std::vector<LevelData *> &r,
+                             int iters) {
+  const int n = numLevels();
+  MGIC_CHECK((int)e.size() == n && (int)r.size() == n, "AMR: one field per level");
+  for (int l = 0; l < n; ++l) op(l).setToZero(*e[l]);
+  for (int i = 0; i < iters; ++i) {
+    // the first residual r - L(0) (homogeneous BCs) is r itself (covered
+    // cells already zero); later ones are recomputed from e
+    for (int l = 0; l < n; ++l) {
+      if (i == 0) op(l).assignLocal(*L_[l].res, *r[l]);
+      else AMRResidual(l, *L_[l].res, *e[l], l ? e[l - 1] : nullptr, *r[l], true);
+    }
+    if (i > 0)
+      for (int l = 1; l < n; ++l) L_[l].cf->zeroCovered(*L_[l - 1].res, op(l).stream());
+    cycle(n - 1);
+    for (int l = 0; l < n; ++l) op(l).incr(*e[l], *L_[l].corr, 1.0);
+    for (int l = n - 1; l > 0; --l) L_[l].cf->averageDown(*e[l - 1], *e[l], op(l).stream());
+  }
+}
+
+int AMRSolver::solve(std::vector<LevelData *> &phi, const std::vector<LevelData *> &rhs,
+                     const SolveParams &p, double *final_norm) {
+  const int n = numLevels();
+  MGIC_CHECK((int)phi.size() == n && (int)rhs.size() == n, "AMR: one field per level");
+  BiCGStabParams prm = mgp_.bicg;  // reps, small, restarts: BiCGStabSolver defaults
+  prm.imax = p.max_iterations;
+  prm.eps = p.tolerance;
+  prm.normType = p.norm_type;
+  const int iters = std::max(1, p.num_mg_iterations);
+  std::vector<LevelData *> R = bicgVec(0), RT = bicgVec(1), E = bicgVec(2), P = bicgVec(3),
+                           PT = bicgVec(4), S = bicgVec(5), ST = bicgVec(6), T = bicgVec(7),
+                           V = bicgVec(8);
+  auto each = [&](auto f) {
+    for (int l = 0; l < n; ++l) f(l, op(l));
+  };
+  const int nt = prm.normType;
+  residual(R, phi, rhs, false);
+  each([&](int l, VariableCoeffPoissonOperator &o) {
+    o.assignLocal(*RT[l], *R[l]);
+    o.setToZero(*E[l]);
+    o.setToZero(*PT[l]);
+    o.setToZero(*ST[l]);
+    o.setToZero(*P[l]);
+    o.setToZero(*V[l]);
+  });
+  double rho1 = 0.0, rho2 = 0.0, alpha = 0.0, beta = 0.0, omega = 0.0;
+  const double init_norm = norm(R, nt);
+  double nrm = init_norm;
+  int it = 0, restarts = 0;
+  bool init = true;
+  while (it < prm.imax && nrm > prm.eps * init_norm && nrm > prm.reps) {
+    ++it;
+    rho2 = rho1;
+    rho1 = dotProduct(RT, R);
+    if (rho1 == 0.0) break;
+    if (init) {
+      each([&](int l, VariableCoeffPoissonOperator &o) { o.assignLocal(*P[l], *R[l]); });
+      init = false;
+    } else {
+      beta = (rho1 / rho2) * (alpha / omega);
+      each([&](int l, VariableCoeffPoissonOperator &o) {
+        o.bicgP(*P[l], *V[l], *R[l], beta, -beta * omega);
+      });
+    }
+    precondition(PT, P, iters);
+    applyOp(V, PT, true);
+    const double m = dotProduct(RT, V);
+    if (std::fabs(m) > prm.small * std::fabs(rho1)) {
+      alpha = rho1 / m;
+      // S = R - alpha V; E += alpha PT (the level norms combined as norm())
+      double s = 0.0;
+      each([&](int l, VariableCoeffPoissonOperator &o) {
+        const double v = o.axpy2Norm(*S[l], *R[l], *V[l], -alpha, *E[l], *PT[l], alpha, nt);
+        s = nt == 0 ? std::max(s, v) : s + weight(l) * (nt == 1 ? v : v * v);
+      });
+      nrm = nt == 0 || nt == 1 ? s : std::sqrt(s);
+      if (nrm <= prm.eps * init_norm || nrm <= prm.reps) break;
+      precondition(ST, S, iters);
+      applyOp(T, ST, true);
+      double ts = 0.0, tt = 0.0;
+      each([&](int l, VariableCoeffPoissonOperator &o) {
+        double a = 0.0, b = 0.0;
+        o.dot2(*T[l], *S[l], a, b);
+        ts += weight(l) * a;
+        tt += weight(l) * b;
+      });
+      if (tt == 0.0) break;
+      omega = ts / tt;
+      s = 0.0;
+      each([&](int l, VariableCoeffPoissonOperator &o) {
+        const double v = o.axpy2Norm(*R[l], *S[l], *T[l], -omega, *E[l], *ST[l], omega, nt);
+        s = nt == 0 ? std::max(s, v) : s + weight(l) * (nt == 1 ? v : v * v);
+      });
+      nrm = nt == 0 || nt == 1 ? s : std::sqrt(s);
+      if (omega == 0.0) break;
+    } else {
+      if (restarts >= prm.numRestarts) break;
+      ++restarts;
+      each([&](int l, VariableCoeffPoissonOperator &o) { o.incr(*phi[l], *E[l], 1.0); });
+      residual(R, phi, rhs, false);
+      each([&](int l, VariableCoeffPoissonOperator &o) {
+        o.assignLocal(*RT[l], *R[l]);
+        o.setToZero(*E[l]);
+      });
+      nrm = norm(R, nt);
+      init = true;
+    }
+  }
+  each([&](int l, VariableCoeffPoissonOperator &o) { o.incr(*phi[l], *E[l], 1.0); });
+  if (final_norm) {
+    residual(R, phi, rhs, false);
+    *final_norm = norm(R, nt);
+  }
+  return it;
 }
 
 }  // namespace mgic

@@ -77,6 +77,37 @@ class AMRSolver {
                    int normType);
   LevelData &residual(int l) { return *L_[l].res; }
 
+  // ---- MultilevelLinearOp<FArrayBox> over the hierarchy (Main_PoissonSolver.
+  // cpp:103-117,169-184 with max_level > 0).  Vectors are one LevelData per
+  // level.  [Chombo] semantics restated (MultilevelLinearOp is not in the
+  // tree; parity unpinned, pinned to oracle/amr.py): the operator is
+  // AMROperator on every level (CF ghosts from the next coarser level of the
+  // same vector, reflux a no-op) with the covered coarse cells of the result
+  // zeroed, as the composite residual is; dot products and norms therefore
+  // see only uncovered cells wherever one operand is an operator result or a
+  // residual.  dotProduct = sum over levels of dx_l^3 * levelDot; norm 0 =
+  // max over levels; norm 1 / 2 = the dx_l^3-weighted sum / root of sums.
+  void applyOp(std::vector<LevelData *> &lhs, std::vector<LevelData *> &x, bool hom);
+  void residual(std::vector<LevelData *> &r, std::vector<LevelData *> &phi,
+                const std::vector<LevelData *> &rhs, bool hom);
+  double dotProduct(const std::vector<LevelData *> &x, const std::vector<LevelData *> &y);
+  double norm(const std::vector<LevelData *> &x, int ord);
+  // computeNorm / computeSum (the reference's NL-loop diagnostics,
+  // Main_PoissonSolver.cpp:144-145,208-209): covered coarse cells masked,
+  // each level weighted by dx_l^3; ord 0 = max norm, 1 / 2 = L1 / L2
+  double compositeNorm(const std::vector<LevelData *> &x, int ord);
+  double compositeSum(const std::vector<LevelData *> &x);
+  // MultilevelLinearOp::preCond: e = 0 on every level, then `iters` AMR
+  // V-cycle iterations on (e, r) with homogeneous physical BCs (r's covered
+  // coarse cells are zero; e's are the average of the finer level after
+  // every iteration)
+  void precondition(std::vector<LevelData *> &e, const std::vector<LevelData *> &r, int iters);
+  // BiCGStabSolver<Vector<LevelData*>>::solve (the control flow of the
+  // single-level BiCGStabSolver::solve) over applyOp / precondition;
+  // returns the iterations, *final_norm = norm(rhs - L(phi), norm_type)
+  int solve(std::vector<LevelData *> &phi, const std::vector<LevelData *> &rhs,
+            const SolveParams &p, double *final_norm);
+
  private:
   struct Level {
     std::shared_ptr<Grid> grid;
@@ -89,6 +120,14 @@ class AMRSolver {
   MultiGrid base_;  // level 0's MG hierarchy (the l_base solve)
   MGParams mgp_;
   void cycle(int l);
+  // multi-level temporaries of solve() (9 vectors) and the masked copies of
+  // compositeNorm / compositeSum
+  std::vector<std::vector<std::unique_ptr<LevelData>>> bicg_;
+  std::vector<std::unique_ptr<LevelData>> mask_;
+  double weight(int l) const;  // dx_l^3
+  std::vector<LevelData *> bicgVec(int i);
+  void zeroCovered(std::vector<LevelData *> &x);
+  std::vector<LevelData *> masked(const std::vector<LevelData *> &x);
 };
 
 }  // namespace mgic

@@ -1234,6 +1234,84 @@ MGIC_API int mgic_amr_residual_field(mgic_amr a, int level, mgic_field *out) {
   });
 }
 
+MGIC_API int mgic_amr_apply_op(mgic_amr a, const mgic_field *lhs, const mgic_field *x,
+                               int homogeneous) {
+  return guard([&] {
+    NEED(a);
+    NEED(lhs);
+    NEED(x);
+    auto l = amr_fields(a, lhs);
+    auto v = amr_fields(a, x);
+    a->amr.applyOp(l, v, homogeneous != 0);
+  });
+}
+MGIC_API int mgic_amr_dot(mgic_amr a, const mgic_field *x, const mgic_field *y, double *out) {
+  return guard([&] {
+    NEED(a);
+    NEED(x);
+    NEED(y);
+    NEED(out);
+    *out = a->amr.dotProduct(amr_fields(a, x), amr_fields(a, y));
+  });
+}
+MGIC_API int mgic_amr_norm(mgic_amr a, const mgic_field *x, int ord, double *out) {
+  return guard([&] {
+    NEED(a);
+    NEED(x);
+    NEED(out);
+    MGIC_CHECK(ord >= 0 && ord <= 2, "norm order must be 0, 1 or 2");
+    *out = a->amr.norm(amr_fields(a, x), ord);
+  });
+}
+MGIC_API int mgic_amr_composite_norm(mgic_amr a, const mgic_field *x, int ord, double *out) {
+  return guard([&] {
+    NEED(a);
+    NEED(x);
+    NEED(out);
+    MGIC_CHECK(ord >= 0 && ord <= 2, "norm order must be 0, 1 or 2");
+    *out = a->amr.compositeNorm(amr_fields(a, x), ord);
+  });
+}
+MGIC_API int mgic_amr_composite_sum(mgic_amr a, const mgic_field *x, double *out) {
+  return guard([&] {
+    NEED(a);
+    NEED(x);
+    NEED(out);
+    *out = a->amr.compositeSum(amr_fields(a, x));
+  });
+}
+MGIC_API int mgic_amr_precondition(mgic_amr a, const mgic_field *e, const mgic_field *r, int iters) {
+  return guard([&] {
+    NEED(a);
+    NEED(e);
+    NEED(r);
+    MGIC_CHECK(iters >= 0, "iters must be >= 0");
+    auto ev = amr_fields(a, e);
+    a->amr.precondition(ev, amr_fields(a, r), iters);
+  });
+}
+MGIC_API int mgic_amr_solve(mgic_amr a, const mgic_field *phi, const mgic_field *rhs,
+                            const mgic_solve_params *p, int *iterations, double *final_norm) {
+  return guard([&] {
+    NEED(a);
+    NEED(phi);
+    NEED(rhs);
+    SolveParams sp;
+    if (p) {
+      sp.num_mg_iterations = p->num_mg_iterations;
+      sp.max_iterations = p->max_iterations;
+      sp.tolerance = p->tolerance;
+      sp.norm_type = p->norm_type;
+    }
+    MGIC_CHECK(sp.max_iterations >= 0 && sp.tolerance >= 0.0, "bad solve parameters");
+    MGIC_CHECK(sp.norm_type >= 0 && sp.norm_type <= 2, "norm type must be 0, 1 or 2");
+    auto pv = amr_fields(a, phi);
+    double nrm = 0.0;
+    const int it = a->amr.solve(pv, amr_fields(a, rhs), sp, &nrm);
+    if (iterations) *iterations = it;
+    if (final_norm) *final_norm = nrm;
+  });
+}
 MGIC_API int mgic_mg_precondition(mgic_mg mg, mgic_field e, mgic_field r, int iters) {
   return guard([&] {
     NEED(mg);

@@ -21,7 +21,16 @@ output_final_data after the loop (:229), through libmgic_io (output.py).
 After the loop the reference stops with MayDay::Error when the final |dpsi|
 is above 1e-1 (:221-225), before output_final_data: `poisson_solve` raises
 NLDivergenceError at the same point, so a diverged solve writes no
-checkpoint.  Not covered: AMR levels (max_level > 0).
+checkpoint.
+
+max_level > 0 (`grid` a list of Grids, coarsest first, finer ones
+Grid(patches=True) properly nested; set_grids' tagging/regridding is out of
+scope, so the hierarchy is given): every step runs per level as the
+reference's loops over ilev do -- coefficients on every level (:154-160),
+the outer BiCGStab over MultilevelLinearOp with AMR V-cycles as its
+preconditioner (:169-184; AMRSolver), then per level QuadCFInterp of dpsi
+from the coarser level before set_update_psi0 (:189-205), and computeNorm /
+computeSum over the hierarchy with covered cells masked (:144-145, :208).
 """
 from __future__ import annotations
 
@@ -32,7 +41,7 @@ import ctypes
 import math
 import os
 
-from .core import (AMRMultiGrid, BiCGStabSolver, Grid, LevelData, MultilevelLinearOp,
+from .core import (AMRMultiGrid, AMRSolver, BiCGStabSolver, Grid, LevelData, MultilevelLinearOp,
                    OperatorParams, SolverParams, defineOperatorFactory, set_nl_coefs, BH_KEYS)
 from ._lib import call
 from .output import output_final_data, output_solver_data
@@ -55,8 +64,8 @@ class NLDivergenceError(RuntimeError):
 
 @dataclass
 class NLResult:
-    psi: LevelData
-    dpsi: LevelData
+    psi: object   # LevelData, or one per AMR level (max_level > 0)
+    dpsi: object
     dpsi_norms: List[float] = field(default_factory=list)
     linear_iterations: List[int] = field(default_factory=list)
     converged: bool = False
@@ -69,10 +78,15 @@ def set_nl_integrand(psi: LevelData, out: LevelData, bh: dict) -> None:
     call("mgic_field_nl_integrand", psi.handle, out.handle, vals)
 
 
-def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
+def poisson_solve(grid, prm: PoissonParameters, max_depth: int = -1,
                   prolong_type: int = 1, bottom_solver: int = 1,
                   max_NL_iterations: Optional[int] = None,
                   output_dir: Optional[str] = None) -> NLResult:
+    if isinstance(grid, (list, tuple)):
+        if len(grid) > 1:
+            return _poisson_solve_amr(list(grid), prm, max_depth, prolong_type, bottom_solver,
+                                      max_NL_iterations, output_dir)
+        grid = grid[0]
     periodic = bool(prm.is_periodic)
     if periodic != all(grid.periodic):
         raise ValueError("grid periodicity must match params is_periodic")
@@ -131,6 +145,80 @@ def poisson_solve(grid: Grid, prm: PoissonParameters, max_depth: int = -1,
     if output_dir is not None:  # :227-230
         def write():
             output_final_data([psi], bh, prm.max_level, [2],
+                              os.path.join(output_dir, "vcPoissonFinal.3d.hdf5"))
+    return finish_nl_loop(res, write)
+
+
+def _op_params(prm: PoissonParameters, prolong_type: int) -> OperatorParams:
+    avg = prm.coefficient_average_type if prm.coefficient_average_type >= 0 else 0
+    return OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                          bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
+                          coefficient_average_type=avg, prolong_type=prolong_type, relax_mode=1)
+
+
+def _poisson_solve_amr(grids: List[Grid], prm: PoissonParameters, max_depth: int,
+                       prolong_type: int, bottom_solver: int, max_NL_iterations: Optional[int],
+                       output_dir: Optional[str]) -> NLResult:
+    """poissonSolve over nlevels = len(grids) AMR levels (Main_PoissonSolver.cpp:51-250)."""
+    periodic = bool(prm.is_periodic)
+    if periodic != all(grids[0].periodic):
+        raise ValueError("grid periodicity must match params is_periodic")
+    nlev = len(grids)
+    psi = [LevelData(g) for g in grids]
+    dpsi = [LevelData(g) for g in grids]
+    a = [LevelData(g) for g in grids]
+    b = [LevelData(g) for g in grids]
+    rhs = [LevelData(g) for g in grids]
+    for l in range(nlev):  # set_initial_conditions / set_b_coef per level (:79-99, :157)
+        psi[l].set_val_all(1.0)
+        dpsi[l].set_zero()
+        b[l].set_val(1.0)
+    bh = prm.bh(constant_K=0.0)
+    op_params = _op_params(prm, prolong_type)
+    depth = prm.preCondSolverDepth if prm.preCondSolverDepth >= 0 else max_depth
+    sp = SolverParams(max_depth=depth, n_pre=prm.numMGsmooth, n_post=prm.numMGsmooth,
+                      n_bottom=prm.numMGsmooth, bottom_solver=bottom_solver,
+                      agglomerate_below=32 if grids[0].comm.size > 1 else 0)
+    res = NLResult(psi=psi, dpsi=dpsi)
+    n_nl = prm.max_NL_iterations if max_NL_iterations is None else max_NL_iterations
+    volume = prm.domainLength[0] * prm.domainLength[1] * prm.domainLength[2]
+    integrand = geom = None
+    refs = [2] * nlev
+    for it in range(n_nl):
+        if periodic:  # integrability condition for K over the hierarchy (:137-150)
+            if integrand is None:
+                integrand = [LevelData(g) for g in grids]
+                # computeSum only needs the hierarchy's geometry
+                geom = AMRSolver(list(zip(grids, a, b)), op_params, sp)
+            bh["constant_K"] = 0.0
+            for l in range(nlev):
+                set_nl_integrand(psi[l], integrand[l], bh)
+            integral = geom.computeSum(integrand)
+            bh["constant_K"] = -math.sqrt(abs(integral) / volume)
+            res.constant_K.append(bh["constant_K"])
+        for l in range(nlev):  # :154-160
+            set_nl_coefs(psi[l], a[l], rhs[l], bh)
+        amr = AMRSolver(list(zip(grids, a, b)), op_params, sp)  # :163-170
+        solver = BiCGStabSolver(MultilevelLinearOp(amr, prm.numMGIterations),
+                                tolerance=prm.tolerance, max_iterations=prm.max_iterations,
+                                norm_type=0)
+        if output_dir is not None:  # :180-181
+            output_solver_data(dpsi, rhs, psi, bh, it, refs,
+                               os.path.join(output_dir, f"vcPoissonOut.3d_{it}.hdf5"))
+        res.linear_iterations.append(solver.solve(dpsi, rhs))  # :184
+        for l in range(nlev):  # :189-205
+            if l > 0:
+                amr.cf_interp(l, dpsi[l], dpsi[l - 1])  # QuadCFInterp::coarseFineInterp
+            amr.level_op(l).update_psi(psi[l], dpsi[l])
+        nrm = amr.computeNorm(dpsi, 2)  # :208-209
+        res.dpsi_norms.append(nrm)
+        if nrm < prm.tolerance or nrm > 1e5:
+            res.converged = nrm < prm.tolerance
+            break
+    write = None
+    if output_dir is not None:  # :227-230
+        def write():
+            output_final_data(psi, bh, nlev - 1, refs,
                               os.path.join(output_dir, "vcPoissonFinal.3d.hdf5"))
     return finish_nl_loop(res, write)
 

@@ -309,3 +309,152 @@ class AMROracle:
             cv = self.phis[l - 1][1:-1, 1:-1, 1:-1]
             self.put_covered(l, cv, average_down(self.phis[l][1:-1, 1:-1, 1:-1]))
         return self.init_residual(self.phis, self.rhss)
+
+    # ------------------------------------------- MultilevelLinearOp + BiCGStab
+    # (csrc/amr.cpp AMRSolver::applyOp / precondition / solve restated; every
+    # vector is a list of full arrays, one per level, ghost layer included)
+    def weight(self, l):
+        return self.L[l].dx ** 3
+
+    def zeros_ml(self):
+        return [lv.full() for lv in self.L]
+
+    def zero_covered(self, xs):
+        for l in range(1, len(self.L)):
+            self.put_covered(l, xs[l - 1][1:-1, 1:-1, 1:-1],
+                             np.zeros(tuple(s // 2 for s in self.L[l].shape)))
+
+    def apply_op(self, xs, hom=True):
+        """lhs = AMROperator on every level (L(u) = -(0 - L(u)), exact), the
+        covered coarse cells zeroed"""
+        out = []
+        for l, lv in enumerate(self.L):
+            self.fill(l, xs[l], xs[l - 1] if l else None, hom)
+            out.append(lv.full(-lv.residual(xs[l], np.zeros(lv.shape))))
+        self.zero_covered(out)
+        return out
+
+    def residual_ml(self, phis, rhss, hom=False):
+        out = [lv.full(self.amr_residual(l, phis[l], phis[l - 1] if l else None,
+                                         rhss[l][1:-1, 1:-1, 1:-1], hom))
+               for l, lv in enumerate(self.L)]
+        self.zero_covered(out)
+        return out
+
+    def dot(self, xs, ys):
+        return sum(self.weight(l) * float(np.sum(x[1:-1, 1:-1, 1:-1] * y[1:-1, 1:-1, 1:-1]))
+                   for l, (x, y) in enumerate(zip(xs, ys)))
+
+    def norm(self, xs, ord=0):
+        if ord == 0:
+            return max(float(np.abs(x[1:-1, 1:-1, 1:-1]).max()) for x in xs)
+        if ord == 1:
+            return sum(self.weight(l) * float(np.abs(x[1:-1, 1:-1, 1:-1]).sum())
+                       for l, x in enumerate(xs))
+        return float(np.sqrt(sum(self.weight(l) * float(np.sum(x[1:-1, 1:-1, 1:-1] ** 2))
+                                 for l, x in enumerate(xs))))
+
+    def masked(self, xs):
+        out = [x.copy() for x in xs]
+        self.zero_covered(out)
+        return out
+
+    def precondition(self, rs, iters):
+        """e = 0, then `iters` AMR iterations on (e, r), homogeneous physical BCs"""
+        n = len(self.L)
+        es = self.zeros_ml()
+        for i in range(iters):
+            if i == 0:
+                self.res = [r[1:-1, 1:-1, 1:-1].copy() for r in rs]
+            else:
+                self.res = [self.amr_residual(l, es[l], es[l - 1] if l else None,
+                                              rs[l][1:-1, 1:-1, 1:-1], True) for l in range(n)]
+                for l in range(1, n):
+                    self.put_covered(l, self.res[l - 1],
+                                     np.zeros(tuple(s // 2 for s in self.L[l].shape)))
+            self.corr = [None] * n
+            self.cycle(n - 1)
+            for l in range(n):
+                es[l][1:-1, 1:-1, 1:-1] = es[l][1:-1, 1:-1, 1:-1] + self.corr[l][1:-1, 1:-1, 1:-1]
+            for l in range(n - 1, 0, -1):
+                self.put_covered(l, es[l - 1][1:-1, 1:-1, 1:-1],
+                                 average_down(es[l][1:-1, 1:-1, 1:-1]))
+        return es
+
+    def solve(self, phis, rhss, num_mg_iterations=1, imax=10, eps=1e-7, norm_type=0,
+              reps=1e-12, small=1e-30, num_restarts=5):
+        """BiCGStabSolver::solve over the multi-level operator (the control
+        flow of csrc/op.cpp BiCGStabSolver::solve); phis modified in place;
+        returns (iterations, final norm)"""
+        n = len(self.L)
+        it_mg = max(1, num_mg_iterations)
+
+        def ax(a, x, b, y):  # a*x + b*y per level on the valid cells
+            out = []
+            for xl, yl in zip(x, y):
+                z = np.zeros_like(xl)
+                z[1:-1, 1:-1, 1:-1] = a * xl[1:-1, 1:-1, 1:-1] + b * yl[1:-1, 1:-1, 1:-1]
+                out.append(z)
+            return out
+
+        def incr(x, y, s):
+            for xl, yl in zip(x, y):
+                xl[1:-1, 1:-1, 1:-1] = xl[1:-1, 1:-1, 1:-1] + s * yl[1:-1, 1:-1, 1:-1]
+
+        R = self.residual_ml(phis, rhss, False)
+        RT = [r.copy() for r in R]
+        E, P, V = self.zeros_ml(), self.zeros_ml(), self.zeros_ml()
+        rho1 = rho2 = alpha = beta = omega = 0.0
+        init_norm = self.norm(R, norm_type)
+        nrm = init_norm
+        it = restarts = 0
+        init = True
+        while it < imax and nrm > eps * init_norm and nrm > reps:
+            it += 1
+            rho2 = rho1
+            rho1 = self.dot(RT, R)
+            if rho1 == 0.0:
+                break
+            if init:
+                P = [r.copy() for r in R]
+                init = False
+            else:
+                beta = (rho1 / rho2) * (alpha / omega)
+                c = -beta * omega
+                for pl, vl, rl in zip(P, V, R):
+                    pl[1:-1, 1:-1, 1:-1] = ((pl[1:-1, 1:-1, 1:-1] * beta + c * vl[1:-1, 1:-1, 1:-1])
+                                            + rl[1:-1, 1:-1, 1:-1])
+            PT = self.precondition(P, it_mg)
+            V = self.apply_op(PT, True)
+            m = self.dot(RT, V)
+            if abs(m) > small * abs(rho1):
+                alpha = rho1 / m
+                S = ax(1.0, R, -alpha, V)
+                incr(E, PT, alpha)
+                nrm = self.norm(S, norm_type)
+                if nrm <= eps * init_norm or nrm <= reps:
+                    break
+                ST = self.precondition(S, it_mg)
+                T = self.apply_op(ST, True)
+                ts, tt = self.dot(T, S), self.dot(T, T)
+                if tt == 0.0:
+                    break
+                omega = ts / tt
+                R = ax(1.0, S, -omega, T)
+                incr(E, ST, omega)
+                nrm = self.norm(R, norm_type)
+                if omega == 0.0:
+                    break
+            else:
+                if restarts >= num_restarts:
+                    break
+                restarts += 1
+                incr(phis, E, 1.0)
+                R = self.residual_ml(phis, rhss, False)
+                RT = [r.copy() for r in R]
+                E = self.zeros_ml()
+                nrm = self.norm(R, norm_type)
+                init = True
+        incr(phis, E, 1.0)
+        R = self.residual_ml(phis, rhss, False)
+        return it, self.norm(R, norm_type)

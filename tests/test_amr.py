@@ -229,3 +229,133 @@ def test_amr_level_operators_match_oracle(comm):
     amr.AMRUpdateResidual(1, fr1, fu1, fu0)
     U1 = o.L[1].full(u1)
     assert np.array_equal(fr1.download(0), o.amr_residual(1, U1, o.L[0].full(u0), r1, True))
+
+
+# ------------------------------------------- MultilevelLinearOp + BiCGStab
+def _full_ml(o, arrs):
+    return [o.L[l].full(a) for l, a in enumerate(arrs)]
+
+
+def test_amr_oracle_multilevel_bicgstab_converges():
+    # the outer solve over the hierarchy (Main_PoissonSolver.cpp:169-184 with
+    # max_level > 0): BiCGStab with AMR V-cycles as the preconditioner
+    rng = np.random.default_rng(21)
+    lv = _data(rng, 3, bvar=False)
+    o = _oracle(lv)
+    phis = o.zeros_ml()
+    rhss = _full_ml(o, [x["rhs"] for x in lv])
+    r0 = o.norm(o.residual_ml([p.copy() for p in phis], rhss), 0)
+    it, nrm = o.solve(phis, rhss, num_mg_iterations=2, imax=20, eps=1e-10)
+    assert nrm <= 1e-10 * r0 * 10 and it <= 12, (it, nrm, r0)
+    # the preconditioner alone reduces the composite residual
+    r = o.residual_ml(o.zeros_ml(), rhss)
+    e = o.precondition(r, 2)
+    r1 = o.residual_ml(e, rhss)
+    assert o.norm(r1, 0) < 0.2 * o.norm(r, 0)
+
+
+def _ml_setup(comm, rng, nlev=3, boxes=BOXES):
+    lv = _data(rng, nlev, bvar=False, boxes=boxes)
+    amr, F = _gpu(comm, lv)
+    o = _oracle(lv)
+    return lv, amr, F, o
+
+
+def _new_fields(F):
+    import mg_ic_code_amd as mg
+    return [mg.LevelData(f["grid"]) for f in F]
+
+
+def _up(F, fields, arrs):
+    for f, d, a in zip(F, fields, arrs):
+        d.upload(0, a[1:-1, 1:-1, 1:-1])
+
+
+@pytest.mark.gpu
+def test_amr_multilevel_apply_op_and_precondition_bitwise(comm):
+    rng = np.random.default_rng(22)
+    lv, amr, F, o = _ml_setup(comm, rng)
+    xs = [o.L[l].full(rng.uniform(-1, 1, _shape(BOXES[l]))) for l in range(3)]
+    fx, fl = _new_fields(F), _new_fields(F)
+    _up(F, fx, xs)
+    amr.applyOp(fl, fx, True)
+    want = o.apply_op([x.copy() for x in xs], True)
+    for l in range(3):
+        assert np.array_equal(fl[l].download(0), want[l][1:-1, 1:-1, 1:-1]), l
+    # dot / norms: reductions in another order
+    assert amr.dotProduct(fl, fx) == pytest.approx(o.dot(want, xs), rel=1e-12)
+    for ord_ in (0, 1, 2):
+        assert amr.norm(fl, ord_) == pytest.approx(o.norm(want, ord_), rel=1e-12)
+        assert amr.computeNorm(fx, ord_) == pytest.approx(o.norm(o.masked(xs), ord_), rel=1e-12)
+    assert amr.computeSum(fx) == pytest.approx(
+        sum(o.weight(l) * float(m[1:-1, 1:-1, 1:-1].sum()) for l, m in enumerate(o.masked(xs))),
+        rel=1e-11)
+    # the preconditioner on a composite residual (covered cells zero)
+    r = o.residual_ml(o.zeros_ml(), _full_ml(o, [x["rhs"] for x in lv]))
+    fr, fe = _new_fields(F), _new_fields(F)
+    _up(F, fr, r)
+    amr.precondition(fe, fr, 2)
+    e = o.precondition(r, 2)
+    for l in range(3):
+        assert np.array_equal(fe[l].download(0), e[l][1:-1, 1:-1, 1:-1]), l
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("boxes", [BOXES, BOXES_EDGE], ids=["interior", "edge"])
+def test_amr_multilevel_bicgstab_solve_matches_oracle(comm, boxes):
+    import mg_ic_code_amd as mg
+    rng = np.random.default_rng(23)
+    lv, amr, F, o = _ml_setup(comm, rng, boxes=boxes)
+    solver = mg.BiCGStabSolver(mg.MultilevelLinearOp(amr, 2), tolerance=1e-10,
+                               max_iterations=20, norm_type=0)
+    it = solver.solve([f["phi"] for f in F], [f["rhs"] for f in F])
+    phis = o.zeros_ml()
+    it_o, nrm_o = o.solve(phis, _full_ml(o, [x["rhs"] for x in lv]), num_mg_iterations=2,
+                          imax=20, eps=1e-10)
+    assert it == it_o
+    assert solver.final_norm == pytest.approx(nrm_o, rel=1e-6, abs=1e-14)
+    for l in range(3):
+        got, want = _get(F[l]), phis[l][1:-1, 1:-1, 1:-1]
+        assert np.linalg.norm(got - want) <= 1e-10 * np.linalg.norm(want), l
+
+
+# ------------------------------------------- the NL loop over AMR levels
+# params.txt on a 32^3 base with two refined patches around the punctures
+NL_BOXES = [(0, 0, 0, 31, 31, 31), (16, 16, 16, 47, 47, 47), (48, 48, 48, 79, 79, 79)]
+
+
+def test_amr_oracle_nl_loop_converges():
+    import os
+    from mg_ic_code_amd.params import read_params_file
+    from tests.nl_ref import oracle_poisson_solve_amr
+    prm = read_params_file(os.path.join(os.path.dirname(__file__), "golden", "params.txt"))
+    psi, norms, iters = oracle_poisson_solve_amr(prm, NL_BOXES, 32, max_depth=3, n_nl=4)
+    assert norms[-1] < 1e-3 * norms[0], norms
+    assert all(b < a for a, b in zip(norms, norms[1:])), norms
+
+
+@pytest.mark.gpu
+def test_amr_nl_loop_matches_oracle(comm):
+    # Main_PoissonSolver.cpp:129-220 with max_level = 2 on a fixed hierarchy:
+    # per-level coefficients, multilevel BiCGStab, QuadCFInterp of dpsi,
+    # set_update_psi0, computeNorm -- GPU against the numpy/C oracle loop
+    import os
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.nl import poisson_solve
+    from mg_ic_code_amd.params import read_params_file
+    from tests.nl_ref import oracle_poisson_solve_amr
+    prm = read_params_file(os.path.join(os.path.dirname(__file__), "golden", "params.txt"))
+    dx = prm.domainLength[0] / 32
+    grids, dom = [], NL_BOXES[0]
+    for l, b in enumerate(NL_BOXES):
+        grids.append(mg.Grid(comm, dom, [b], dx, patches=l > 0))
+        dom = tuple(2 * v if i < 3 else 2 * v + 1 for i, v in enumerate(dom))
+        dx /= 2
+    res = poisson_solve(grids, prm, max_depth=3, max_NL_iterations=3)
+    psi_o, norms_o, iters_o = oracle_poisson_solve_amr(prm, NL_BOXES, 32, max_depth=3, n_nl=3)
+    assert res.linear_iterations[:2] == iters_o[:2]
+    np.testing.assert_allclose(res.dpsi_norms[:2], norms_o[:2], rtol=1e-6)
+    for l in range(3):
+        g = res.psi[l].download(0)
+        c = psi_o[l][1:-1, 1:-1, 1:-1]
+        assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c), l
