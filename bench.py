@@ -119,6 +119,7 @@ def main():
     boxes, grid, fa, frhs, fphi, fres = (case[k] for k in ("boxes", "grid", "fa", "frhs", "fphi",
                                                            "fres"))
     dom, dx, amg, op_params = case["dom"], case["dx"], case["amg"], case["op_params"]
+    fused_res = amg.fused_residual
     r0 = amg.init_residual(fphi, frhs, fres, norm_type=0)
     nt = args.norm_type
 
@@ -126,8 +127,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        amg.iteration(fphi, frhs, fres, norm_type=nt)
+    # AMRMultiGrid::solve's loop body K times (amg.iterations: the same phi
+    # and norms as K iteration() calls, bit for bit; iteration i's residual is
+    # formed in iteration i+1's first pre-smoothing launch where the level
+    # allows)
+    amg.iterations(fphi, frhs, fres, args.warmup, norm_type=nt)
     comm.synchronize()
 
     fine_cells = max((b[3] - b[0] + 1) * (b[4] - b[1] + 1) * (b[5] - b[2] + 1) for b in boxes)
@@ -136,11 +140,10 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    hist = []
-    for _ in range(args.steps):
-        # AMRMultiGrid::solve's iteration: the V-cycle, r = rhs - L(phi) and
-        # (norm_type >= 0) its norm for the stop test, on the host
-        hist.append(amg.iteration(fphi, frhs, fres, norm_type=nt))
+    # K AMRMultiGrid iterations: the V-cycle, r = rhs - L(phi) and
+    # (norm_type >= 0) its norm for the stop test, read on the host each
+    # iteration
+    hist = amg.iterations(fphi, frhs, fres, args.steps, norm_type=nt)
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -206,6 +209,7 @@ def main():
                 if world > 1 else "single GPU",
                 "transport": transport,
                 "agglomerate_below": case["agglomerate_below"],
+                "residual_fused": fused_res,
             },
             "roofline": {
                 "bound": "hbm",
@@ -248,12 +252,17 @@ def main():
 def make_comm(mg, torch, dist, rank, world, transport):
     """The N > 1 communicator: the peer-mapped transport ("ipc": ranks map
     each other's receive buffers, csrc/transport.hpp; works when ranks share
-    a device) or RCCL.  "auto" tries ipc and falls back to RCCL on every rank
-    when any rank could not set it up (a collective decision)."""
+    a device) or RCCL.  "auto" tries ipc, checks it on this job's devices
+    (mg_ic_code_amd/commcheck.py: one exchange and one reduction with known
+    results), and falls back to RCCL on every rank when any rank could not
+    set it up or saw a wrong value (a collective decision)."""
     if transport in ("ipc", "auto"):
         comm, ok, err = None, 1, ""
         try:
             comm = mg.Comm(rank, world, transport="ipc")
+            from mg_ic_code_amd.commcheck import check_transport
+            if not check_transport(comm, world):
+                ok, err = 0, "transport check: wrong halo or reduction values"
         except Exception as e:  # noqa: BLE001 -- decided collectively below
             ok, err = 0, str(e)
         t = torch.tensor([ok], dtype=torch.int32)
@@ -386,8 +395,10 @@ def pmc_traffic(args):
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(work, ctr)
+            # the two-sweep smoother launches (64 x 22 tiles), not the fused
+            # residual + sweeps launch (64 x 20 tiles)
             cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "--kernel-include-regex",
-                   "k_gsrb_tb2", "-d", d, "-o", "p", "--output-format", "csv", "--",
+                   "k_gsrb_tb2<double, 64, 22", "-d", d, "-o", "p", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
                    "--size", str(args.size), "--levels", str(args.levels), "--nsmooth",
                    str(args.nsmooth), "--no-cpu-baseline", "--no-traffic",
@@ -417,7 +428,8 @@ def pmc_traffic(args):
             "kernel": kname,
             "method": "this run: rocprofv3 --pmc FETCH_SIZE (x1024 x2, gfx950 half count) and "
                       "WRITE_SIZE (x1024) in separate child passes of the same workload, averaged "
-                      "over the fine-level k_gsrb_tb2 launches (plain, ACC and ZIN variants)"}
+                      "over the fine-level two-sweep launches (64 x 22 tiles: plain, ACC, and the ZIN "
+                      "launch of iterations without a fused residual)"}
 
 
 if __name__ == "__main__":

@@ -252,6 +252,18 @@ MGIC_API int mgic_mg_one_cycle(mgic_mg mg, mgic_field e, mgic_field r); /* Multi
  * norm_type >= 0, else not computed and nothing synchronised) */
 MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                                int norm_type, int homogeneous, double *norm);
+/* `count` iterations (AMRMultiGrid::solve's loop body) from the state
+ * mgic_mg_iteration / mgic_mg_init_residual leave; norms[i] (count values,
+ * may be NULL) = what the i-th mgic_mg_iteration call would return, bit for
+ * bit.  Iteration i+1's first pre-smoothing launch computes iteration i's
+ * residual (and its max norm) when the level allows it (one box per rank, no
+ * exchanged faces, two sweeps per launch): the same residual evaluations,
+ * one streaming pass fewer per iteration. */
+MGIC_API int mgic_mg_iterations(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
+                                int count, int norm_type, int homogeneous, double *norms);
+/* *fused = 1 when mgic_mg_iterations / the preconditioner fuse the residual
+ * into the first pre-smoothing launch on this hierarchy */
+MGIC_API int mgic_mg_fused_residual(mgic_mg mg, int *fused);
 MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
                                    mgic_field resid, int norm_type, int homogeneous,
                                    double *norm);

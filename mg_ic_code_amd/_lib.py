@@ -161,6 +161,8 @@ SIGNATURES = {
     "mgic_mg_level_field": [H, c_int, c_int, PH],
     "mgic_mg_one_cycle": [H, H, H],
     "mgic_mg_iteration": [H, H, H, H, c_int, c_int, PD],
+    "mgic_mg_iterations": [H, H, H, H, c_int, c_int, c_int, PD],
+    "mgic_mg_fused_residual": [H, PI],
     "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_precondition": [H, H, H, c_int],
     "mgic_mg_fmg": [H, H, H, H, c_int, c_int, c_int, PD],

@@ -594,6 +594,24 @@ class AMRMultiGrid:
              int(bool(homogeneous)), ctypes.byref(out))
         return out.value
 
+    def iterations(self, phi: LevelData, rhs: LevelData, resid: LevelData, count: int,
+                   norm_type: int = 0, homogeneous: bool = False) -> List[float]:
+        """`count` iteration() calls (same phi, resid and norms, bit for bit);
+        iteration i+1's first launch computes iteration i's residual where the
+        level allows (mgic_mg_iterations)."""
+        out = (ctypes.c_double * max(1, count))()
+        call("mgic_mg_iterations", self._h, phi.handle, rhs.handle, resid.handle, int(count),
+             int(norm_type), int(bool(homogeneous)), out)
+        return [out[i] for i in range(count)]
+
+    @property
+    def fused_residual(self) -> bool:
+        """iterations() / the preconditioner fuse the residual into the
+        first pre-smoothing launch on this hierarchy"""
+        v = ctypes.c_int()
+        call("mgic_mg_fused_residual", self._h, ctypes.byref(v))
+        return bool(v.value)
+
     def init_residual(self, phi: LevelData, rhs: LevelData, resid: LevelData, norm_type: int = 0,
                       homogeneous: bool = False) -> float:
         out = ctypes.c_double()

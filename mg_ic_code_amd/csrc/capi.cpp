@@ -964,6 +964,24 @@ MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_
     if (norm) *norm = v;
   });
 }
+MGIC_API int mgic_mg_iterations(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
+                                int count, int norm_type, int h, double *norms) {
+  return guard([&] {
+    NEED(mg);
+    NEED(phi);
+    NEED(rhs);
+    NEED(resid);
+    MGIC_CHECK(count >= 0, "count must be >= 0");
+    mg->amg.iterations(*phi->f, *rhs->f, *resid->f, count, norm_type, h != 0, norms);
+  });
+}
+MGIC_API int mgic_mg_fused_residual(mgic_mg mg, int *fused) {
+  return guard([&] {
+    NEED(mg);
+    NEED(fused);
+    *fused = mg->amg.mg.fusedResidualApplies() ? 1 : 0;
+  });
+}
 MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                                    int norm_type, int h, double *norm) {
   return guard([&] {

@@ -61,6 +61,16 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
                     hipStream_t st);
+// the first two-sweep launch of a V-cycle iteration with that iteration's
+// residual fused in: r_out = rhs - L(phi) under g_res's BC (VCCOMPUTERES3D)
+// and e_out = two sweeps from zero on r_out under g_hom's (homogeneous) BC,
+// one max |r| partial per block into partials[0, gsrb_sweep_tb2_res_blocks).
+// Bit-identical to residual_norm + gsrb_sweep_tb2(zero_in).  Boxes with only
+// domain faces, the two-sweep kernel's other conditions.
+long gsrb_sweep_tb2_res_blocks(const BoxArgs &g);
+void gsrb_sweep_tb2_res(double *e_out, double *r_out, const double *phi, const double *rhs,
+                        const double *a, const BoxArgs &g_hom, const BoxArgs &g_res,
+                        const StencilCoefs &s, double *partials, hipStream_t st);
 // the same two-sweep launch on fp32 fields (no phi += e)
 void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
                       const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st);

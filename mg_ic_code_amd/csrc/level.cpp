@@ -18,8 +18,8 @@ Comm::Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl)
     MGIC_CHECK(id != nullptr, "RCCL unique id required for size > 1");
     MGIC_NCCL(ncclCommInitRank(&nccl_, size, *id, rank));
   }
-  MGIC_HIP(hipMalloc(&d_result_, 2 * sizeof(double)));
-  MGIC_HIP(hipHostMalloc(&h_result_, 2 * sizeof(double), hipHostMallocDefault));
+  MGIC_HIP(hipMalloc(&d_result_, kResultSlots * sizeof(double)));
+  MGIC_HIP(hipHostMalloc(&h_result_, kResultSlots * sizeof(double), hipHostMallocDefault));
 }
 
 // the peer-mapped transport: signal page + receive arena per rank, mapped by
@@ -38,8 +38,8 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
                                                "(32-bit buffer offsets)");
   MGIC_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   own_stream_ = true;
-  MGIC_HIP(hipMalloc(&d_result_, 2 * sizeof(double)));
-  MGIC_HIP(hipHostMalloc(&h_result_, 2 * sizeof(double), hipHostMallocDefault));
+  MGIC_HIP(hipMalloc(&d_result_, kResultSlots * sizeof(double)));
+  MGIC_HIP(hipHostMalloc(&h_result_, kResultSlots * sizeof(double), hipHostMallocDefault));
   MGIC_HIP(hipHostMalloc(&h_err_, sizeof(unsigned long long), hipHostMallocDefault));
   *h_err_ = 0;
   // counters are polled across processes / devices: uncached memory

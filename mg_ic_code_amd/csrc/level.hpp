@@ -65,6 +65,11 @@ class Comm {
   void allreduce(double *d_val, int op);
   // scratch for reductions (device partials + result, pinned host result)
   double *d_partials(int n);
+  // reduction results (device) and their host copies (pinned): slots 0-1 for
+  // the operators' reductions, slot 2 for the max norm a fused-residual
+  // launch leaves behind while the rest of its V-cycle runs
+  static constexpr int kResultSlots = 4;
+  static constexpr int kFusedNormSlot = 2;
   double *d_result() const { return d_result_; }
   double *h_result() const { return h_result_; }
 

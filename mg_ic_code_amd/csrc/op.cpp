@@ -506,6 +506,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     }
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
+  if (flags & kSrcInScratch) std::swap(src, dst);  // (the fused-residual launch's output)
   // two sweeps per launch (temporal blocking): on boxes with only domain
   // faces, or with exchanged faces in deep-halo mode (the kernel's rings run
   // onto the 4-deep shell, exchanged before every pair; rhs / coefficient
@@ -658,6 +659,53 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     dpsi.exchange(st);
   }
   return restrict_last;
+}
+
+bool VariableCoeffPoissonOperator::fusedResidualApplies(int n) {
+  static const int on = [] {  // MGIC_FUSED_RESIDUAL=0: separate residual launches (A/B)
+    const char *e = getenv("MGIC_FUSED_RESIDUAL");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || n < 2 || prm.relax_mode != 1 || cf || grid->has_memory_faces() ||
+      !fusedSmootherApplies() || sweeps_per_launch() != 2)
+    return false;
+  const StencilCoefs s = coefs();
+  for (int b = 0; b < grid->nlocal(); ++b)
+    if (!kern::gsrb_sweep_tb2_applies(args_hom_[b], s, prm.fused_smoother)) return false;
+  return true;
+}
+
+void VariableCoeffPoissonOperator::residualRelaxFromZero(LevelData &e, LevelData &r,
+                                                         LevelData &phi, const LevelData &rhs,
+                                                         int n, bool homogeneous, int normType,
+                                                         int slot, int flags) {
+  MGIC_CHECK(fusedResidualApplies(n), "the fused residual launch does not apply to this level");
+  check_same_layout(*grid, e, "correction");
+  check_same_layout(*grid, r, "residual");
+  check_same_layout(*grid, phi, "phi");
+  check_same_layout(*grid, rhs, "rhs");
+  resetLambda();  // .cpp:283
+  const hipStream_t st = stream();
+  const StencilCoefs s = coefs();
+  if (!sweep_tmp_) sweep_tmp_ = create();
+  Comm &c = *grid->comm;
+  long total = 0;
+  for (int b = 0; b < grid->nlocal(); ++b) total += kern::gsrb_sweep_tb2_res_blocks(args_hom_[b]);
+  double *parts = c.d_partials((int)std::max(1L, total));
+  long off = 0;
+  for (int b = 0; b < grid->nlocal(); ++b) {  // r = rhs - L(phi); two sweeps from zero on r
+    kern::gsrb_sweep_tb2_res(sweep_tmp_->p[b], r.p[b], phi.p[b], rhs.p[b], m_aCoef->p[b],
+                             args_hom_[b], args(b, homogeneous), s, parts + off, st);
+    off += kern::gsrb_sweep_tb2_res_blocks(args_hom_[b]);
+  }
+  if (normType == 0) finish_reduce(3, parts, (int)total, slot);
+  if (n > 2) {
+    fusedRelax(e, r, n - 2, false, nullptr, flags | kSrcInScratch);
+  } else {
+    for (int b = 0; b < grid->nlocal(); ++b)
+      kern::blas(0, e.p[b], sweep_tmp_->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
+    if (flags & kHaloOut) e.exchange(st);
+  }
 }
 
 void VariableCoeffPoissonOperator::relaxAccumulate(LevelData &e, const LevelData &r, int n,
@@ -1133,8 +1181,15 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
   // restricts in its last sweep
   Level &N = levels_[d + 1];
   LevelData &rc = N.agg ? *N.r_stage : *N.r;
-  if (!op.relaxRestrict(e, r, prm.n_pre, e_zero, rf | kHaloOut, rc))
+  if (d == 0 && fres_) {  // r = rhs - L(phi) fused into the first pre-smoothing launch
+    const FusedRes f = *fres_;
+    fres_ = nullptr;
+    op.residualRelaxFromZero(e, r, *f.phi, *f.rhs, prm.n_pre, f.hom, f.normType, f.slot,
+                             rf | kHaloOut);
     op.restrictResidual(rc, e, r, false);
+  } else if (!op.relaxRestrict(e, r, prm.n_pre, e_zero, rf | kHaloOut, rc)) {
+    op.restrictResidual(rc, e, r, false);
+  }
   if (N.agg) N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
   // coarse correction e_c = 0 (folded into its first sweep when possible);
   // its last relax exchanges e_c's ghosts for the linear prolongation
@@ -1151,6 +1206,25 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
     op.relaxAccumulate(e, r, prm.n_post, *phi_acc, rf);
   else
     op.relaxFlags(e, r, prm.n_post, rf | out);
+}
+
+bool MultiGrid::fusedResidualApplies() {
+  return depths() >= 2 && op(0).fusedResidualApplies(prm.n_pre);
+}
+
+void MultiGrid::oneCycleResidualFromZero(LevelData &e, LevelData &r, LevelData &phi,
+                                         const LevelData &rhs, bool homogeneous, int normType,
+                                         int slot, LevelData *phi_acc) {
+  MGIC_CHECK(fusedResidualApplies(), "the fused residual does not apply to this hierarchy");
+  const FusedRes f{&phi, &rhs, homogeneous, normType, slot};
+  fres_ = &f;
+  try {
+    cycle(0, e, r, true, phi_acc);
+  } catch (...) {
+    fres_ = nullptr;
+    throw;
+  }
+  fres_ = nullptr;
 }
 
 void MultiGrid::fmg(LevelData &e0, LevelData &r0, LevelData &phi, int ncycles) {
@@ -1200,6 +1274,41 @@ double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &
   return op0.residualNorm(resid, phi, rhs, homogeneous, normType);
 }
 
+void AMRMultiGrid::iterations(LevelData &phi, const LevelData &rhs, LevelData &resid, int count,
+                              int normType, bool homogeneous, double *norms) {
+  if (count <= 0) return;
+  if (!mg.fusedResidualApplies()) {
+    for (int i = 0; i < count; ++i) {
+      const double v = iteration(phi, rhs, resid, normType, homogeneous);
+      if (norms) norms[i] = v;
+    }
+    return;
+  }
+  VariableCoeffPoissonOperator &op0 = mg.op(0);
+  Comm &c = *op0.grid->comm;
+  const hipStream_t st = op0.stream();
+  mg.oneCycleFromZeroInto(*corr_, resid, phi);  // iteration 1 on the current residual
+  for (int i = 1; i < count; ++i) {
+    // iteration i+1, whose first launch forms iteration i's residual
+    const int slot = Comm::kFusedNormSlot;  // (the bottom solver's reductions use 0-1)
+    mg.oneCycleResidualFromZero(*corr_, resid, phi, rhs, homogeneous, normType, slot, &phi);
+    double v = -1.0;
+    if (normType == 0) {  // the fused launch's max norm
+      MGIC_HIP(hipMemcpyAsync(c.h_result() + slot, c.d_result() + slot, sizeof(double),
+                              hipMemcpyDeviceToHost, st));
+      c.ipc_err_async(st);
+      MGIC_HIP(hipStreamSynchronize(st));
+      c.ipc_err_raise();
+      v = c.h_result()[slot];
+    } else if (normType > 0) {
+      v = op0.norm(resid, normType);  // resid is still iteration i's residual
+    }
+    if (norms) norms[i - 1] = v;
+  }
+  const double v = op0.residualNorm(resid, phi, rhs, homogeneous, normType);
+  if (norms) norms[count - 1] = v;
+}
+
 double AMRMultiGrid::fmg(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
                          bool homogeneous, int ncycles) {
   VariableCoeffPoissonOperator &op0 = mg.op(0);
@@ -1215,7 +1324,12 @@ void AMRMultiGrid::precondition(LevelData &e, const LevelData &r, int iters) {
   // first cycle runs on r (its ghosts are the only cells it writes); the
   // residual after the last cycle is not needed
   LevelData &r0 = const_cast<LevelData &>(r);
+  const bool fused = iters > 1 && mg.fusedResidualApplies();
   for (int i = 0; i < iters; ++i) {
+    if (i > 0 && fused) {  // r - L(e) fused into the cycle's first launch
+      mg.oneCycleResidualFromZero(*corr_, *pre_resid_, e, r, true, -1, Comm::kFusedNormSlot, &e);
+      continue;
+    }
     if (i > 0) op0.residual(*pre_resid_, e, r, true);
     mg.oneCycleFromZeroInto(*corr_, i == 0 ? r0 : *pre_resid_, e);
   }

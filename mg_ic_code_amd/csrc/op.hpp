@@ -50,7 +50,9 @@ struct OpParams {
 
 // relax flags (MultiGrid::cycle): the caller exchanged rhs's ghost layer
 // already / wants the result's face ghosts exchanged on return
-enum RelaxFlags { kRhsHaloReady = 1, kHaloOut = 2 };
+enum RelaxFlags { kRhsHaloReady = 1, kHaloOut = 2, kSrcInScratch = 4 };
+// (kSrcInScratch: fusedRelax's input sits in the operator's sweep scratch
+// buffer, not in dpsi -- the fused-residual launch leaves it there)
 
 class VariableCoeffPoissonOperator {
  public:
@@ -177,6 +179,16 @@ class VariableCoeffPoissonOperator {
   void relaxFromZero(LevelData &e, const LevelData &r, int n, int flags = 0);
   // relax(e, r, n) with RelaxFlags
   void relaxFlags(LevelData &e, const LevelData &r, int n, int flags);
+  // r = rhs - L(phi) (residualI with `homogeneous`) and then e = 0;
+  // relax(e, r, n), the residual fused into the first two-sweep launch
+  // (gsrb_sweep_tb2_res; bit-identical to residualI + relaxFromZero).  The
+  // max norm of r (normType 0) is reduced into the communicator's result
+  // slot `slot` on the stream (read it after a synchronisation); other
+  // norm types are taken by a separate pass.  Call only when
+  // fusedResidualApplies(n).
+  void residualRelaxFromZero(LevelData &e, LevelData &r, LevelData &phi, const LevelData &rhs,
+                             int n, bool homogeneous, int normType, int slot, int flags = 0);
+  bool fusedResidualApplies(int n);
   // (e = 0 when zero_in;) relax(e, r, n); and, when the fused sweep can
   // fold it into its last pass, restrictResidual(resC, e, r) -- returns
   // whether the restriction was done (else the caller restricts)
@@ -265,6 +277,14 @@ class MultiGrid {
   void oneCycleFromZeroInto(LevelData &e, const LevelData &r, LevelData &phi) {
     cycle(0, e, const_cast<LevelData &>(r), true, &phi);
   }
+  // the V-cycle of an AMRMultiGrid iteration that starts from phi's
+  // residual: r = rhs - L(phi) (norm into result slot `slot`, see
+  // residualRelaxFromZero), e = 0; oneCycle(e, r); phi += e -- the residual
+  // fused into the first pre-smoothing launch (fusedResidualApplies) or
+  // computed first.  With phi_acc == nullptr, phi is only read.
+  void oneCycleResidualFromZero(LevelData &e, LevelData &r, LevelData &phi, const LevelData &rhs,
+                                bool homogeneous, int normType, int slot, LevelData *phi_acc);
+  bool fusedResidualApplies();
   // full multigrid from the residual r at depth 0: r_{d+1} = R(r_d) at every
   // depth, the bottom solve from zero, then per finer depth e_d = P e_{d+1}
   // and `ncycles` V-cycles on it; phi += e_0 (folded into the last sweep)
@@ -290,6 +310,15 @@ class MultiGrid {
   void cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
              bool halo_out = false);
   std::vector<Level> levels_;
+  // set by oneCycleResidualFromZero for the depth-0 pre-smoothing of that
+  // cycle: the residual's inputs
+  struct FusedRes {
+    LevelData *phi;
+    const LevelData *rhs;
+    bool hom;
+    int normType, slot;
+  };
+  const FusedRes *fres_ = nullptr;
 };
 
 // [Chombo] AMRMultiGrid on a single AMR level: iterations of
@@ -315,6 +344,14 @@ class AMRMultiGrid {
   // else -1 without synchronising
   double iteration(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
                    bool homogeneous);
+  // `count` iterations from the state iteration() / initResidual() leave
+  // (resid = rhs - L(phi)); norms[i] = what the i-th iteration() call would
+  // return, bit for bit.  Iteration i+1's V-cycle computes iteration i's
+  // residual in its first launch when the fused residual applies, so the
+  // count includes the same residual evaluations as `count` iteration()
+  // calls (the last one separately).
+  void iterations(LevelData &phi, const LevelData &rhs, LevelData &resid, int count,
+                  int normType, bool homogeneous, double *norms);
   double initResidual(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
                       bool homogeneous);
   // an FMG cycle on the current residual (resid as left by initResidual /

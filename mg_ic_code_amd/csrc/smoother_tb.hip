@@ -77,7 +77,7 @@ using IC = std::integral_constant<int, N>;
 #define TB2_NO_READ2 0
 #endif
 // TB2_PF2 1 = loads two steps ahead (plain / ZIN variants); TB2_STORE_CPOL =
-// cache-policy bits of the u_out stores (16 = sc1: drop the line from L2)
+// cache-policy bits of the u_out stores (2 = nt, 16 = sc1: drop the line from L2)
 #ifndef TB2_PF2
 #define TB2_PF2 1
 #endif
@@ -108,7 +108,7 @@ using IC = std::integral_constant<int, N>;
 //     red  (m):  x-1, x+1 = B[m-1], B[m];  y+-1, z+-1 = B[m-1+s] of that row / plane
 //     black(m):  x-1, x+1 = R[m], R[m+1];  y+-1, z+-1 = R[m+s]
 // (a neighbouring row or plane has the opposite shift).
-template <int TX, int TY, int NT>
+template <int TX, int TY, int NT, int NSL = 8>
 struct TB2 {
   static_assert(TX % 2 == 0, "TX must be even");
   static constexpr int PW = TX / 2 + 5;            // pairs per LDS row: X = x0-6+s .. x0+TX+2+s
@@ -116,7 +116,10 @@ struct TB2 {
   static constexpr int CP = PW * LH;               // pairs per plane
   static constexpr int SS = CP + 2 * PW + 2;       // slot stride: + a scratch row
   static constexpr int PAD = CP + PW + 1;          // write target of elements never updated
-  static constexpr int NS = 8;                     // ring slots (planes p+1 .. p-5 live)
+  // ring slots: 8 (planes p+1 .. p-5 live); the fused-residual launch (RES)
+  // 9: the correction's planes p .. p-5 in slots 0-5 (plane mod 6) and the
+  // input phi's planes p .. p+2 in slots 6-8 (plane mod 3)
+  static constexpr int NS = NSL;
   static constexpr int UW = PW - 1;                // update pairs per row: m = 1 .. PW-1
   static constexpr int NRP = UW * (TY + 6);        // update pairs: rows y0-3 .. y0+TY+2
   static constexpr int NL = (CP + NT - 1) / NT;
@@ -167,16 +170,28 @@ template <> struct TB2Vec<float> { using type = float2; };
 // One tile (x0, y0) of the box, planes [z0, z1).  FAST: alpha == 1, beta ==
 // -1, bval == 1 (exact specialisation, see above); EDGE: the tile's rings
 // reach an x / y domain face (BC code compiled in).
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE>
+//
+// RES (with ZIN): the launch that starts an AMRMultiGrid iteration's
+// V-cycle also computes that iteration's residual.  ui is phi and rhs the
+// level's right-hand side; the residual r = rhs - L(phi) (VCCOMPUTERES3D,
+// .ChF:283-339, with the BC of gr) is formed from a 3-plane phi ring on
+// ring 3 of every plane one step before its sweep-1 red pass needs it as
+// the correction equation's right-hand side, carried in the coefficient
+// registers in place of the loaded rhs, and its tile cells are stored to ro
+// (the restriction and the later sweeps read it) while their max |r| goes
+// to *nmax.  Bit-identical to k_residual_z2 followed by the ZIN launch.
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE, bool RES>
 __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                                          T *__restrict__ uo, double *__restrict__ acc,
                                          const T *__restrict__ ui,
                                          const T *__restrict__ rhs,
                                          const T *__restrict__ a, const BoxArgs &g,
                                          const StencilCoefs &s64, const TB2Ghosts<T> &gg, int x0,
-                                         int y0, int z0, int z1, int ef) {
+                                         int y0, int z0, int z1, int ef, T *__restrict__ ro,
+                                         const TB2Ghosts<T> &gr, double &nmax) {
   static_assert(!ACC || std::is_same<T, double>::value, "phi += e is folded into fp64 sweeps only");
-  using F = TB2<TX, TY, NT>;
+  static_assert(!RES || (ZIN && !ACC), "the fused residual starts a zero-input launch");
+  using F = TB2<TX, TY, NT, RES ? 9 : 8>;
   using V = typename TB2Vec<T>::type;
   const TB2Coefs<T> s(s64);
   constexpr int PW = F::PW, CP = F::CP, SS = F::SS, UW = F::UW, NRP = F::NRP, NL = F::NL,
@@ -221,6 +236,16 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   };
   auto boff = [&](int x, int y) {  // byte offset of cell (x, y) from the corner
     return (unsigned)(sizeof(T) * (16 + x + (long)(y + 4) * sy));
+  };
+  // ring slot of plane q: es for the correction, ps for the loaded input
+  // (one ring of 8 slots; RES: slots 0-5 and 6-8, q >= pstart - 1 >= -4)
+  auto es = [](int q) -> int {
+    if constexpr (RES) return (q + 12) % 6;
+    else return q & 7;
+  };
+  auto ps = [](int q) -> int {
+    if constexpr (RES) return 6 + (q + 12) % 3;
+    else return q & 7;
   };
 
   // ---- loads of u (slot c = LDS pair index), per plane parity t ----------
@@ -335,7 +360,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     const char *pl = plane(ui, p == zgl ? 0 : p == zgh ? nz - 1 : p);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      if (ZIN || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
+      if ((ZIN && !RES) || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
         pu0[b][i] = 0.0;
         pu1[b][i] = 0.0;
       } else if (NL * NT <= CP || tid + i * NT < CP) {  // (whole waves past the plane skip)
@@ -348,15 +373,17 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     }
   };
   // a z ghost plane of a domain face, fetched as the plane it images ->
-  // ParseBC's images.  (x / y ghosts are never stored: see pass.)
+  // ParseBC's images (RES: the loaded phi's, with the residual's BC).  (x / y
+  // ghosts are never stored: see pass.)
   auto image = [&](int p, auto bc) {
     constexpr int b = decltype(bc)::value;
+    const TB2Ghosts<T> &G = RES ? gr : gg;
     if (p == zgl || p == zgh) {
       const int zf = p == -1 ? 4 : 5;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
-        pu0[b][i] = ghost(gg, zf, pu0[b][i]);
-        pu1[b][i] = ghost(gg, zf, pu1[b][i]);
+        pu0[b][i] = ghost(G, zf, pu0[b][i]);
+        pu1[b][i] = ghost(G, zf, pu1[b][i]);
       }
     }
   };
@@ -427,7 +454,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // +0 either way.  Sweep-1 black starts from its own u = 0 (the constant
   // lets x - 2*0 fold to x, exact).  Both skip the LDS reads they no longer
   // need.
-  auto pass = [&](auto zc, bool red, int W, int sl, int t, int k, const T (&cr)[NP],
+  auto pass = [&](auto zc, bool red, int W, int t, int k, const T (&cr)[NP],
                   const T (&ca)[NP], const T (&cl)[NP]) {
     constexpr int ZC = decltype(zc)::value;
     if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
@@ -436,10 +463,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     if (NP == 1 && W < 3 && wv < 3 - W) return;  // (one pair per lane only)
     if ((TB2_PROBE_SKIP & 8) && red) return;
     if ((TB2_PROBE_SKIP & 16) && !red) return;
-    T *X = (red ? R : B) + sl * SS;
-    T *N = (red ? B : R) + sl * SS;
-    T *Nm = (red ? B : R) + ((sl + 7) & 7) * SS;
-    T *Np = (red ? B : R) + ((sl + 1) & 7) * SS;
+    T *X = (red ? R : B) + es(k) * SS;
+    T *N = (red ? B : R) + es(k) * SS;
+    T *Nm = (red ? B : R) + es(k - 1) * SS;
+    T *Np = (red ? B : R) + es(k + 1) * SS;
     if constexpr (ZC == 1) {
       T v[NP];
 #pragma unroll
@@ -508,7 +535,8 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // an out-of-range offset, so every step issues exactly NP * 2 stores with
   // no branch around them and the next step waits vmcnt(2) for its loads
   // instead of vmcnt(0), which would also wait for these stores.
-  auto store = [&](int sl, int t, int k) {
+  auto store = [&](int t, int k) {
+    const int sl = es(k);
     if (TB2_PROBE_SKIP & 4) return;
     const bool kin = k >= z0 && k < z1;  // uniform
     char *dst = ACC ? reinterpret_cast<char *>(acc + corner + (long)clampi(k, z0, z1 - 1) * sz)
@@ -531,12 +559,93 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       const unsigned o4 = st == 3 ? off : kDrop;
       const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
       const T e = st == 1 ? w.x : w.y;
-      sweep::bstore(rs, w, o4);
-      sweep::bstore(rs, e, o2);
+      sweep::bstore<TB2_STORE_CPOL>(rs, w, o4);
+      sweep::bstore<TB2_STORE_CPOL>(rs, e, o2);
     }
   };
-  // One pipeline step at plane p (t: its parity relative to pstart; slot
-  // sl = p & 7), two barriers:
+  // RES: r = rhs - L(phi) on plane k, both elements of every pair of ring 3
+  // (the pairs sweep-1 red updates), from the phi ring; the loaded rhs of
+  // coefficient set b is replaced by r, which is what the sweeps of plane k
+  // solve against.  The expressions are k_residual_z2's (.ChF:312-336):
+  //   res = rhs - (alpha a) phi; ldpsi = ((L7 dxinv) beta) b; r = res + ldpsi
+  // with x / y domain-face neighbours as gr's ghosts of the cell (ParseBC of
+  // the residual's BC) and z ghost planes imaged in the ring.  The tile's
+  // cells of planes [z0, z1) are stored to ro and enter nmax.
+  auto residual = [&](int t, int k, auto bc) {
+    constexpr int b = decltype(bc)::value;
+    if constexpr (RES) {
+      if ((unsigned)(k - kl[3]) > kw[3]) return;  // uniform: outside sweep-1 red's planes
+      const T *Rc = R + ps(k) * SS, *Bc = B + ps(k) * SS;
+      const T *Rm = R + ps(k - 1) * SS, *Bm = B + ps(k - 1) * SS;
+      const T *Rq = R + ps(k + 1) * SS, *Bq = B + ps(k + 1) * SS;
+      auto res = [&](T c, T xm, T xp, T ym, T yp, T zm, T zp, T rv, T aa) -> T {
+        const T r0 = rv - s.alpha * aa * c;  // .ChF:314-316
+        const T tx = (xp + xm) - (T)2 * c;
+        const T ty = (yp + ym) - (T)2 * c;
+        const T tz = (zp + zm) - (T)2 * c;
+        T ld = (tx + ty) + tz;                   // .ChF:320-329
+        ld = ld * s.dxinv * s.beta * s.bval;     // .ChF:331
+        return r0 + ld;                          // .ChF:333
+      };
+      const bool kin = k >= z0 && k < z1;  // uniform
+      char *dst = reinterpret_cast<char *>(ro + corner + (long)clampi(k, z0, z1 - 1) * sz);
+      const __amdgpu_buffer_rsrc_t rs = sweep::store_rsrc(dst);
+      constexpr unsigned kDrop = sweep::kDrop;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int c = ci[i], o = yzo[t][i];
+        // red element: black neighbours at pair m-1, m (x) and m-1+s (y, z)
+        const T u0 = Rc[c];
+        T xm0 = Bc[c - 1], xp0 = Bc[c], ym0 = Bc[c + o - PW], yp0 = Bc[c + o + PW];
+        const T zm0 = Bm[c + o], zp0 = Bq[c + o];
+        // black element: red neighbours at pair m, m+1 (x) and m+s (y, z)
+        const T u1 = Bc[c];
+        T xm1 = Rc[c], xp1 = Rc[c + 1], ym1 = Rc[c + o + 1 - PW], yp1 = Rc[c + o + 1 + PW];
+        const T zm1 = Rm[c + o + 1], zp1 = Rq[c + o + 1];
+        if (EDGE) {
+          const int f0 = rinf[t][i] & 15, f1 = (rinf[t][i] >> 4) & 15;
+          if (ef & 1) {
+            xm0 = (f0 & 1) ? ghost(gr, 0, u0) : xm0;
+            xm1 = (f1 & 1) ? ghost(gr, 0, u1) : xm1;
+          }
+          if (ef & 2) {
+            xp0 = (f0 & 2) ? ghost(gr, 1, u0) : xp0;
+            xp1 = (f1 & 2) ? ghost(gr, 1, u1) : xp1;
+          }
+          if (ef & 4) {
+            ym0 = (f0 & 4) ? ghost(gr, 2, u0) : ym0;
+            ym1 = (f1 & 4) ? ghost(gr, 2, u1) : ym1;
+          }
+          if (ef & 8) {
+            yp0 = (f0 & 8) ? ghost(gr, 3, u0) : yp0;
+            yp1 = (f1 & 8) ? ghost(gr, 3, u1) : yp1;
+          }
+        }
+        const T r0 = res(u0, xm0, xp0, ym0, yp0, zm0, zp0, nr0[b][i], na0[b][i]);
+        const T r1 = res(u1, xm1, xp1, ym1, yp1, zm1, zp1, nr1[b][i], na1[b][i]);
+        nr0[b][i] = r0;
+        nr1[b][i] = r1;
+        // the tile's cells: stored (static store count, as in store) and
+        // into the max norm
+        const int st = kin ? (rinf[t][i] >> 8) & 3 : 0;
+        const unsigned off = roff[t][i];
+        V w;
+        w.x = r0;
+        w.y = r1;
+        const unsigned o4 = st == 3 ? off : kDrop;
+        const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
+        sweep::bstore<TB2_STORE_CPOL>(rs, w, o4);
+        sweep::bstore<TB2_STORE_CPOL>(rs, st == 1 ? r0 : r1, o2);
+        // (max as k_residual_z2 / red_op<3> take it: a > b ? a : b)
+        const double m0 = (st & 1) ? fabs((double)r0) : 0.0;
+        const double m1 = (st & 2) ? fabs((double)r1) : 0.0;
+        nmax = nmax > m0 ? nmax : m0;
+        nmax = nmax > m1 ? nmax : m1;
+      }
+    }
+  };
+  // One pipeline step at plane p (t: its parity relative to pstart; ring
+  // slots es(q) / ps(q)), two barriers:
   //   phase A: sweep-1 red of plane p (ring 3), sweep-2 red of plane p-3 (ring 1)
   //   phase B: sweep-1 black of plane p-1 (ring 2), sweep-2 black of plane
   //            p-4 (the tile) + its store
@@ -544,6 +653,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // cells only, phase B red ones.  Live ring planes p+1 .. p-5; plane p+1 is
   // written over plane p-7.
   auto step = [&](auto tc, int p) {
+    static_assert(!RES || PF == 2, "the fused residual keeps loads two steps ahead");
     // J: position in the 4-step unrolled loop; T / U: parity of p / of p +- 1;
     // coefficient sets live in slot J (made this step) .. slot J3 (made
     // three steps ago, last use), so no register moves between steps
@@ -552,7 +662,6 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     constexpr int FB = PF == 2 ? (J & 1) : 0;  // in-flight register set consumed / refilled
     using ICF = IC<FB>;
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
-    const int sl = p & 7;
     TB2_STAMP(0, p);
     // coefficient sets: black of plane p-1 from the raw black element, red
     // of plane p from its pair fetched last step (alpha * a, .ChF:107)
@@ -567,8 +676,13 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       rb[i] = nr1[FB][i];
       ab[i] = na1[FB][i];
     }
-    image(p + 1, ICF{});
-    put((sl + 1) & 7, ICF{});
+    if constexpr (RES) {  // phi of plane p+2 into the phi ring
+      image(p + 2, ICF{});
+      put(ps(p + 2), ICF{});
+    } else {
+      image(p + 1, ICF{});
+      put(ps(p + 1), ICF{});
+    }
     if (PF == 2) fetch_c(PT, p + 2, ICF{});
     else fetch_c(PU, p + 1, ICF{});
     if constexpr (ACC) {
@@ -582,34 +696,67 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         an1[i] = v.y;
       }
     }
-    if (PF == 2) fetch_u(PU, p + 3, ICF{});
+    if constexpr (RES) fetch_u(PT, p + 4, ICF{});
+    else if (PF == 2) fetch_u(PU, p + 3, ICF{});
     else fetch_u(PT, p + 2, ICF{});
     TB2_STAMP(1, p);
     __syncthreads();
     TB2_STAMP(2, p);
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, true, 3, sl, PT, p, Rr[J0], Ra[J0], Rl[J0]);
-    pass(IC<0>{}, true, 1, (sl + 5) & 7, PU, p - 3, Rr[J3], Ra[J3], Rl[J3]);
+    // RES: r of plane p+1 (phi planes p .. p+2 are in the phi ring) into the
+    // coefficient set that step p+1 turns into plane p+1's sweep-1 inputs
+    if constexpr (RES) {
+      residual(PU, p + 1, IC<FB ^ 1>{});
+      // a z ghost plane of the (zero) correction: its red elements image the
+      // black cells of the face plane, which are 0 until sweep-1 black reads
+      // them (the plain ZIN launch puts those images with the zero input;
+      // here the correction's slots are never put).  Its black elements are
+      // written by the face plane's sweep-1 red pass before any read.  (The
+      // slot's previous plane was last read in step p-1's black phase.)
+      if (p == zgl || p == zgh) {
+        const T g0 = ghost(gg, p == zgl ? 4 : 5, (T)0);
+        T *Rs = R + es(p) * SS;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          if (NL * NT > CP && tid + i * NT >= CP) continue;
+          Rs[tid + i * NT] = g0;
+        }
+      }
+    }
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, true, 3, PT, p, Rr[J0], Ra[J0], Rl[J0]);
+    pass(IC<0>{}, true, 1, PU, p - 3, Rr[J3], Ra[J3], Rl[J3]);
     TB2_STAMP(3, p);
     __syncthreads();
     TB2_STAMP(4, p);
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, false, 2, (sl + 7) & 7, PU, p - 1, Br[J0], Ba[J0], Bl[J0]);
-    pass(IC<0>{}, false, 0, (sl + 4) & 7, PT, p - 4, Br[J3], Ba[J3], Bl[J3]);
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, false, 2, PU, p - 1, Br[J0], Ba[J0], Bl[J0]);
+    pass(IC<0>{}, false, 0, PT, p - 4, Br[J3], Ba[J3], Bl[J3]);
     TB2_STAMP(5, p);
-    store((sl + 4) & 7, PT, p - 4);
+    store(PT, p - 4);
     TB2_STAMP(6, p);
   };
 
   fetch_u(1, pstart - 1, IC<0>{});
   image(pstart - 1, IC<0>{});
-  put((pstart - 1) & 7, IC<0>{});
+  put(ps(pstart - 1), IC<0>{});
   fetch_u(0, pstart, IC<0>{});
   image(pstart, IC<0>{});
-  put(pstart & 7, IC<0>{});
+  put(ps(pstart), IC<0>{});
   fetch_u(1, pstart + 1, IC<0>{});
-  fetch_c(0, pstart, IC<0>{});
-  if (PF == 2) {
-    fetch_u(0, pstart + 2, IC<PF - 1>{});
-    fetch_c(1, pstart + 1, IC<PF - 1>{});
+  if constexpr (RES) {  // phi planes pstart-1 .. pstart+1 in the ring, r of plane pstart
+    image(pstart + 1, IC<0>{});
+    put(ps(pstart + 1), IC<0>{});
+    fetch_u(0, pstart + 2, IC<0>{});
+    fetch_u(1, pstart + 3, IC<1>{});
+    fetch_c(0, pstart, IC<0>{});
+    fetch_c(1, pstart + 1, IC<1>{});
+    __syncthreads();
+    residual(0, pstart, IC<0>{});
+    __syncthreads();  // (step pstart's put overwrites phi plane pstart-1)
+  } else {
+    fetch_c(0, pstart, IC<0>{});
+    if (PF == 2) {
+      fetch_u(0, pstart + 2, IC<PF - 1>{});
+      fetch_c(1, pstart + 1, IC<PF - 1>{});
+    }
   }
   // (up to three steps past pend: their passes and stores fall outside every
   // range test, their loads are clamped)
@@ -622,7 +769,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 }
 
 
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST>
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool RES = false>
 __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  double *__restrict__ acc,
                                                  const T *__restrict__ ui,
@@ -630,9 +777,11 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  const T *__restrict__ a,
                                                  const BoxArgs g, const StencilCoefs s,
                                                  const TB2Ghosts<T> gg, int kc, int ntx, int nty,
-                                                 int nblocks) {
-  using F = TB2<TX, TY, NT>;
-  __shared__ T R[F::NS * F::SS];  // red element of every pair, 8 plane slots
+                                                 int nblocks, T *__restrict__ ro,
+                                                 const TB2Ghosts<T> gr,
+                                                 double *__restrict__ parts) {
+  using F = TB2<TX, TY, NT, RES ? 9 : 8>;
+  __shared__ T R[F::NS * F::SS];  // red element of every pair, one per ring slot
   __shared__ T B[F::NS * F::SS];  // black element
   const int L = sweep::xcd_tile(blockIdx.x, nblocks);
   const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
@@ -641,22 +790,37 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   // uniform: the x / y domain faces the tile's rings (3 cells) reach
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
+  double nmax = 0.0;  // RES: max |r| over this workgroup's tile cells
   if (ef)
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
-                                               z1, ef);
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
+                                                       z0, z1, ef, ro, gr, nmax);
   else
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
-                                                z1, 0);
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
+                                                        z0, z1, 0, ro, gr, nmax);
+  if constexpr (RES) {  // the workgroup's partial of the max norm
+    __shared__ double wmax[NT / 64];
+    for (int o = 32; o > 0; o >>= 1) {
+      const double v = __shfl_xor(nmax, o, 64);
+      nmax = nmax > v ? nmax : v;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = nmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double m = wmax[0];
+      for (int w = 1; w < NT / 64; ++w) m = m > wmax[w] ? m : wmax[w];
+      parts[blockIdx.x] = m;
+    }
+  }
 }
 
-template <class T, int TX, int TY, int NT>
+template <class T, int TX, int TY, int NT, bool RES = false>
 int tb2_resident_slots() {
   static const int slots = [] {
     int dev = 0, ncu = 0, per = 0;
     MGIC_HIP(hipGetDevice(&dev));
     MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     MGIC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per, k_gsrb_tb2<T, TX, TY, NT, false, false, true>, NT, 0));
+        &per, k_gsrb_tb2<T, TX, TY, NT, RES, false, true, RES>, NT, 0));
     return (per > 0 ? per : 1) * (ncu > 0 ? ncu : 1);
   }();
   return slots;
@@ -679,23 +843,33 @@ int tb2_choose_kc(int tiles, int nz, int slots) {
   return best;
 }
 
+// the launch geometry of one two-sweep launch (tiles, z chunk, blocks)
+template <class T, int TX, int TY, int NT, bool RES = false>
+struct TB2Geom {
+  int ntx, nty, kc, nblocks;
+  explicit TB2Geom(const BoxArgs &g) {
+    ntx = (g.nx + TX - 1) / TX;
+    nty = (g.ny + TY - 1) / TY;
+    // the raw buffer stores address a plane with unsigned 32-bit byte offsets
+    // and drop masked lanes at kDrop = 2^31: every in-plane offset must stay
+    // below that, or valid stores would be dropped silently
+    if ((double)(g.ny + 8) * (double)g.sy * sizeof(T) >= 2147483648.0)
+      throw Error(kBadArg, "two-sweep launch: a plane exceeds the 2 GB buffer-offset range");
+    static const int kc_env = [] {
+      const char *e = getenv("MGIC_TB2_KC");
+      return e ? atoi(e) : 0;
+    }();
+    kc = kc_env >= 8 ? (kc_env < g.nz ? kc_env : g.nz)
+                     : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<T, TX, TY, NT, RES>());
+    nblocks = ntx * nty * ((g.nz + kc - 1) / kc);
+  }
+};
+
 template <class T, int TX, int TY, int NT>
 void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs &g,
                 const StencilCoefs &s, bool zero_in, double *acc, hipStream_t st) {
-  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
-  // the raw buffer stores address a plane with unsigned 32-bit byte offsets
-  // and drop masked lanes at kDrop = 2^31: every in-plane offset must stay
-  // below that, or valid stores would be dropped silently
-  if ((double)(g.ny + 8) * (double)g.sy * sizeof(T) >= 2147483648.0)
-    throw Error(kBadArg, "two-sweep launch: a plane exceeds the 2 GB buffer-offset range");
-  static const int kc_env = [] {
-    const char *e = getenv("MGIC_TB2_KC");
-    return e ? atoi(e) : 0;
-  }();
-  int kc = kc_env >= 8 ? (kc_env < g.nz ? kc_env : g.nz)
-                       : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<T, TX, TY, NT>());
-  const int ntz = (g.nz + kc - 1) / kc;
-  const int nblocks = ntx * nty * ntz;
+  const TB2Geom<T, TX, TY, NT> G(g);
+  const int ntx = G.ntx, nty = G.nty, kc = G.kc, nblocks = G.nblocks;
   const dim3 grid((unsigned)nblocks), block(NT);
   const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0;
   const TB2Ghosts<T> gg = make_ghosts<T>(g);
@@ -705,7 +879,8 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
         throw Error(kBadArg, "two-sweep launch: zero input under an inhomogeneous BC");
 #define MGIC_TB2(Z, A, FA)                                                                        \
   k_gsrb_tb2<T, TX, TY, NT, Z, A, FA><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, g, s, gg, \
-                                                              kc, ntx, nty, nblocks)
+                                                              kc, ntx, nty, nblocks, nullptr, gg, \
+                                                              nullptr)
   if (acc) {
     if constexpr (std::is_same<T, double>::value) {
       if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
@@ -726,7 +901,42 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   if (e != hipSuccess) throw Error(kHipErr, std::string("two-sweep launch: ") + hipGetErrorString(e));
 }
 
+// the fused-residual launch (RES): 64 x 20 tiles, so that the 9-slot ring
+// (148 + 12 KB) fits the 160 KB of LDS
+constexpr int kResTY = 20;
+
 }  // namespace
+
+long gsrb_sweep_tb2_res_blocks(const BoxArgs &g) {
+  return TB2Geom<double, 64, kResTY, 1024, true>(g).nblocks;
+}
+
+void gsrb_sweep_tb2_res(double *e_out, double *r_out, const double *phi, const double *rhs,
+                        const double *a, const BoxArgs &g_hom, const BoxArgs &g_res,
+                        const StencilCoefs &s, double *partials, hipStream_t st) {
+  constexpr int TX = 64, TY = kResTY, NT = 1024;
+  const TB2Geom<double, TX, TY, NT, true> G(g_hom);
+  const dim3 grid((unsigned)G.nblocks), block(NT);
+  const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0;
+  const TB2Ghosts<double> gg = make_ghosts<double>(g_hom), gr = make_ghosts<double>(g_res);
+  for (int f = 0; f < 6; ++f) {
+    if (g_hom.bcm[f] == kBcMemory || g_res.bcm[f] == kBcMemory)
+      throw Error(kBadArg, "fused-residual launch: exchanged faces are not supported");
+    if (gg.c[f] != 0.0)
+      throw Error(kBadArg, "fused-residual launch: the correction's BC must be homogeneous");
+  }
+  if (fast)
+    k_gsrb_tb2<double, TX, TY, NT, true, false, true, true><<<grid, block, 0, st>>>(
+        e_out, nullptr, phi, rhs, a, g_hom, s, gg, G.kc, G.ntx, G.nty, G.nblocks, r_out, gr,
+        partials);
+  else
+    k_gsrb_tb2<double, TX, TY, NT, true, false, false, true><<<grid, block, 0, st>>>(
+        e_out, nullptr, phi, rhs, a, g_hom, s, gg, G.kc, G.ntx, G.nty, G.nblocks, r_out, gr,
+        partials);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    throw Error(kHipErr, std::string("fused-residual launch: ") + hipGetErrorString(e));
+}
 
 bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
   if (!s.bconst || kind == 0 || kind == 3) return false;

@@ -46,7 +46,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t store_rsrc(void *base) {
 }
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-// CP: cache-policy bits (0 plain; 16 = sc1)
+// CP: cache-policy bits (0 plain; 2 = nt; 16 = sc1)
 template <int CP = 0>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, double2 v, unsigned off) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, off, 0, CP);
@@ -55,11 +55,13 @@ template <int CP = 0>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, double v, unsigned off) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, CP);
 }
+template <int CP = 0>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float2 v, unsigned off) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, v), r, off, 0, CP);
 }
+template <int CP = 0>
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, float v, unsigned off) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, CP);
 }
 
 // XCD-aware workgroup -> tile order: blocks are dealt round-robin over the

@@ -44,13 +44,16 @@ def main():
                             world_size=a.world, timeout=datetime.timedelta(seconds=120))
     mg.set_device(a.device)
     comm = mg.Comm(a.rank, a.world, transport="ipc")
+    from mg_ic_code_amd.commcheck import check_transport
+    checked = check_transport(comm, a.world)  # bench.py's transport check
     case = bench.build_case(mg, comm, a.world, a.n, a.levels, 4, deep_halo=1,
                             agglomerate_below=a.agglomerate_below)
     amg, fphi, frhs, fres, grid = (case[k] for k in ("amg", "fphi", "frhs", "fres", "grid"))
     norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
     norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(a.iters)]
     comm.synchronize()
-    out = {"norms": np.array(norms), "transport": np.array(comm.transport)}
+    out = {"norms": np.array(norms), "transport": np.array(comm.transport),
+           "checked": np.array(checked)}
     for i in range(grid.num_local):
         out[f"box{i}"] = np.array(grid.local_box(i))
         out[f"phi{i}"] = fphi.download(i)

@@ -824,6 +824,16 @@ def test_full_size_512_vcycle_bitwise():
     assert o.init_residual(0) == r0
     assert [o.iteration(0) for _ in range(2)] == rg
     assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
+    # the bench's timed loop: iterations() fuses iteration 1's residual into
+    # iteration 2's first launch -- the same phi and norms, bit for bit
+    del o
+    fphi2, fres2 = mg.LevelData(grid), mg.LevelData(grid)
+    fphi2.set_zero()
+    assert amg.fused_residual
+    assert amg.init_residual(fphi2, frhs, fres2, norm_type=0) == r0
+    assert amg.iterations(fphi2, frhs, fres2, 2, norm_type=0) == rg
+    assert np.array_equal(fphi2.download(0), fphi.download(0))
+    assert np.array_equal(fres2.download(0), fres.download(0))
 
 
 @pytest.mark.gpu
@@ -908,3 +918,49 @@ def test_full_size_512_eight_boxes_rccl_deep_halo_bitwise():
     for r in out[1:]:
         assert out[0][0] == r[0]
         assert np.array_equal(out[0][1], r[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,bc,bval,kind", [
+    ((100, 66, 42), "mixed", 1.0, 2),     # ragged tiles, inhomogeneous Dirichlet / Neumann
+    ((96, 80, 72), "dirichlet", 1.0, 2),  # homogeneous, the reference's BC
+    ((72, 48, 40), "mixed", 2.0, 2),      # bCoef = 2 (the non-specialised expressions)
+    ((160, 144, 112), "dirichlet", 1.0, 1),  # the default kernel choice (fine level streamed)
+], ids=["ragged-mixed", "dirichlet", "bconst2", "default-kind"])
+@pytest.mark.parametrize("norm_type", [0, 2])
+def test_fused_residual_iterations_bitwise(rng, shape, bc, bval, kind, norm_type):
+    # AMRMultiGrid::iterations: iteration i's residual r = rhs - L(phi) (and
+    # its max norm) formed inside iteration i+1's first two-sweep launch
+    # (gsrb_sweep_tb2_res) -- phi, the residual and every norm identical to
+    # the same number of iteration() calls (themselves bit-identical to the
+    # oracle: test_vcycle_iterations_bitwise, test_full_size_512_vcycle_bitwise)
+    nx, ny, nz = shape
+    dom = (0, 0, 0, nx - 1, ny - 1, nz - 1)
+    kw = dict(bc_lo=(0, 1, 0), bc_hi=(1, 0, 0), bc_value=0.125) if bc == "mixed" else {}
+    op = mg.OperatorParams(alpha=1.0, beta=-1.0, coefficient_average_type=1, prolong_type=1,
+                           relax_mode=1, fused_smoother=kind, **kw)
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    rhs = rng.uniform(-1.0, 1.0, (nz, ny, nx))
+    phi0 = rng.uniform(-0.5, 0.5, (nz, ny, nx))
+    runs = []
+    for pipelined in (False, True):
+        grid = mg.Grid(mg.Comm(), dom, [dom], 100.0 / nx)
+        fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+        fa.upload(0, a)
+        fb.set_val(bval)
+        frhs.upload(0, rhs)
+        fphi.upload(0, phi0)
+        amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, op),
+                              mg.SolverParams(max_depth=2, n_pre=4, n_post=4, n_bottom=4,
+                                              bottom_solver=0))
+        assert amg.fused_residual  # the hierarchy takes the fused launch
+        h = [amg.init_residual(fphi, frhs, fres, norm_type=norm_type)]
+        if pipelined:
+            h += amg.iterations(fphi, frhs, fres, 3, norm_type=norm_type)
+        else:
+            h += [amg.iteration(fphi, frhs, fres, norm_type=norm_type) for _ in range(3)]
+        runs.append((h, fphi.download(0), fres.download(0)))
+    assert runs[0][0] == runs[1][0]
+    assert np.array_equal(runs[0][1], runs[1][1])
+    assert np.array_equal(runs[0][2], runs[1][2])
+    assert runs[1][0][-1] < runs[1][0][0]

@@ -76,6 +76,7 @@ def check(out, n, levels, iters=2):
     norms, phi = single_box(n, levels, iters)
     for o in out:
         assert str(o["transport"]) == "ipc"
+        assert bool(o["checked"])  # commcheck.check_transport passed on every rank
         assert list(o["norms"]) == norms, (list(o["norms"]), norms)
         i = 0
         while f"box{i}" in o:
@@ -98,3 +99,10 @@ def test_four_processes_with_agglomeration_bitwise(tmp_path):
     # gather / scatter plans run between processes too
     n, levels = 128, 3
     check(run_workers(tmp_path, 4, n, levels, agglomerate_below=17), n, levels)
+
+
+def test_transport_check_single_rank():
+    # the check bench.py runs before trusting a transport, on one rank: the
+    # periodic images arrive through local copies, the reduction is local
+    from mg_ic_code_amd.commcheck import check_transport
+    assert check_transport(mg.Comm(), 1)
