@@ -63,6 +63,10 @@ def parse():
                          "(default; time / launches) or one pair per launch")
     ap.add_argument("--no-roofline-events", action="store_true",
                     help="no events in the timed region (roofline fields null)")
+    ap.add_argument("--fused-residual", type=int, default=0,
+                    help="1: form each iteration's residual inside the next V-cycle's first "
+                         "two-sweep launch (SolverParams.fused_residual; measured slower, "
+                         "DESIGN.md 3); 0 (default): a separate residual launch")
     ap.add_argument("--norm-type", type=int, default=0,
                     help="per-iteration residual norm of AMRMultiGrid's stop test (params.txt:37-38, "
                          "m_normType 0 = max norm; -1 skips it)")
@@ -114,7 +118,7 @@ def main():
                       fused=0 if args.no_fused else 1, overlap=args.overlap,
                       deep_halo=(1 if world > 1 else 0) if args.deep_halo < 0 else args.deep_halo,
                       agglomerate_below=(32 if world > 1 else 0) if args.agglomerate_below < 0
-                      else args.agglomerate_below)
+                      else args.agglomerate_below, fused_residual=args.fused_residual)
     n = args.size
     boxes, grid, fa, frhs, fphi, fres = (case[k] for k in ("boxes", "grid", "fa", "frhs", "fphi",
                                                            "fres"))
@@ -280,7 +284,7 @@ def make_comm(mg, torch, dist, rank, world, transport):
 
 
 def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fused=1, overlap=0,
-               deep_halo=0, agglomerate_below=0):
+               deep_halo=0, agglomerate_below=0, fused_residual=0):
     """The bench workload (BASELINE config C3 / C4): n^3 split over `world`
     ranks (z first), SetBinaryBH aCoef / rhs of params.txt at psi = 1 on
     device, bCoef = 1, phi = 0, the reference operator settings, and an
@@ -304,7 +308,8 @@ def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fu
                                   deep_halo=deep_halo)
     fac = mg.defineOperatorFactory(grid, fa, fb, op_params)
     sp = mg.SolverParams(max_depth=levels - 1, n_pre=nsmooth, n_post=nsmooth, n_bottom=nsmooth,
-                         bottom_solver=0, agglomerate_below=agglomerate_below)
+                         bottom_solver=0, agglomerate_below=agglomerate_below,
+                         fused_residual=fused_residual)
     amg = mg.AMRMultiGrid(fac, sp)
     assert amg.num_depths == levels, amg.num_depths
     return dict(dom=dom, boxes=boxes, owners=owners, dx=dx, grid=grid, fa=fa, fb=fb, frhs=frhs,

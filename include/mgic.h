@@ -86,6 +86,10 @@ typedef struct {
   int bicg_imax;
   double bicg_eps, bicg_reps, bicg_small;
   int bicg_restarts, bicg_norm_type;
+  int fused_residual;    /* 1: AMRMultiGrid iterations form r = rhs - L(phi) inside the next
+                            V-cycle's first two-sweep launch (mgic_mg_iterations, the
+                            preconditioner); 0 (default): a separate residual launch, which
+                            measured faster */
 } mgic_mg_params;
 
 MGIC_API const char *mgic_version(void);

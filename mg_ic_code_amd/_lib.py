@@ -70,6 +70,7 @@ class MGParams(ctypes.Structure):
         ("bicg_small", c_double),
         ("bicg_restarts", c_int),
         ("bicg_norm_type", c_int),
+        ("fused_residual", c_int),
     ]
 
 

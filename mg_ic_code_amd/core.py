@@ -351,6 +351,7 @@ class SolverParams:
     bicg_small: float = 1.0e-30
     bicg_restarts: int = 5
     bicg_norm_type: int = 2
+    fused_residual: int = 0  # 1: residual inside the next V-cycle's first launch
 
     def to_c(self) -> MGParams:
         p = MGParams()

@@ -97,6 +97,7 @@ MGParams to_mg(const mgic_mg_params *p) {
   m.bicg.small = p->bicg_small;
   m.bicg.numRestarts = p->bicg_restarts;
   m.bicg.normType = p->bicg_norm_type;
+  m.fused_residual = p->fused_residual;
   return m;
 }
 
@@ -220,6 +221,7 @@ MGIC_API void mgic_mg_params_default(mgic_mg_params *p) {
   p->bicg_small = m.bicg.small;
   p->bicg_restarts = m.bicg.numRestarts;
   p->bicg_norm_type = m.bicg.normType;
+  p->fused_residual = m.fused_residual;
 }
 
 // ---------------------------------------------------------------- comm

@@ -662,11 +662,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
 }
 
 bool VariableCoeffPoissonOperator::fusedResidualApplies(int n) {
-  static const int on = [] {  // MGIC_FUSED_RESIDUAL=0: separate residual launches (A/B)
-    const char *e = getenv("MGIC_FUSED_RESIDUAL");
-    return e ? atoi(e) : 1;
-  }();
-  if (!on || n < 2 || prm.relax_mode != 1 || cf || grid->has_memory_faces() ||
+  if (n < 2 || prm.relax_mode != 1 || cf || grid->has_memory_faces() ||
       !fusedSmootherApplies() || sweeps_per_launch() != 2)
     return false;
   const StencilCoefs s = coefs();
@@ -1209,7 +1205,7 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
 }
 
 bool MultiGrid::fusedResidualApplies() {
-  return depths() >= 2 && op(0).fusedResidualApplies(prm.n_pre);
+  return prm.fused_residual && depths() >= 2 && op(0).fusedResidualApplies(prm.n_pre);
 }
 
 void MultiGrid::oneCycleResidualFromZero(LevelData &e, LevelData &r, LevelData &phi,

@@ -257,6 +257,7 @@ struct MGParams {
   int bottom_solver = 1;       // 0: relax(n_bottom), 1: BiCGStab
   int cycles = 1;              // 1 = V-cycle
   int agglomerate_below = 0;   // gather to rank 0 when a box side < this (0 off)
+  int fused_residual = 0;      // residual inside the next V-cycle's first launch (1 on)
   BiCGStabParams bicg;
 };
 

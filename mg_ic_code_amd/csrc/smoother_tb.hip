@@ -247,6 +247,25 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     if constexpr (RES) return 6 + (q + 12) % 3;
     else return q & 7;
   };
+  // the slot of plane q + j from plane q's slot s0 (scalar adds and
+  // selects: the steps derive every slot from one es / ps per step)
+  auto eadd = [](int s0, int j) -> int {
+    if constexpr (RES) {
+      int v = s0 + j;
+      v = v < 0 ? v + 6 : v;
+      return v >= 6 ? v - 6 : v;
+    } else {
+      return (s0 + j) & 7;
+    }
+  };
+  auto padd = [](int s0, int j) -> int {  // j in 0 .. 2
+    if constexpr (RES) {
+      const int v = s0 + j;
+      return v >= 9 ? v - 3 : v;
+    } else {
+      return (s0 + j) & 7;
+    }
+  };
 
   // ---- loads of u (slot c = LDS pair index), per plane parity t ----------
   // (ghost pairs of x / y domain faces load whatever the ghost cells hold:
@@ -337,7 +356,16 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // plane p+1 while step p runs; PF 2: planes p+3 / p+2, one register set
   // per step parity)
   constexpr int PF = (TB2_PF2 && !ACC) ? 2 : 1;
-  T pu0[PF][NL], pu1[PF][NL];
+  // (RES: the phi planes one step ahead only -- its registers are the
+  // tightest; PFU u register sets)
+  constexpr int PFU = RES ? 1 : PF;
+  // LAMC (RES): lambda is not carried in registers but recomputed where a
+  // pass needs it (two more divisions per step, 16 VGPRs fewer)
+#ifndef TB2_RES_LAMC
+#define TB2_RES_LAMC 1
+#endif
+  constexpr bool LAMC = RES && TB2_RES_LAMC;
+  T pu0[PFU][NL], pu1[PFU][NL];
   T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
@@ -454,7 +482,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // +0 either way.  Sweep-1 black starts from its own u = 0 (the constant
   // lets x - 2*0 fold to x, exact).  Both skip the LDS reads they no longer
   // need.
-  auto pass = [&](auto zc, bool red, int W, int t, int k, const T (&cr)[NP],
+  auto pass = [&](auto zc, bool red, int W, int t, int k, int sk, const T (&cr)[NP],
                   const T (&ca)[NP], const T (&cl)[NP]) {
     constexpr int ZC = decltype(zc)::value;
     if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
@@ -463,10 +491,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     if (NP == 1 && W < 3 && wv < 3 - W) return;  // (one pair per lane only)
     if ((TB2_PROBE_SKIP & 8) && red) return;
     if ((TB2_PROBE_SKIP & 16) && !red) return;
-    T *X = (red ? R : B) + es(k) * SS;
-    T *N = (red ? B : R) + es(k) * SS;
-    T *Nm = (red ? B : R) + es(k - 1) * SS;
-    T *Np = (red ? B : R) + es(k + 1) * SS;
+    T *X = (red ? R : B) + sk * SS;  // sk = es(k)
+    T *N = (red ? B : R) + sk * SS;
+    T *Nm = (red ? B : R) + eadd(sk, -1) * SS;
+    T *Np = (red ? B : R) + eadd(sk, 1) * SS;
     if constexpr (ZC == 1) {
       T v[NP];
 #pragma unroll
@@ -535,8 +563,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // an out-of-range offset, so every step issues exactly NP * 2 stores with
   // no branch around them and the next step waits vmcnt(2) for its loads
   // instead of vmcnt(0), which would also wait for these stores.
-  auto store = [&](int t, int k) {
-    const int sl = es(k);
+  auto store = [&](int t, int k, int sl) {  // sl = es(k)
     if (TB2_PROBE_SKIP & 4) return;
     const bool kin = k >= z0 && k < z1;  // uniform
     char *dst = ACC ? reinterpret_cast<char *>(acc + corner + (long)clampi(k, z0, z1 - 1) * sz)
@@ -571,13 +598,14 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // with x / y domain-face neighbours as gr's ghosts of the cell (ParseBC of
   // the residual's BC) and z ghost planes imaged in the ring.  The tile's
   // cells of planes [z0, z1) are stored to ro and enter nmax.
-  auto residual = [&](int t, int k, auto bc) {
+  auto residual = [&](int t, int k, auto bc, int sm) {  // sm = ps(k - 1)
     constexpr int b = decltype(bc)::value;
     if constexpr (RES) {
       if ((unsigned)(k - kl[3]) > kw[3]) return;  // uniform: outside sweep-1 red's planes
-      const T *Rc = R + ps(k) * SS, *Bc = B + ps(k) * SS;
-      const T *Rm = R + ps(k - 1) * SS, *Bm = B + ps(k - 1) * SS;
-      const T *Rq = R + ps(k + 1) * SS, *Bq = B + ps(k + 1) * SS;
+      const int sc = padd(sm, 1), sq = padd(sm, 2);
+      const T *Rc = R + sc * SS, *Bc = B + sc * SS;
+      const T *Rm = R + sm * SS, *Bm = B + sm * SS;
+      const T *Rq = R + sq * SS, *Bq = B + sq * SS;
       auto res = [&](T c, T xm, T xp, T ym, T yp, T zm, T zp, T rv, T aa) -> T {
         const T r0 = rv - s.alpha * aa * c;  // .ChF:314-316
         const T tx = (xp + xm) - (T)2 * c;
@@ -622,6 +650,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
           }
         }
         const T r0 = res(u0, xm0, xp0, ym0, yp0, zm0, zp0, nr0[b][i], na0[b][i]);
+        __builtin_amdgcn_sched_barrier(0);  // (one element's operands live at a time)
         const T r1 = res(u1, xm1, xp1, ym1, yp1, zm1, zp1, nr1[b][i], na1[b][i]);
         nr0[b][i] = r0;
         nr1[b][i] = r1;
@@ -669,19 +698,20 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     for (int i = 0; i < NP; ++i) {
       Br[J0][i] = rb[i];
       Ba[J0][i] = FAST ? ab[i] : s.alpha * ab[i];
-      Bl[J0][i] = lam(Ba[J0][i]);
+      if constexpr (!LAMC) Bl[J0][i] = lam(Ba[J0][i]);
       Rr[J0][i] = nr0[FB][i];
       Ra[J0][i] = FAST ? na0[FB][i] : s.alpha * na0[FB][i];
-      Rl[J0][i] = lam(Ra[J0][i]);
+      if constexpr (!LAMC) Rl[J0][i] = lam(Ra[J0][i]);
       rb[i] = nr1[FB][i];
       ab[i] = na1[FB][i];
     }
-    if constexpr (RES) {  // phi of plane p+2 into the phi ring
-      image(p + 2, ICF{});
-      put(ps(p + 2), ICF{});
+    const int E0 = es(p), P0 = ps(p);  // this step's slots derive from these
+    if constexpr (RES) {  // phi of plane p+2 into the phi ring (one u register set)
+      image(p + 2, IC<0>{});
+      put(padd(P0, 2), IC<0>{});
     } else {
       image(p + 1, ICF{});
-      put(ps(p + 1), ICF{});
+      put(padd(P0, 1), ICF{});
     }
     if (PF == 2) fetch_c(PT, p + 2, ICF{});
     else fetch_c(PU, p + 1, ICF{});
@@ -696,7 +726,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         an1[i] = v.y;
       }
     }
-    if constexpr (RES) fetch_u(PT, p + 4, ICF{});
+    if constexpr (RES) fetch_u(PU, p + 3, IC<0>{});
     else if (PF == 2) fetch_u(PU, p + 3, ICF{});
     else fetch_u(PT, p + 2, ICF{});
     TB2_STAMP(1, p);
@@ -705,7 +735,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     // RES: r of plane p+1 (phi planes p .. p+2 are in the phi ring) into the
     // coefficient set that step p+1 turns into plane p+1's sweep-1 inputs
     if constexpr (RES) {
-      residual(PU, p + 1, IC<FB ^ 1>{});
+      residual(PU, p + 1, IC<FB ^ 1>{}, P0);
       // a z ghost plane of the (zero) correction: its red elements image the
       // black cells of the face plane, which are 0 until sweep-1 black reads
       // them (the plain ZIN launch puts those images with the zero input;
@@ -714,7 +744,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       // slot's previous plane was last read in step p-1's black phase.)
       if (p == zgl || p == zgh) {
         const T g0 = ghost(gg, p == zgl ? 4 : 5, (T)0);
-        T *Rs = R + es(p) * SS;
+        T *Rs = R + E0 * SS;
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
           if (NL * NT > CP && tid + i * NT >= CP) continue;
@@ -722,15 +752,25 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         }
       }
     }
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, true, 3, PT, p, Rr[J0], Ra[J0], Rl[J0]);
-    pass(IC<0>{}, true, 1, PU, p - 3, Rr[J3], Ra[J3], Rl[J3]);
+    // (LAMC: lambda recomputed from alpha*a where a pass needs it)
+    auto lamv = [&](const T(&aa)[NP], T(&out)[NP]) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) out[i] = lam(aa[i]);
+    };
+    T lt[NP];
+    if constexpr (LAMC) lamv(Ra[J0], lt);
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], LAMC ? lt : Rl[J0]);
+    if constexpr (LAMC) lamv(Ra[J3], lt);
+    pass(IC<0>{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], LAMC ? lt : Rl[J3]);
     TB2_STAMP(3, p);
     __syncthreads();
     TB2_STAMP(4, p);
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, false, 2, PU, p - 1, Br[J0], Ba[J0], Bl[J0]);
-    pass(IC<0>{}, false, 0, PT, p - 4, Br[J3], Ba[J3], Bl[J3]);
+    if constexpr (LAMC) lamv(Ba[J0], lt);
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], LAMC ? lt : Bl[J0]);
+    if constexpr (LAMC) lamv(Ba[J3], lt);
+    pass(IC<0>{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], LAMC ? lt : Bl[J3]);
     TB2_STAMP(5, p);
-    store(PT, p - 4);
+    store(PT, p - 4, eadd(E0, -4));
     TB2_STAMP(6, p);
   };
 
@@ -745,11 +785,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     image(pstart + 1, IC<0>{});
     put(ps(pstart + 1), IC<0>{});
     fetch_u(0, pstart + 2, IC<0>{});
-    fetch_u(1, pstart + 3, IC<1>{});
     fetch_c(0, pstart, IC<0>{});
     fetch_c(1, pstart + 1, IC<1>{});
     __syncthreads();
-    residual(0, pstart, IC<0>{});
+    residual(0, pstart, IC<0>{}, ps(pstart - 1));
     __syncthreads();  // (step pstart's put overwrites phi plane pstart-1)
   } else {
     fetch_c(0, pstart, IC<0>{});
@@ -902,8 +941,12 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
 }
 
 // the fused-residual launch (RES): 64 x 20 tiles, so that the 9-slot ring
-// (148 + 12 KB) fits the 160 KB of LDS
-constexpr int kResTY = 20;
+// (156 KB) fits the 160 KB of LDS (TB2_RES_TY: measurement builds; 18 has
+// one u load per lane)
+#ifndef TB2_RES_TY
+#define TB2_RES_TY 20
+#endif
+constexpr int kResTY = TB2_RES_TY;
 
 }  // namespace
 
