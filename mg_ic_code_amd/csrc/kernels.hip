@@ -671,6 +671,34 @@ __global__ __launch_bounds__(RB) void k_reduce_final(const double *__restrict__ 
   if (threadIdx.x == 0) out[0] = sm[0];
 }
 
+// max-type kinds (3, 4, 5): any order gives the same result, so a wide
+// block with four independent loads in flight per thread (the single 256-
+// thread loop above is latency bound: 16 K residual partials took 25 us)
+template <int KIND>
+__global__ __launch_bounds__(1024) void k_reduce_final_wide(const double *__restrict__ p, int n,
+                                                           double *__restrict__ out) {
+  static_assert(KIND >= 3, "order-independent reductions only");
+  __shared__ double sm[16];
+  double a0 = red_init<KIND>(), a1 = a0, a2 = a0, a3 = a0;
+  int t = threadIdx.x;
+  for (; t + 3 * 1024 < n; t += 4 * 1024) {
+    a0 = red_op<KIND>(a0, p[t]);
+    a1 = red_op<KIND>(a1, p[t + 1024]);
+    a2 = red_op<KIND>(a2, p[t + 2048]);
+    a3 = red_op<KIND>(a3, p[t + 3072]);
+  }
+  for (; t < n; t += 1024) a0 = red_op<KIND>(a0, p[t]);
+  double acc = red_op<KIND>(red_op<KIND>(a0, a1), red_op<KIND>(a2, a3));
+  for (int o = 32; o > 0; o >>= 1) acc = red_op<KIND>(acc, __shfl_xor(acc, o, 64));
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = sm[0];
+    for (int w = 1; w < 16; ++w) m = red_op<KIND>(m, sm[w]);
+    out[0] = m;
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void k_copy_items(const CopyItem *__restrict__ items,
                                                     T *const *__restrict__ src_tab,
@@ -1273,9 +1301,9 @@ void reduce_final(int kind, const double *partials, int n, double *out, hipStrea
     case 0: k_reduce_final<0><<<1, RB, 0, st>>>(partials, n, out); break;
     case 1: k_reduce_final<1><<<1, RB, 0, st>>>(partials, n, out); break;
     case 2: k_reduce_final<2><<<1, RB, 0, st>>>(partials, n, out); break;
-    case 3: k_reduce_final<3><<<1, RB, 0, st>>>(partials, n, out); break;
-    case 4: k_reduce_final<4><<<1, RB, 0, st>>>(partials, n, out); break;
-    case 5: k_reduce_final<5><<<1, RB, 0, st>>>(partials, n, out); break;
+    case 3: k_reduce_final_wide<3><<<1, 1024, 0, st>>>(partials, n, out); break;
+    case 4: k_reduce_final_wide<4><<<1, 1024, 0, st>>>(partials, n, out); break;
+    case 5: k_reduce_final_wide<5><<<1, 1024, 0, st>>>(partials, n, out); break;
     default: throw Error(kBadArg, "reduce: bad kind");
   }
   check_launch();
