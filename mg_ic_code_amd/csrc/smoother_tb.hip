@@ -84,14 +84,15 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_STORE_CPOL
 #define TB2_STORE_CPOL 0
 #endif
-// TB2_NT_INT 1 = the waves whose loads cover only interior rows of the tile
-// (no y halo) load u / rhs / aCoef non-temporally: those lines are read by
-// this tile alone, so keeping them out of L2 leaves it to the halo lines that
-// the neighbouring tiles share.  Measured (r03, three interleaved rounds on
-// one box): 1.39 vs 1.08 ms per 512^3 launch -- the wave-uniform select
-// between the two load forms costs more than L2 gains; off
-#ifndef TB2_NT_INT
-#define TB2_NT_INT 0
+// TB2_NTW 1 = the waves whose loads cover only rows no other tile reads
+// (outside this tile's y halo and outside the y halos of the tiles above and
+// below) load u / rhs / aCoef non-temporally, keeping L2 for the halo lines
+// neighbouring tiles share; the choice is a template parameter of the tile
+// body (the waves run separate code), so no load is selected at run time.
+// (An earlier form selected per load and counted the neighbours' halo rows as
+// private: 1.39 vs 1.08 ms.)
+#ifndef TB2_NTW
+#define TB2_NTW 0
 #endif
 // TB2_ZIN_SHORT 0 = ZIN launches run sweep 1 through the generic passes
 #ifndef TB2_ZIN_SHORT
@@ -180,7 +181,8 @@ template <> struct TB2Vec<float> { using type = float2; };
 // registers in place of the loaded rhs, and its tile cells are stored to ro
 // (the restriction and the later sweeps read it) while their max |r| goes
 // to *nmax.  Bit-identical to k_residual_z2 followed by the ZIN launch.
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE, bool RES>
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE, bool RES,
+          bool NTW = false>
 __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                                          T *__restrict__ uo, double *__restrict__ acc,
                                          const T *__restrict__ ui,
@@ -392,8 +394,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         pu0[b][i] = 0.0;
         pu1[b][i] = 0.0;
       } else if (NL * NT <= CP || tid + i * NT < CP) {  // (whole waves past the plane skip)
-        // interior-row waves of the first load (TB2_NT_INT): rows 4 .. TY+3
-        const bool nt = TB2_NT_INT && i == 0 && wv * 64 >= 4 * PW && wv * 64 + 63 < (TY + 4) * PW;
+        const bool nt = NTW && i == 0;  // (the kernel picks NTW waves by their rows)
         const V v = nt ? at2n(pl, loff[t][i]) : at2(pl, loff[t][i]);
         pu0[b][i] = v.x;
         pu1[b][i] = v.y;
@@ -437,9 +438,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         na1[b][i] = -1.25;
         continue;
       }
-      // interior-row waves (TB2_NT_INT): wave w holds rows w and NR-1-w, and
-      // rows 3 .. TY+2 are the tile's
-      const bool nt = TB2_NT_INT && NP == 1 && wv >= 3 && wv < NR / 2;
+      const bool nt = NTW && NP == 1;
       const V vr = nt ? at2n(pr, roff[t][i]) : at2(pr, roff[t][i]);
       const V va = nt ? at2n(pa, roff[t][i]) : at2(pa, roff[t][i]);
       nr0[b][i] = vr.x;
@@ -830,12 +829,30 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
   double nmax = 0.0;  // RES: max |r| over this workgroup's tile cells
-  if (ef)
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
-                                                       z0, z1, ef, ro, gr, nmax);
-  else
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
-                                                        z0, z1, 0, ro, gr, nmax);
+  // TB2_NTW: the waves whose u rows (first load: pairs 64w .. 64w+63 of the
+  // plane, PW per row) and rhs / aCoef rows (update rows w and TY+5-w) all
+  // lie in rows no other tile reads: LDS rows 8 .. TY-1, update rows 6 .. TY-1
+  using F0 = TB2<TX, TY, NT>;
+  constexpr int kNtLo = (8 * F0::PW + 63) / 64 > 6 ? (8 * F0::PW + 63) / 64 : 6;
+  constexpr int kNtHi = (TY * F0::PW) / 64 - 1 < TY + 5 - 6 ? (TY * F0::PW) / 64 - 1 : TY - 1;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const bool ntw = TB2_NTW && !RES && (NT / 64) >= kNtHi && wv >= kNtLo && wv <= kNtHi &&
+                   (TY + 5 - wv) <= TY - 1;
+  if (ef) {
+    if (ntw)
+      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, RES, true>(R, B, uo, acc, ui, rhs, a, g, s, gg,
+                                                               x0, y0, z0, z1, ef, ro, gr, nmax);
+    else
+      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
+                                                         z0, z1, ef, ro, gr, nmax);
+  } else {
+    if (ntw)
+      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, RES, true>(R, B, uo, acc, ui, rhs, a, g, s, gg,
+                                                                x0, y0, z0, z1, 0, ro, gr, nmax);
+    else
+      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0,
+                                                          y0, z0, z1, 0, ro, gr, nmax);
+  }
   if constexpr (RES) {  // the workgroup's partial of the max norm
     __shared__ double wmax[NT / 64];
     for (int o = 32; o > 0; o >>= 1) {
