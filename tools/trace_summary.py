@@ -27,6 +27,21 @@ def summarise(path):
     return out
 
 
+def timeline(path, last=90):
+    """The last `last` launches in start order: duration and idle gap before."""
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    out, prev = [], None
+    for r in rows[-last:]:
+        m = re.search(r"::(k_\w+(?:<[^>]*>)?)\(", r["Kernel_Name"])
+        name = m.group(1) if m else r["Kernel_Name"][:40]
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s - prev) / 1e3 if prev is not None else 0.0
+        prev = e
+        g = "x".join((r["Grid_Size_X"], r["Grid_Size_Y"], r["Grid_Size_Z"]))
+        out.append(f"{name[:60]:60s} grid={g:16s} dur={(e - s) / 1e3:9.1f}us gap={gap:8.1f}us")
+    return out
+
+
 def clusters(durations, gap=1.8):
     """Split durations into groups separated by a jump of more than `gap`x."""
     v = sorted(durations)
@@ -43,3 +58,5 @@ def clusters(durations, gap=1.8):
 
 if __name__ == "__main__":
     print("\n".join(summarise(sys.argv[1])))
+    print("--- last launches (start order) ---")
+    print("\n".join(timeline(sys.argv[1])))
