@@ -67,7 +67,10 @@ using IC = std::integral_constant<int, N>;
 // diagnostic builds of tools/tb2_probe.hip only: bit 0 skips the global
 // loads, bit 1 the colour passes, bit 2 the stores, bit 3 the red (phase A)
 // passes, bit 4 the black (phase B) passes, bit 5 replaces the update chain
-// by six adds of its inputs, bit 6 the divisions (wrong results, timing)
+// by six adds of its inputs, bit 6 the divisions, bit 7 the barrier between
+// the red and the black phase, bit 8 the barrier before the red phase, bit 9
+// loads every plane from planes 0 / 1 (L2-resident: the same instructions
+// without the HBM stream), bit 10 drops every store (wrong results, timing)
 #ifndef TB2_PROBE_SKIP
 #define TB2_PROBE_SKIP 0
 #endif
@@ -217,6 +220,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   const long corner = -16 - 4 * sy;
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
   auto plane = [&](const T *f, int p) {  // corner of (clamped) plane p
+    if (TB2_PROBE_SKIP & 512) p = __builtin_amdgcn_readfirstlane(p & 1);
     return reinterpret_cast<const char *>(f + corner + (long)clampi(p, -4, nz + 3) * sz);
   };
   // the lane offset is laundered per access: otherwise the compiler hoists
@@ -582,8 +586,13 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       const unsigned off = roff[t][i];
       // both elements (st 3) as one pair store; a single one (st 1 / 2, the
       // tile's x edges) as an element store
-      const unsigned o4 = st == 3 ? off : kDrop;
-      const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
+      unsigned o4 = st == 3 ? off : kDrop;
+      unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
+      if (TB2_PROBE_SKIP & 1024) {
+        asm volatile("" : "+v"(o4), "+v"(o2));
+        o4 |= kDrop;
+        o2 |= kDrop;
+      }
       const T e = st == 1 ? w.x : w.y;
       sweep::bstore<TB2_STORE_CPOL>(rs, w, o4);
       sweep::bstore<TB2_STORE_CPOL>(rs, e, o2);
@@ -705,6 +714,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       ab[i] = na1[FB][i];
     }
     const int E0 = es(p), P0 = ps(p);  // this step's slots derive from these
+    TB2_STAMP(1, p);
     if constexpr (RES) {  // phi of plane p+2 into the phi ring (one u register set)
       image(p + 2, IC<0>{});
       put(padd(P0, 2), IC<0>{});
@@ -712,6 +722,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       image(p + 1, ICF{});
       put(padd(P0, 1), ICF{});
     }
+    TB2_STAMP(2, p);
     if (PF == 2) fetch_c(PT, p + 2, ICF{});
     else fetch_c(PU, p + 1, ICF{});
     if constexpr (ACC) {
@@ -728,9 +739,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     if constexpr (RES) fetch_u(PU, p + 3, IC<0>{});
     else if (PF == 2) fetch_u(PU, p + 3, ICF{});
     else fetch_u(PT, p + 2, ICF{});
-    TB2_STAMP(1, p);
-    __syncthreads();
-    TB2_STAMP(2, p);
+    TB2_STAMP(3, p);
+    if (!(TB2_PROBE_SKIP & 256)) __syncthreads();
+    TB2_STAMP(4, p);
     // RES: r of plane p+1 (phi planes p .. p+2 are in the phi ring) into the
     // coefficient set that step p+1 turns into plane p+1's sweep-1 inputs
     if constexpr (RES) {
@@ -761,16 +772,16 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], LAMC ? lt : Rl[J0]);
     if constexpr (LAMC) lamv(Ra[J3], lt);
     pass(IC<0>{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], LAMC ? lt : Rl[J3]);
-    TB2_STAMP(3, p);
-    __syncthreads();
-    TB2_STAMP(4, p);
+    TB2_STAMP(5, p);
+    if (!(TB2_PROBE_SKIP & 128)) __syncthreads();
+    TB2_STAMP(6, p);
     if constexpr (LAMC) lamv(Ba[J0], lt);
     pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], LAMC ? lt : Bl[J0]);
     if constexpr (LAMC) lamv(Ba[J3], lt);
     pass(IC<0>{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], LAMC ? lt : Bl[J3]);
-    TB2_STAMP(5, p);
+    TB2_STAMP(7, p);
     store(PT, p - 4, eadd(E0, -4));
-    TB2_STAMP(6, p);
+    TB2_STAMP(8, p);
   };
 
   fetch_u(1, pstart - 1, IC<0>{});

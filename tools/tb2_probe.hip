@@ -10,11 +10,14 @@
 #include <vector>
 
 #ifdef STAMPS
+#ifndef STAMP_T
+#define STAMP_T 0  // the stamping thread (lane 0 of wave STAMP_T / 64)
+#endif
 __device__ unsigned long long g_stamps[4][64][12];
 __device__ int g_probe_blocks[4];
 #define TB2_STAMP(id, p)                                                              \
   do {                                                                                \
-    if (threadIdx.x == 0) {                                                           \
+    if (threadIdx.x == STAMP_T) {                                                     \
       for (int w_ = 0; w_ < 4; ++w_)                                                  \
         if ((int)blockIdx.x == g_probe_blocks[w_] && (p) >= z0 + 40 && (p) < z0 + 104) \
           g_stamps[w_][(p) - z0 - 40][id] = __builtin_amdgcn_s_memtime();             \
@@ -94,7 +97,7 @@ int main(int argc, char **argv) {
   printf("{\"n\": %d, \"zin\": %d, \"ms_per_launch\": %.4f, \"compulsory_GBps\": %.1f}\n", n, zin,
          ms, (zin ? 24.0 : 32.0) * cells / (ms * 1e-3) / 1e9);
 #ifdef STAMPS
-  constexpr int kStamps = 7;  // TB2_STAMP ids 0..6 per step (smoother_tb.hip)
+  constexpr int kStamps = 9;  // TB2_STAMP ids 0..8 per step (smoother_tb.hip)
   static unsigned long long st[4][64][12];
   MGIC_HIP(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st)));
   for (int w = 0; w < 4; ++w) {
