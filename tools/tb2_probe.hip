@@ -5,6 +5,7 @@
 // breakdown).  Not part of the library; built by tools/build_probe.sh.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -29,13 +30,17 @@ __device__ int g_probe_blocks[4];
 // per-block progress: thread 0 stamps step p = z0 + 32k (k < 16) and the
 // tile origin, so the host can see how far neighbouring tiles drift apart
 __device__ unsigned long long g_drift[2048][16];
-__device__ int g_tile[2048][2];
+__device__ int g_tile[2048][4];  // x0, y0, z0, XCC the block ran on
 #define TB2_STAMP(id, p)                                                              \
   do {                                                                                \
     if (id == 0 && threadIdx.x == 0 && (p) >= z0 && (p) < z0 + 512 && (((p) - z0) & 31) == 0) { \
       g_drift[blockIdx.x][((p) - z0) >> 5] = __builtin_amdgcn_s_memrealtime();           \
+      unsigned xcc_;                                                                  \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_));       \
       g_tile[blockIdx.x][0] = x0;                                                     \
       g_tile[blockIdx.x][1] = y0;                                                     \
+      g_tile[blockIdx.x][2] = z0;                                                     \
+      g_tile[blockIdx.x][3] = (int)xcc_;                                              \
     }                                                                                 \
   } while (0)
 #endif
@@ -120,13 +125,33 @@ int main(int argc, char **argv) {
 #endif
 #ifdef DRIFT
   static unsigned long long dr[2048][16];
-  static int tl[2048][2];
+  static int tl[2048][4];
   MGIC_HIP(hipMemcpyFromSymbol(dr, HIP_SYMBOL(g_drift), sizeof(dr)));
   MGIC_HIP(hipMemcpyFromSymbol(tl, HIP_SYMBOL(g_tile), sizeof(tl)));
   // blocks of the last launch: those with a stamp at k = 0
   std::vector<int> bs;
   for (int b = 0; b < 2048; ++b)
     if (dr[b][0]) bs.push_back(b);
+  {  // where the blocks ran: XCC against blockIdx % 8, neighbours sharing an XCC
+    int same_rr = 0, xs = 0, xn = 0, ys = 0, yn = 0;
+    double xlag = 0, ylag = 0;
+    for (int b : bs) {
+      same_rr += tl[b][3] == b % 8;
+      for (int c : bs) {
+        if (tl[c][2] != tl[b][2]) continue;
+        const bool xnb = tl[c][1] == tl[b][1] && tl[c][0] == tl[b][0] + 64;
+        const bool ynb = tl[c][0] == tl[b][0] && tl[c][1] == tl[b][1] + 22;
+        const double st = fabs((double)dr[c][0] - (double)dr[b][0]);
+        if (xnb) { ++xn; xs += tl[c][3] == tl[b][3]; xlag += st; }
+        if (ynb) { ++yn; ys += tl[c][3] == tl[b][3]; ylag += st; }
+      }
+    }
+    printf("XCC == blockIdx %% 8 for %d of %zu blocks; x-neighbours on one XCC %d of %d (start lag %.0f x10ns), "
+           "y-neighbours %d of %d (start lag %.0f x10ns)\n",
+           same_rr, bs.size(), xs, xn, xn ? xlag / xn : 0.0, ys, yn, yn ? ylag / yn : 0.0);
+    for (int b = 0; b < 12 && b < (int)bs.size(); ++b)
+      printf("  block %d: tile (%d, %d, %d) XCC %d\n", bs[b], tl[bs[b]][0], tl[bs[b]][1], tl[bs[b]][2], tl[bs[b]][3]);
+  }
   {  // time over the first 128 steps, interior vs edge tiles
     double ti = 0, te = 0;
     int ni = 0, ne = 0;
@@ -148,7 +173,7 @@ int main(int argc, char **argv) {
       lo = dr[b][k] < lo ? dr[b][k] : lo;
       hi = dr[b][k] > hi ? dr[b][k] : hi;
       for (int c : bs)  // x neighbour (same y0, x0 + 64)
-        if (tl[c][1] == tl[b][1] && tl[c][0] == tl[b][0] + 64 && dr[c][k]) {
+        if (tl[c][2] == tl[b][2] && tl[c][1] == tl[b][1] && tl[c][0] == tl[b][0] + 64 && dr[c][k]) {
           nb += dr[c][k] > dr[b][k] ? (double)(dr[c][k] - dr[b][k]) : (double)(dr[b][k] - dr[c][k]);
           ++nn;
         }
