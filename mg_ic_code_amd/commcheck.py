@@ -22,32 +22,35 @@ def _value(k, j, i, n):
     return ((np.mod(k, n) * n + np.mod(j, n)) * n + np.mod(i, n)) + 1.0
 
 
-def check_transport(comm: Comm, world: int, n: int = 32) -> bool:
-    """True when one exchange and one reduction over `comm` give exactly the
-    expected values on this rank (the caller combines the ranks' answers)."""
+def check_transport(comm: Comm, world: int, n: int = 32, rounds: int = 4) -> bool:
+    """True when `rounds` exchanges (each of a different field, so a value
+    left over from an earlier round is caught) and one reduction over `comm`
+    give exactly the expected values on this rank (the caller combines the
+    ranks' answers)."""
     dom, boxes, owners = decompose((n, n, n), world)
     grid = Grid(comm, dom, boxes, 1.0, periodic=(1, 1, 1), owners=owners)
     f = LevelData(grid)
-    expect = []
-    for li in range(grid.num_local):
-        b = grid.local_box(li)
-        k, j, i = np.meshgrid(np.arange(b[2] - 1, b[5] + 2), np.arange(b[1] - 1, b[4] + 2),
-                              np.arange(b[0] - 1, b[3] + 2), indexing="ij")
-        want = _value(k, j, i, n)
-        full = np.full(want.shape, -1.0)
-        full[1:-1, 1:-1, 1:-1] = want[1:-1, 1:-1, 1:-1]
-        f.upload(li, full, with_ghosts=True)
-        expect.append(want)
-    f.exchange()
-    comm.synchronize()
     ok = True
-    for li, want in enumerate(expect):
-        g = f.download(li, with_ghosts=True)
-        for ax in range(3):  # the six face ghost layers (edges / corners are not exchanged)
-            for side in (0, -1):
-                sl = [slice(1, -1)] * 3
-                sl[ax] = side
-                ok &= bool(np.array_equal(g[tuple(sl)], want[tuple(sl)]))
+    for r in range(rounds):
+        expect = []
+        for li in range(grid.num_local):
+            b = grid.local_box(li)
+            k, j, i = np.meshgrid(np.arange(b[2] - 1, b[5] + 2), np.arange(b[1] - 1, b[4] + 2),
+                                  np.arange(b[0] - 1, b[3] + 2), indexing="ij")
+            want = _value(k, j, i, n) + r * float(n) ** 3
+            full = np.full(want.shape, -1.0)
+            full[1:-1, 1:-1, 1:-1] = want[1:-1, 1:-1, 1:-1]
+            f.upload(li, full, with_ghosts=True)
+            expect.append(want)
+        f.exchange()
+        comm.synchronize()
+        for li, want in enumerate(expect):
+            g = f.download(li, with_ghosts=True)
+            for ax in range(3):  # the six face ghost layers (edges / corners are not exchanged)
+                for side in (0, -1):
+                    sl = [slice(1, -1)] * 3
+                    sl[ax] = side
+                    ok &= bool(np.array_equal(g[tuple(sl)], want[tuple(sl)]))
     # a reduction across the ranks: every rank's cells hold rank + 1
     fr = LevelData(grid)
     fr.set_val(float(comm.rank + 1))
