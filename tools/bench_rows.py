@@ -8,7 +8,10 @@
      poisson_solve on an m^3 level (NL iterations to convergence or the cap).
 (f)3 AMR V-cycle: a 3-level hierarchy (a^3 base, then a^3-cell patches of the
      2a^3 and 4a^3 domains, properly nested, centred on the punctures), the
-     params.txt coefficients on every level; time per AMR iteration.
+     params.txt coefficients on every level; time per AMR iteration.  And the
+     NL loop over that hierarchy (poisson_solve with max_level = 2:
+     per-level coefficients, multilevel BiCGStab, QuadCFInterp of dpsi,
+     Main_PoissonSolver.cpp:129-220).
 
 Prints one JSON line.  usage: bench_rows.py [--n 512] [--m 256] [--amr 128]
 """
@@ -147,6 +150,27 @@ def main():
         "config": f"3 AMR levels: {a}^3 base + patches of {cells[1]} and {cells[2]} cells",
         "ms_per_iteration": round(t_amr * 1e3, 3), "cells_per_level": cells,
         "residual_max_norm": {"initial": hist[0], f"after_{args.amr_iters + 1}": hist[1]}}
+    del amr, phis, rhss, fields
+    grids = [lv[0] for lv in levels]
+    del levels
+    sync()
+    t0 = time.perf_counter()
+    status = "converged"
+    try:
+        res = poisson_solve(grids, prm, max_depth=2, bottom_solver=0,
+                            max_NL_iterations=args.nl_iters)
+        if not res.converged:
+            status = "truncated"
+    except NLDivergenceError as e:
+        res, status = e.result, "diverged or truncated above the 1e-1 threshold"
+    sync()
+    t_nl = time.perf_counter() - t0
+    out["f3_amr_nl_loop"] = {
+        "config": f"poisson_solve over the 3 AMR levels above (max_level = 2, params.txt)",
+        "status": status, "nl_iterations": len(res.dpsi_norms),
+        "linear_iterations": res.linear_iterations, "dpsi_norms": res.dpsi_norms,
+        "s_total": round(t_nl, 3),
+        "ms_per_nl_iteration": round(t_nl * 1e3 / max(1, len(res.dpsi_norms)), 1)}
     print(json.dumps(out), flush=True)
 
 
