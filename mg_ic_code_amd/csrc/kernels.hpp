@@ -75,17 +75,6 @@ void gsrb_sweep_tb2_res(double *e_out, double *r_out, const double *phi, const d
 void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
                       const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st);
 long gsrb_block_max_cells();
-// two red+black sweeps u_in -> u_out in one z-streaming launch (128x16
-// tiles, 6-plane LDS ring, coefficients carried in registers): boxes whose
-// six faces are domain faces, constant bCoef, above the block-kernel size
-bool gsrb_sweep_fused2s_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
-void gsrb_sweep_fused2s(double *u_out, const double *u_in, const double *rhs, const double *a,
-                        const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st);
-// two red+black sweeps u_in -> u_out in one launch (temporal blocking);
-// BC folded in-kernel, u_in is not modified (zero_in: not read either)
-void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,
-                        const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                        hipStream_t st);
 // VCCOMPUTEOP3D (.ChF:181-237)
 void apply_op(double *lu, const double *u, const double *a, const double *b,
               const BoxArgs &g, const StencilCoefs &s, hipStream_t st);

@@ -360,12 +360,12 @@ bool VariableCoeffPoissonOperator::fusedSmootherApplies() {
 
 // MGIC_SWEEPS_PER_LAUNCH: 2 (default) pairs consecutive sweeps in the
 // temporally blocked kernel (smoother_tb.hip) where it applies; 1 one sweep
-// per launch; 3 / 4 the round-1 two-sweep kernels (wide ring / 128x16
-// rings recomputing lambda per update; measurement only)
+// per launch.  (Round 1's two-sweep kernels, selected by 3 / 4, ran no faster
+// than the single sweep and were removed in round 3.)
 static int sweeps_per_launch() {
   static const int v = [] {
     const char *e = getenv("MGIC_SWEEPS_PER_LAUNCH");
-    return e ? std::max(1, std::min(4, atoi(e))) : 2;
+    return e ? std::max(1, std::min(2, atoi(e))) : 2;
   }();
   return v;
 }
@@ -514,12 +514,10 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   const int spl = sweeps_per_launch();
   bool two = (!halo || (deep_ok && spl == 2)) && !cfl && spl >= 2 && n >= 2;
   for (int b = 0; two && b < grid->nlocal(); ++b)
-    two = spl == 3 ||
-          (spl == 4 ? kern::gsrb_sweep_fused2s_applies(args_hom_[b], s, prm.fused_smoother)
-                    : kern::gsrb_sweep_tb2_applies(args_hom_[b], s, prm.fused_smoother));
+    two = kern::gsrb_sweep_tb2_applies(args_hom_[b], s, prm.fused_smoother);
   const int per = two ? 2 : 1;
-  // the new kernel takes the phi += e sweep too; the round-1 ones do not
-  const bool pair_acc = two && spl == 2;
+  // the pair also takes the phi += e sweep
+  const bool pair_acc = two;
   const bool want_out = halo && (flags & kHaloOut) && !acc;
   const bool overlap = halo && per == 1 && overlapApplies();
   const bool split = halo && per == 1 && !overlap && splitApplies();
@@ -613,13 +611,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
       // sweep+restriction launch moves other bytes)
       const long nc = last && restrict_last ? 0 : grid->geom[b].valid.ncells();
       prof_mark(st, nc, true, 2 * k);
-      if (k == 2 && spl == 3)
-        kern::gsrb_sweep_fused2x(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
-                                 args_hom_[b], s, zin, st);
-      else if (k == 2 && spl == 4)
-        kern::gsrb_sweep_fused2s(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], args_hom_[b], s,
-                                 zin, st);
-      else if (k == 2)  // two sweeps in one launch (temporal blocking), + phi += e
+      if (k == 2)  // two sweeps in one launch (temporal blocking), + phi += e
         kern::gsrb_sweep_tb2(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], args_hom_[b], s, zin,
                              last && acc ? acc->p[b] : nullptr, st);
       else if (last && restrict_last)  // + restrictResidual(rst, result, rhs)

@@ -1021,542 +1021,6 @@ __global__ __launch_bounds__(NT) void k_gsrb_fused_rst(double *__restrict__ uo,
   }
 }
 
-// ---- two sweeps per launch (temporal blocking) ---------------------------
-// The same streaming scheme carried two sweeps deep: at step p the workgroup
-// updates RED(sweep 1) on plane p, BLACK(1) on p-1, RED(2) on p-2 and
-// BLACK(2) on p-3, on rings of width 3, 2, 1, 0 around its tile, then stores
-// plane p-3.  Each plane lives in one LDS slot from its load until its final
-// store and is updated in place by the four stages (a colour pass reads only
-// the other colour, so in-place order inside a pass does not matter).
-// Compulsory traffic: 40 B/cell per TWO sweeps.  The domain BC is folded into
-// every update (a ghost is the BC image of the cell being updated, before its
-// update -- exactly the value ParseBC writes before each colour pass), so no
-// ghost fill is needed.  rhs/a/b: the pair of plane p+1 is loaded one step
-// ahead for stages 1-2 (kept in registers, as in the single sweep); stages
-// 3-4 reload their element from the cache hierarchy two / three steps later.
-template <int TX, int TY, int NT>
-struct Fused2x {
-  static_assert(TX % 2 == 0, "TX must be even");
-  static constexpr int PW = TX / 2 + 4;      // pairs per region row (x0-4 .. x0+TX+3)
-  static constexpr int LH = TY + 8;          // region rows y0-4 .. y0+TY+3
-  static constexpr int CP = PW * LH;         // pairs per plane
-  static constexpr int NRP = PW * (TY + 6);  // ring pairs (rows y0-3 .. y0+TY+2)
-  static constexpr int NL = (CP + NT - 1) / NT;
-  static constexpr int NP = (NRP + NT - 1) / NT;
-  static constexpr int S = 7;                // LDS ring planes p-5 .. p+1
-};
-
-template <int TX, int TY, int NT, bool ZIN, bool BC>
-__global__ __launch_bounds__(NT) void k_gsrb_fused2x(double *__restrict__ uo,
-                                                     const double *__restrict__ ui,
-                                                     const double *__restrict__ rhs,
-                                                     const double *__restrict__ a,
-                                                     const double *__restrict__ b,
-                                                     const BoxArgs g, const StencilCoefs s, int kc,
-                                                     int ntx, int nty, int nblocks) {
-  using F = Fused2x<TX, TY, NT>;
-  constexpr int PW = F::PW, CP = F::CP, NRP = F::NRP, NL = F::NL, NP = F::NP, S = F::S;
-  __shared__ double R[S * CP];  // red element of every pair
-  __shared__ double B[S * CP];  // black element
-
-  const int bid = blockIdx.x;  // XCD-aware: consecutive tiles on one XCD
-  const int q8 = nblocks / 8, r8 = nblocks % 8;
-  const int xcd = bid % 8, i8 = bid / 8;
-  const int L = xcd * q8 + min(xcd, r8) + i8;
-  const int tx_ = L % ntx, ty_ = (L / ntx) % nty, tz_ = L / (ntx * nty);
-  const int x0 = tx_ * TX, y0 = ty_ * TY;
-  const int z0 = tz_ * kc, z1 = min(z0 + kc, g.nz);
-  const int tid = threadIdx.x;
-  const long sy = g.sy, sz = g.sz;
-  const int nx = g.nx, ny = g.ny, nz = g.nz;
-  const int xpmax = nx & ~1;
-  const int q0 = (x0 + g.glo[0] + g.glo[1] + g.glo[2]) & 1;
-  auto slot = [](int p) { return ((p % S) + S) % S; };
-  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
-
-  long loff[NL];
-  int lgy[NL];
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int c = tid + i * NT;
-    const int r = c / PW, m = c - r * PW;
-    lgy[i] = y0 - 4 + r;
-    loff[i] = c < CP ? (long)min(x0 - 4 + 2 * m, xpmax) + (long)clampi(lgy[i], -1, ny) * sy : 0;
-  }
-  long roff[NP], rcoff[NP];
-  int rgy[NP], rgx0[NP], rci[NP], rok[NP], rtile[NP];
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int c = tid + i * NT;
-    const int rr = c / PW, m = c - rr * PW;
-    rgy[i] = y0 - 3 + rr;
-    rgx0[i] = x0 - 4 + 2 * m;
-    roff[i] = (long)rgx0[i] + (long)rgy[i] * sy;
-    rcoff[i] = c < NRP ? (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], -1, ny) * sy : 0;
-    rci[i] = (rr + 1) * PW + m;
-    rok[i] = c < NRP && rgy[i] >= 0 && rgy[i] < ny;
-    rtile[i] = rok[i] && rr >= 3 && rr <= TY + 2 && m >= 2 && m <= TX / 2 + 1 && rgx0[i] < nx;
-  }
-  // no cell this workgroup updates touches an x or y domain face
-  const bool xy_interior = x0 - 4 > 0 && x0 + TX + 3 < nx - 1 && y0 - 4 > 0 && y0 + TY + 3 < ny - 1;
-  // cell (gx, gy) is on the ring of width w around the tile, inside the box
-  auto on_ring = [&](int gx, int gy, int w) {
-    return gx >= max(x0 - w, 0) && gx <= min(x0 + TX - 1 + w, nx - 1) && gy >= max(y0 - w, 0) &&
-           gy <= min(y0 + TY - 1 + w, ny - 1);
-  };
-
-  double pu0[NL], pu1[NL];
-  double c0r0[NP], c0r1[NP], c0a0[NP], c0a1[NP], c0b0[NP], c0b1[NP];  // plane p (pairs)
-  double nr0[NP], nr1[NP], na0[NP], na1[NP], nb0[NP], nb1[NP];        // plane p+1 (loading)
-  double c1r[NP], c1a[NP], c1b[NP];  // black element, plane p-1 (stage 2)
-  double c3r[NP], c3a[NP], c3b[NP];  // red element, plane p-2 (stage 3)
-  double c4r[NP], c4a[NP], c4b[NP];  // black element, plane p-3 (stage 4)
-
-  auto fetch_u = [&](int p) {
-    const long pz = (long)clampi(p, -1, nz) * sz;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      if (ZIN) {  // the input is identically +0 (a freshly zeroed correction)
-        pu0[i] = 0.0;
-        pu1[i] = 0.0;
-      } else {
-        const double2 v = *reinterpret_cast<const double2 *>(ui + loff[i] + pz);
-        pu0[i] = v.x;
-        pu1[i] = v.y;
-      }
-    }
-  };
-  auto put_u = [&](int p) {
-    double *Rs = R + slot(p) * CP, *Bs = B + slot(p) * CP;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int c = tid + i * NT;
-      if (NL * NT > CP && c >= CP) continue;
-      const int q = (q0 + lgy[i] + p) & 1;  // 1: the red element is the second
-      Rs[c] = bsel(q, pu1[i], pu0[i]);
-      Bs[c] = bsel(q, pu0[i], pu1[i]);
-    }
-  };
-  auto fetch_c = [&](int p) {
-    const long pz = (long)clampi(p, 0, nz - 1) * sz;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const long off = rcoff[i] + pz;
-      const double2 vr = *reinterpret_cast<const double2 *>(rhs + off);
-      const double2 va = *reinterpret_cast<const double2 *>(a + off);
-      const double2 vb = BC ? make_double2(s.bval, s.bval)
-                            : *reinterpret_cast<const double2 *>(b + off);
-      nr0[i] = vr.x; nr1[i] = vr.y;
-      na0[i] = va.x; na1[i] = va.y;
-      nb0[i] = vb.x; nb1[i] = vb.y;
-    }
-  };
-  // the element of colour `black` (0 red, 1 black) of every ring pair, plane p
-  auto fetch_elem = [&](int p, int black, double *r, double *av, double *bv) {
-    const long pz = (long)clampi(p, 0, nz - 1) * sz;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int e = ((q0 + rgy[i] + p) & 1) ^ black;
-      const long off = rcoff[i] + pz + e;
-      r[i] = rhs[off];
-      av[i] = a[off];
-      bv[i] = BC ? s.bval : b[off];
-    }
-  };
-  auto upd = [&](double uc, double xm, double xp, double ym, double yp, double zm, double zp,
-                 double rv, double av, double bv, int gx, int gy, int p) -> double {
-    if (!xy_interior) {  // SetBCs.cpp:49-131 folded (workgroup-uniform branch)
-      if (gx == 0) xm = ghost_of(g.bcm[0], g.bcc[0], uc);
-      if (gx == nx - 1) xp = ghost_of(g.bcm[1], g.bcc[1], uc);
-      if (gy == 0) ym = ghost_of(g.bcm[2], g.bcc[2], uc);
-      if (gy == ny - 1) yp = ghost_of(g.bcm[3], g.bcc[3], uc);
-    }
-    if (p == 0) zm = ghost_of(g.bcm[4], g.bcc[4], uc);  // plane-uniform
-    if (p == nz - 1) zp = ghost_of(g.bcm[5], g.bcc[5], uc);
-    const double tx = (xp + xm) - 2.0 * uc;
-    const double ty = (yp + ym) - 2.0 * uc;
-    const double tz = (zp + zm) - 2.0 * uc;
-    const double lap = (tx + ty) + tz;                     // .ChF:111-120
-    double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
-    const double ldpsi = lap * s.dxinv * bv;               // .ChF:122
-    lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
-    const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
-    return uc - lam * (lofdpsi - rv);                      // .ChF:127-128
-  };
-  // one colour pass on plane p over the ring of width w; `red` selects the
-  // updated colour, coef(i, q) returns (rhs, a, b) of the updated element
-  auto pass_red = [&](int p, int w, const double *cr, const double *ca, const double *cb,
-                      bool from_pairs) {
-    double *Rs = R + slot(p) * CP;
-    const double *Bs = B + slot(p) * CP;
-    const double *Bm = B + slot(p - 1) * CP;
-    const double *Bp = B + slot(p + 1) * CP;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int q = (q0 + rgy[i] + p) & 1;
-      const int gx = rgx0[i] + q;
-      if (!rok[i] || !on_ring(gx, rgy[i], w)) continue;
-      const int ci = rci[i];
-      const double xm = q ? Bs[ci] : Bs[ci - 1];
-      const double xp = q ? Bs[ci + 1] : Bs[ci];
-      double rv, av, bv;
-      if (from_pairs) {
-        rv = bsel(q, c0r1[i], c0r0[i]);
-        av = bsel(q, c0a1[i], c0a0[i]);
-        bv = bsel(q, c0b1[i], c0b0[i]);
-      } else {
-        rv = cr[i];
-        av = ca[i];
-        bv = cb[i];
-      }
-      Rs[ci] = upd(Rs[ci], xm, xp, Bs[ci - PW], Bs[ci + PW], Bm[ci], Bp[ci], rv, av, bv, gx,
-                   rgy[i], p);
-    }
-  };
-  auto pass_black = [&](int k, int w, const double *cr, const double *ca, const double *cb) {
-    double *Bs = B + slot(k) * CP;
-    const double *Rs = R + slot(k) * CP;
-    const double *Rm = R + slot(k - 1) * CP;
-    const double *Rp = R + slot(k + 1) * CP;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int qb = 1 - ((q0 + rgy[i] + k) & 1);
-      const int gx = rgx0[i] + qb;
-      if (!rok[i] || !on_ring(gx, rgy[i], w)) continue;
-      const int ci = rci[i];
-      const double xm = qb ? Rs[ci] : Rs[ci - 1];
-      const double xp = qb ? Rs[ci + 1] : Rs[ci];
-      Bs[ci] = upd(Bs[ci], xm, xp, Rs[ci - PW], Rs[ci + PW], Rm[ci], Rp[ci], cr[i], ca[i], cb[i],
-                   gx, rgy[i], k);
-    }
-  };
-
-  fetch_u(z0 - 4);
-  put_u(z0 - 4);
-  fetch_u(z0 - 3);
-  put_u(z0 - 3);
-  fetch_u(z0 - 2);
-  fetch_c(z0 - 3);
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    c0r0[i] = nr0[i]; c0r1[i] = nr1[i];
-    c0a0[i] = na0[i]; c0a1[i] = na1[i];
-    c0b0[i] = nb0[i]; c0b1[i] = nb1[i];
-    c1r[i] = c1a[i] = c1b[i] = 0.0;
-  }
-  const int zlo = max(z0 - 3, 0), zhi = min(z1 + 2, nz - 1);  // stage-1 planes
-  for (int p = z0 - 3; p <= z1 + 2; ++p) {
-    put_u(p + 1);
-    fetch_u(p + 2);
-    fetch_c(p + 1);
-    fetch_elem(p - 2, 0, c3r, c3a, c3b);
-    fetch_elem(p - 3, 1, c4r, c4a, c4b);
-    __syncthreads();
-    if (p >= zlo && p <= zhi) pass_red(p, 3, nullptr, nullptr, nullptr, true);  // sweep 1 red
-    __syncthreads();
-    {
-      const int k = p - 1;  // sweep 1 black
-      if (k >= max(z0 - 2, 0) && k <= min(z1 + 1, nz - 1)) pass_black(k, 2, c1r, c1a, c1b);
-    }
-    __syncthreads();
-    {
-      const int k = p - 2;  // sweep 2 red
-      if (k >= max(z0 - 1, 0) && k <= min(z1, nz - 1)) pass_red(k, 1, c3r, c3a, c3b, false);
-    }
-    __syncthreads();
-    const int k = p - 3;  // sweep 2 black on the tile + store
-    if (k >= z0 && k < z1) {
-      double *Bs = B + slot(k) * CP;
-      const double *Rs = R + slot(k) * CP;
-      const double *Rm = R + slot(k - 1) * CP;
-      const double *Rp = R + slot(k + 1) * CP;
-      double *dst = uo + (long)k * sz;
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        if (!rtile[i]) continue;
-        const int qb = 1 - ((q0 + rgy[i] + k) & 1);
-        const int gx = rgx0[i] + qb;
-        const int ci = rci[i];
-        const double red = Rs[ci];
-        double blk = Bs[ci];
-        if (gx < nx) {
-          const double xm = qb ? Rs[ci] : Rs[ci - 1];
-          const double xp = qb ? Rs[ci + 1] : Rs[ci];
-          blk = upd(blk, xm, xp, Rs[ci - PW], Rs[ci + PW], Rm[ci], Rp[ci], c4r[i], c4a[i],
-                    c4b[i], gx, rgy[i], k);
-        }
-        if (rgx0[i] + 1 < nx) {
-          double2 w;
-          w.x = bsel(qb, red, blk);
-          w.y = bsel(qb, blk, red);
-          *reinterpret_cast<double2 *>(dst + roff[i]) = w;
-        } else {
-          dst[roff[i]] = bsel(qb, red, blk);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {  // plane p's black coefficients: stage 2, next step
-      const int qb = 1 - ((q0 + rgy[i] + p) & 1);
-      c1r[i] = bsel(qb, c0r1[i], c0r0[i]);
-      c1a[i] = bsel(qb, c0a1[i], c0a0[i]);
-      c1b[i] = bsel(qb, c0b1[i], c0b0[i]);
-      c0r0[i] = nr0[i]; c0r1[i] = nr1[i];
-      c0a0[i] = na0[i]; c0a1[i] = na1[i];
-      c0b0[i] = nb0[i]; c0b1[i] = nb1[i];
-    }
-  }
-}
-
-
-// ---- two sweeps per launch, z-streaming (temporal blocking) --------------
-// k_gsrb_fused6's scheme carried two sweeps deep on a 128 x 16 tile: at step
-// p a workgroup updates RED(sweep 1) on plane p over the tile grown by 3,
-// BLACK(1) on plane p-1 grown by 2, RED(2) on plane p-2 grown by 1 and
-// BLACK(2) on plane p-3 over the tile, then stores plane p-3.  Each plane
-// lives in one slot of a 6-plane LDS ring (red / black split as in fused6)
-// from its load until its store and is updated in place by the four stages
-// (a colour pass reads only the other colour).  rhs/a pairs are loaded once,
-// one step ahead, and the element each later stage needs is kept in
-// registers (no reloads).  The domain BC is folded into each update (a ghost
-// is the image of the cell being updated, before its update -- the value
-// ParseBC writes before each colour pass); only tiles reaching a face pay.
-// Boxes whose six faces are domain faces, bCoef one value (bval).
-// Compulsory traffic: 32 B/cell per TWO sweeps (u, rhs, a in, u out).
-template <int TX, int TY, int NT>
-struct F2S {
-  static_assert(TX % 2 == 0, "TX must be even");
-  static constexpr int PW = TX / 2 + 4;      // pairs per region row (x0-4 .. x0+TX+3)
-  static constexpr int LH = TY + 8;          // region rows y0-4 .. y0+TY+3
-  static constexpr int CP = PW * LH;         // pairs per plane
-  static constexpr int NS = 6;               // LDS ring planes p-4 .. p+1
-  static constexpr int NRP = PW * (TY + 6);  // update pairs: rows y0-3 .. y0+TY+2
-  static constexpr int NL = (CP + NT - 1) / NT;
-  static constexpr int NP = (NRP + NT - 1) / NT;
-};
-
-template <int TX, int TY, int NT, bool ZIN>
-__global__ __launch_bounds__(NT) void k_gsrb_fused2s(double *__restrict__ uo,
-                                                     const double *__restrict__ ui,
-                                                     const double *__restrict__ rhs,
-                                                     const double *__restrict__ a,
-                                                     const BoxArgs g, const StencilCoefs s, int kc,
-                                                     int ntx, int nty, int nblocks) {
-  using F = F2S<TX, TY, NT>;
-  constexpr int PW = F::PW, CP = F::CP, NS = F::NS, NRP = F::NRP, NL = F::NL, NP = F::NP;
-  __shared__ double R[NS * CP];  // red element of every pair
-  __shared__ double B[NS * CP];  // black element
-  const int bid = blockIdx.x;    // XCD-aware tile order, as k_gsrb_fused6
-  const int q8 = nblocks / 8, r8 = nblocks % 8;
-  const int L = (bid % 8) * q8 + min(bid % 8, r8) + bid / 8;
-  const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
-  const int z0 = (L / (ntx * nty)) * kc, z1 = min(z0 + kc, g.nz);
-  const int tid = threadIdx.x;
-  const long sy = g.sy, sz = g.sz;
-  const int nx = g.nx, ny = g.ny, nz = g.nz;
-  const int xpmax = (nx + 2) & ~1;  // last pair start inside the padded row (x <= nx + 3)
-  const int q0 = (x0 + g.glo[0] + g.glo[1] + g.glo[2]) & 1;
-  auto slot = [](int p) { return ((p % NS) + NS) % NS; };
-  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
-
-  long loff[NL];
-  int lgy[NL];
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    const int c = tid + i * NT;
-    const int r = c / PW, m = c - r * PW;
-    lgy[i] = y0 - 4 + r;
-    loff[i] = c < CP ? (long)min(x0 - 4 + 2 * m, xpmax) + (long)clampi(lgy[i], -4, ny + 3) * sy : 0;
-  }
-  // update pairs: ring level of each element (0 tile, 1..3 the rings, 99 off
-  // the box or no pair), BC-face flags, LDS index, store offset
-  long rcoff[NP], roff[NP];
-  int rgy[NP], rgx0[NP], rci[NP], rw[NP], rbc[NP];
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int c = tid + i * NT;
-    const int rr = c / PW, m = c - rr * PW;
-    rgy[i] = y0 - 3 + rr;
-    rgx0[i] = x0 - 4 + 2 * m;
-    rci[i] = c < NRP ? (rr + 1) * PW + m : PW + 1;  // padding slots read a valid cell
-    roff[i] = (long)rgx0[i] + (long)rgy[i] * sy;
-    rcoff[i] = c < NRP ? (long)min(rgx0[i], xpmax) + (long)clampi(rgy[i], -4, ny + 3) * sy : 0;
-    const int gy = rgy[i];
-    const int dy = gy < 0 || gy >= ny ? 99 : (gy < y0 ? y0 - gy : (gy >= y0 + TY ? gy - (y0 + TY - 1) : 0));
-    int w2 = 0, f2 = 0;
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int gx = rgx0[i] + e;
-      const int dx = gx < 0 || gx >= nx ? 99 : (gx < x0 ? x0 - gx : (gx >= x0 + TX ? gx - (x0 + TX - 1) : 0));
-      const int w = c < NRP ? max(dx, dy) : 99;
-      w2 |= (w > 15 ? 15 : w) << (4 * e);
-      f2 |= ((gx == 0) | ((gx == nx - 1) << 1) | ((gy == 0) << 2) | ((gy == ny - 1) << 3)) << (4 * e);
-    }
-    rw[i] = w2;
-    rbc[i] = f2;
-  }
-  // does any cell this workgroup updates touch an x / y domain face?
-  const bool edge = x0 - 3 <= 0 || x0 + TX + 2 >= nx - 1 || y0 - 3 <= 0 || y0 + TY + 2 >= ny - 1;
-
-  double pu0[NL], pu1[NL];
-  double nr0[NP], nr1[NP], na0[NP], na1[NP];  // pairs of plane p+1 (in flight)
-  double cr0[NP], cr1[NP], ca0[NP], ca1[NP];  // pairs of plane p
-  double k1r[NP], k1a[NP], k1R[NP], k1A[NP];  // plane p-1: black element, red element
-  double k2r[NP], k2a[NP], k2R[NP], k2A[NP];  // plane p-2: black element, red element
-  double k3r[NP], k3a[NP];                    // plane p-3: black element
-
-  auto fetch_u = [&](int p) {
-    const long pz = (long)clampi(p, -4, nz + 3) * sz;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      if (ZIN) {
-        pu0[i] = 0.0;
-        pu1[i] = 0.0;
-      } else {
-        const double2 v = *reinterpret_cast<const double2 *>(ui + loff[i] + pz);
-        pu0[i] = v.x;
-        pu1[i] = v.y;
-      }
-    }
-  };
-  // a plane enters the ring in two halves: its slot's previous plane (p-6)
-  // is read as R by the last stage of the previous step, so the R half is
-  // written only after the step's first barrier
-  auto put_half = [&](int p, bool red) {
-    double *Xs = (red ? R : B) + slot(p) * CP;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int c = tid + i * NT;
-      if (NL * NT > CP && c >= CP) continue;
-      const int q = (q0 + lgy[i] + p) & 1;  // 1: the red element is the second
-      Xs[c] = red ? bsel(q, pu1[i], pu0[i]) : bsel(q, pu0[i], pu1[i]);
-    }
-  };
-  auto put_u = [&](int p) {
-    put_half(p, true);
-    put_half(p, false);
-  };
-  auto fetch_c = [&](int p) {
-    const long pz = (long)clampi(p, -4, nz + 3) * sz;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const double2 vr = *reinterpret_cast<const double2 *>(rhs + rcoff[i] + pz);
-      const double2 va = *reinterpret_cast<const double2 *>(a + rcoff[i] + pz);
-      nr0[i] = vr.x; nr1[i] = vr.y;
-      na0[i] = va.x; na1[i] = va.y;
-    }
-  };
-  // one colour pass on plane p over the ring of width w: RED updates the red
-  // element of every pair from the black neighbours, BLACK the converse
-  auto stage = [&](bool red, int p, int w, const double *cr, const double *ca) {
-    double *Xs = (red ? R : B) + slot(p) * CP;
-    const double *Ns = (red ? B : R) + slot(p) * CP;
-    const double *Nm = (red ? B : R) + slot(p - 1) * CP;
-    const double *Np = (red ? B : R) + slot(p + 1) * CP;
-    const bool zlo = p == 0, zhi = p == nz - 1;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int q = (q0 + rgy[i] + p) & 1;
-      const int e = red ? q : 1 - q;  // element updated: 1 = the second of the pair
-      const int sh = 4 * e;
-      if (((rw[i] >> sh) & 15) > w) continue;
-      const int ci = rci[i];
-      const double uc = Xs[ci];
-      double xm = e ? Ns[ci] : Ns[ci - 1];
-      double xp = e ? Ns[ci + 1] : Ns[ci];
-      double ym = Ns[ci - PW], yp = Ns[ci + PW], zm = Nm[ci], zp = Np[ci];
-      if (edge) {  // SetBCs.cpp:49-131 folded: ghost = image of uc
-        const int f = rbc[i] >> sh;
-        if (f & 1) xm = ghost_of(g.bcm[0], g.bcc[0], uc);
-        if (f & 2) xp = ghost_of(g.bcm[1], g.bcc[1], uc);
-        if (f & 4) ym = ghost_of(g.bcm[2], g.bcc[2], uc);
-        if (f & 8) yp = ghost_of(g.bcm[3], g.bcc[3], uc);
-      }
-      if (zlo) zm = ghost_of(g.bcm[4], g.bcc[4], uc);
-      if (zhi) zp = ghost_of(g.bcm[5], g.bcc[5], uc);
-      const double av = ca[i];
-      const double tx = (xp + xm) - 2.0 * uc;
-      const double ty = (yp + ym) - 2.0 * uc;
-      const double tz = (zp + zm) - 2.0 * uc;
-      const double lap = (tx + ty) + tz;                     // .ChF:111-120
-      double lofdpsi = s.alpha * av * uc;                    // .ChF:107-108
-      const double ldpsi = lap * s.dxinv * s.bval;           // .ChF:122
-      lofdpsi = lofdpsi - s.beta * ldpsi;                    // .ChF:124
-      const double lam = 1.0 / (av * s.alpha + s.lamshift);  // .cpp:234-243
-      Xs[ci] = uc - lam * (lofdpsi - cr[i]);                 // .ChF:127-128
-    }
-  };
-
-  fetch_u(z0 - 4);
-  put_u(z0 - 4);
-  fetch_u(z0 - 3);
-  put_u(z0 - 3);
-  fetch_u(z0 - 2);
-  fetch_c(z0 - 3);
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    cr0[i] = nr0[i]; cr1[i] = nr1[i];
-    ca0[i] = na0[i]; ca1[i] = na1[i];
-    k1r[i] = k1a[i] = k1R[i] = k1A[i] = 0.0;
-    k2r[i] = k2a[i] = k2R[i] = k2A[i] = 0.0;
-    k3r[i] = k3a[i] = 0.0;
-  }
-  for (int p = z0 - 3; p <= z1 + 2; ++p) {
-    put_half(p + 1, false);
-    fetch_c(p + 1);
-    double er[NP], ea[NP];  // red element of plane p
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int q = (q0 + rgy[i] + p) & 1;
-      er[i] = bsel(q, cr1[i], cr0[i]);
-      ea[i] = bsel(q, ca1[i], ca0[i]);
-    }
-    __syncthreads();
-    put_half(p + 1, true);  // R of plane p+1 is first read next step
-    fetch_u(p + 2);
-    if (p >= max(z0 - 3, 0) && p <= min(z1 + 2, nz - 1)) stage(true, p, 3, er, ea);
-    __syncthreads();
-    if (p - 1 >= max(z0 - 2, 0) && p - 1 <= min(z1 + 1, nz - 1)) stage(false, p - 1, 2, k1r, k1a);
-    __syncthreads();
-    if (p - 2 >= max(z0 - 1, 0) && p - 2 <= min(z1, nz - 1)) stage(true, p - 2, 1, k2R, k2A);
-    __syncthreads();
-    const int k = p - 3;
-    if (k >= z0 && k < z1) {  // BLACK(2) on the tile, then store plane k
-      stage(false, k, 0, k3r, k3a);
-      // each thread stores the pairs it updated (its own LDS writes: no barrier)
-      const double *Rs = R + slot(k) * CP, *Bs = B + slot(k) * CP;
-      double *dst = uo + (long)k * sz;
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int gy = rgy[i];
-        if (gy < y0 || gy >= y0 + TY || gy >= ny || rgx0[i] < x0 || rgx0[i] >= x0 + TX ||
-            rgx0[i] >= nx || tid + i * NT >= NRP)
-          continue;
-        const int qb = 1 - ((q0 + gy + k) & 1);  // 1: the black element is the second
-        const double red = Rs[rci[i]], blk = Bs[rci[i]];
-        double2 w;
-        w.x = bsel(qb, red, blk);
-        w.y = bsel(qb, blk, red);
-        if (rgx0[i] + 1 < nx) *reinterpret_cast<double2 *>(dst + roff[i]) = w;
-        else dst[roff[i]] = w.x;
-      }
-    }
-    // the elements later stages need move down one plane
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int qb = 1 - ((q0 + rgy[i] + p) & 1);
-      k3r[i] = k2r[i]; k3a[i] = k2a[i];
-      k2r[i] = k1r[i]; k2a[i] = k1a[i];
-      k2R[i] = k1R[i]; k2A[i] = k1A[i];
-      k1r[i] = bsel(qb, cr1[i], cr0[i]);
-      k1a[i] = bsel(qb, ca1[i], ca0[i]);
-      k1R[i] = er[i];
-      k1A[i] = ea[i];
-      cr0[i] = nr0[i]; cr1[i] = nr1[i];
-      ca0[i] = na0[i]; ca1[i] = na1[i];
-    }
-  }
-}
 }  // namespace
 
 // workgroups of kernel `k` the whole device holds at once
@@ -1629,89 +1093,7 @@ static void launch_fused6(T *u_out, T *u_in, const T *rhs, const T *a, const T *
   if (e != hipSuccess) throw Error(kHipErr, std::string("fused sweep launch: ") + hipGetErrorString(e));
 }
 
-template <int TX, int TY, int NT>
-static void launch_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,
-                           const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                           hipStream_t st) {
-  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
-  static const int slots = resident_slots(k_gsrb_fused2x<TX, TY, NT, false, false>, NT);
-  const int kc = choose_kc(ntx * nty, g.nz, slots, 7);
-  const int ntz = (g.nz + kc - 1) / kc;
-  const int nblocks = ntx * nty * ntz;
-  const dim3 grid((unsigned)nblocks), block(NT);
-  if (zero_in && s.bconst)
-    k_gsrb_fused2x<TX, TY, NT, true, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
-                                                                   kc, ntx, nty, nblocks);
-  else if (zero_in)
-    k_gsrb_fused2x<TX, TY, NT, true, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
-                                                                    kc, ntx, nty, nblocks);
-  else if (s.bconst)
-    k_gsrb_fused2x<TX, TY, NT, false, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s,
-                                                                    kc, ntx, nty, nblocks);
-  else
-    k_gsrb_fused2x<TX, TY, NT, false, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g,
-                                                                     s, kc, ntx, nty, nblocks);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw Error(kHipErr, std::string("fused sweep launch: ") + hipGetErrorString(e));
-}
-
-static int fused2x_variant() {
-  static int v = [] {
-    const char *e = getenv("MGIC_FUSED2X_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 static long block_max_cells();
-
-template <int TX, int TY, int NT>
-static void launch_fused2s(double *u_out, const double *u_in, const double *rhs, const double *a,
-                           const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st) {
-  const int ntx = (g.nx + TX - 1) / TX, nty = (g.ny + TY - 1) / TY;
-  static const int slots = resident_slots(k_gsrb_fused2s<TX, TY, NT, false>, NT);
-  const int kc = choose_kc(ntx * nty, g.nz, slots, 6);
-  const int ntz = (g.nz + kc - 1) / kc;
-  const int nblocks = ntx * nty * ntz;
-  const dim3 grid((unsigned)nblocks), block(NT);
-  if (zero_in)
-    k_gsrb_fused2s<TX, TY, NT, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, g, s, kc, ntx,
-                                                             nty, nblocks);
-  else
-    k_gsrb_fused2s<TX, TY, NT, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, g, s, kc, ntx,
-                                                              nty, nblocks);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw Error(kHipErr, std::string("two-sweep launch: ") + hipGetErrorString(e));
-}
-
-bool gsrb_sweep_fused2s_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
-  static const int enabled = [] {
-    const char *e = getenv("MGIC_TWO_SWEEPS");
-    return e ? atoi(e) : 1;
-  }();
-  if (!enabled || !s.bconst) return false;
-  for (int f = 0; f < 6; ++f)
-    if (!g.bcm[f]) return false;  // exchanged faces would need a 4-deep shell
-  if (kind == 0 || kind == 3) return false;
-  return kind == 2 || (long)g.nx * g.ny * g.nz > block_max_cells();  // z-streaming territory
-}
-
-void gsrb_sweep_fused2s(double *u_out, const double *u_in, const double *rhs, const double *a,
-                        const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st) {
-  launch_fused2s<128, 16, 512>(u_out, u_in, rhs, a, g, s, zero_in, st);
-}
-
-void gsrb_sweep_fused2x(double *u_out, const double *u_in, const double *rhs, const double *a,
-                        const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                        hipStream_t st) {
-  switch (fused2x_variant()) {
-    case 1: launch_fused2x<56, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 2: launch_fused2x<120, 12, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 3: launch_fused2x<128, 12, 768>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    case 4: launch_fused2x<120, 12, 1024>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-    default: launch_fused2x<56, 8, 512>(u_out, u_in, rhs, a, b, g, s, zero_in, st); break;
-  }
-}
 
 // tile shape, for measurement (MGIC_FUSED_VARIANT): 0 = 128x16 / 512 threads
 // (default: one 106 KB workgroup per CU, 1 KB contiguous rows, u halo 1.29x,

@@ -723,13 +723,14 @@ print("two-sweep OK")
 """
 
 
-@pytest.mark.parametrize("spl,variant", [("4", "0"), ("2", "0"), ("2", "1")])
+@pytest.mark.parametrize("spl,variant", [("1", "0"), ("2", "0"), ("2", "1")])
 def test_two_sweep_kernel_vcycle_bitwise(spl, variant):
-    # the two-sweep kernels (MGIC_SWEEPS_PER_LAUNCH, read once per process: a
-    # child process): 4 = round 1's 128x16 kernel, 2 = smoother_tb.hip (the
-    # default; MGIC_TB2_VARIANT 1 = its 512-thread form with two pairs per
-    # lane, where whole waves never skip a pass); odd and even sweep counts,
-    # ragged mixed-BC box and a cube, against the oracle bit for bit
+    # the two-sweep kernel and its alternatives (MGIC_SWEEPS_PER_LAUNCH, read
+    # once per process: a child process): 2 = smoother_tb.hip (the default;
+    # MGIC_TB2_VARIANT 1 = its 512-thread form with two pairs per lane, where
+    # whole waves never skip a pass), 1 = one sweep per launch throughout;
+    # odd and even sweep counts, ragged mixed-BC box and a cube, against the
+    # oracle bit for bit
     import os
     import subprocess
     import sys

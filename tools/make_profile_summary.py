@@ -82,7 +82,7 @@ def main():
     fb = sum(fetch[k]["FETCH_SIZE"]) / len(fetch[k]["FETCH_SIZE"]) * 1024 * 2
     wb = sum(write[k]["WRITE_SIZE"]) / len(write[k]["WRITE_SIZE"]) * 1024
     # the key bench.py looks up: colour passes per launch of that kernel
-    kind = ("fused2x" if "tb2" in k[0] or "fused2s" in k[0] else
+    kind = ("fused2x" if "tb2" in k[0] else
             "fused" if "fused" in k[0] or "block" in k[0] else "pass")
     out_path = os.path.join(ROOT, "profiles", "traffic_smoother.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
