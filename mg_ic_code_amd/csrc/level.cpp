@@ -63,15 +63,31 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
       hipIpcMemHandle_t sig, arena;
       unsigned long long arena_bytes;
       int rank;
+      int pci[3];  // domain, bus, device of this rank's GPU
     } mine{}, *all = nullptr;
     MGIC_HIP(hipIpcGetMemHandle(&mine.sig, sig_));
     MGIC_HIP(hipIpcGetMemHandle(&mine.arena, arena_));
     mine.arena_bytes = arena_bytes_;
     mine.rank = rank;
+    {
+      int dev = 0;
+      MGIC_HIP(hipGetDevice(&dev));
+      MGIC_HIP(hipDeviceGetAttribute(&mine.pci[0], hipDeviceAttributePciDomainID, dev));
+      MGIC_HIP(hipDeviceGetAttribute(&mine.pci[1], hipDeviceAttributePciBusId, dev));
+      MGIC_HIP(hipDeviceGetAttribute(&mine.pci[2], hipDeviceAttributePciDeviceId, dev));
+    }
     std::vector<Rec> recs(size);
     all = recs.data();
     if (allgather(&mine, sizeof(Rec), all, user) != 0)
       throw Error(kState, "peer-mapped transport: host allgather failed");
+    // ranks sharing this GPU (one-GPU rehearsals): cap the exchange grids so
+    // that every such rank's exchange blocks fit on the device at once
+    int colocated = 0;
+    for (int r = 0; r < size; ++r)
+      colocated += recs[r].pci[0] == mine.pci[0] && recs[r].pci[1] == mine.pci[1] &&
+                   recs[r].pci[2] == mine.pci[2];
+    const char *ce = getenv("MGIC_IPC_GRID_CAP");
+    grid_cap_ = ce ? atoi(ce) : (colocated > 1 ? std::max(8, 256 / (2 * colocated)) : 0);
     for (int r = 0; r < size; ++r) {
       MGIC_CHECK(recs[r].rank == r && recs[r].arena_bytes == arena_bytes_,
                  "peer-mapped transport: ranks disagree on the setup");
@@ -522,10 +538,12 @@ void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hip
                   &pget.count[q]);
   if constexpr (std::is_same<T, double>::value)
     kern::ipc_exchange(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
-                       n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget, st);
+                       n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget,
+                       comm.ipc_grid_cap(), st);
   else
     kern::ipc_exchange_f(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
-                         n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget, st);
+                         n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget,
+                         comm.ipc_grid_cap(), st);
 }
 
 void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_tab,

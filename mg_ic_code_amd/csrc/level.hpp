@@ -75,6 +75,9 @@ class Comm {
 
   // ---- peer-mapped transport (transport.hpp)
   size_t ipc_arena_bytes() const { return arena_bytes_; }
+  // workgroup cap of one exchange launch: 0 (none) unless ranks share a GPU
+  // (MGIC_IPC_GRID_CAP overrides)
+  int ipc_grid_cap() const { return grid_cap_; }
   // my next message to `peer` (nblocks put blocks): its slot in the peer's
   // arena, the acknowledgement count to wait for (the slot's previous
   // message consumed) and the peer's counter my blocks add to
@@ -106,6 +109,7 @@ class Comm {
   double *d_result_ = nullptr;
   double *h_result_ = nullptr;
   bool ipc_ = false;
+  int grid_cap_ = 0;
   unsigned long long *sig_ = nullptr;            // my signal page (uncached)
   char *arena_ = nullptr;                        // my receive arena: size x 2 x arena_bytes_
   size_t arena_bytes_ = 0;

@@ -219,27 +219,35 @@ __device__ __forceinline__ void local_share(const CopyItem &it, int sub, T *cons
                   [&](unsigned t, T v) { dst[rd.at(t, 1)] = v; });
 }
 
-// one exchange in one launch: blocks [0, npu) put my messages (first, so the
-// peers can start), [npu, npu + nlo) copy the same-rank regions, the rest get
-// my messages.  Blocks are dispatched in index order, so a get block that
-// waits on this launch's own put blocks (self messages) never holds back a
-// put block that has not started.
+// one exchange in one launch: virtual blocks [0, npu) put my messages (first,
+// so the peers can start), [npu, npu + nlo) copy the same-rank regions, the
+// rest get my messages.  Without a cap every virtual block is a workgroup,
+// dispatched in index order, so a get block that waits on this launch's own
+// put blocks (self messages) never holds back a put block that has not
+// started.  With a cap (ranks sharing one device, Comm::ipc_grid_cap) the
+// workgroups stride over the virtual blocks in ascending order: a workgroup
+// has done all its puts before its first get, and the capped grids of every
+// rank on the device fit on it at once beside the other ranks' kernels, so a
+// rank's get blocks cannot hold the CU slots its peers' put blocks need.
 template <class T>
 __global__ __launch_bounds__(256) void k_exchange(const CopyItem *__restrict__ put_items,
                                                   const CopyItem *__restrict__ loc_items,
                                                   const CopyItem *__restrict__ get_items,
                                                   const IpcBlock *__restrict__ blocks, int npu,
-                                                  int nlo, T *const *__restrict__ src_tab,
+                                                  int nlo, int nall, T *const *__restrict__ src_tab,
                                                   T *const *__restrict__ dst_tab,
                                                   const IpcPeers pput, const IpcPeers pget) {
   __shared__ int ok;
-  const IpcBlock b = blocks[blockIdx.x];
-  if ((int)blockIdx.x < npu)
-    put_share<T>(put_items[b.item], b.sub, src_tab, pput, ok);
-  else if ((int)blockIdx.x < npu + nlo)
-    local_share<T>(loc_items[b.item], b.sub, src_tab, dst_tab);
-  else
-    get_share<T>(get_items[b.item], b.sub, dst_tab, pget, ok);
+  for (int v = blockIdx.x; v < nall; v += gridDim.x) {  // (uniform per workgroup)
+    const IpcBlock b = blocks[v];
+    if (v < npu)
+      put_share<T>(put_items[b.item], b.sub, src_tab, pput, ok);
+    else if (v < npu + nlo)
+      local_share<T>(loc_items[b.item], b.sub, src_tab, dst_tab);
+    else
+      get_share<T>(get_items[b.item], b.sub, dst_tab, pget, ok);
+    __syncthreads();  // (ok is rewritten by the next virtual block)
+  }
 }
 
 __global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned long long *err) {
@@ -275,27 +283,28 @@ template <class T>
 static void exchange_t(const CopyItem *put_items, const CopyItem *loc_items,
                        const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
                        T *const *src_tab, T *const *dst_tab, const IpcPeers &pput,
-                       const IpcPeers &pget, hipStream_t st) {
+                       const IpcPeers &pget, int grid_cap, hipStream_t st) {
   const int n = npu + nlo + nge;
   if (n <= 0) return;
-  k_exchange<T><<<dim3((unsigned)n), dim3(256), 0, st>>>(put_items, loc_items, get_items, blocks,
-                                                         npu, nlo, src_tab, dst_tab, pput, pget);
+  const int g = grid_cap > 0 && grid_cap < n ? grid_cap : n;
+  k_exchange<T><<<dim3((unsigned)g), dim3(256), 0, st>>>(put_items, loc_items, get_items, blocks,
+                                                         npu, nlo, n, src_tab, dst_tab, pput, pget);
   check_launch();
 }
 
 void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
                   const IpcBlock *blocks, int npu, int nlo, int nge, double *const *src_tab,
                   double *const *dst_tab, const IpcPeers &pput, const IpcPeers &pget,
-                  hipStream_t st) {
+                  int grid_cap, hipStream_t st) {
   exchange_t<double>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
-                     pput, pget, st);
+                     pput, pget, grid_cap, st);
 }
 void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
                     const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
                     float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
-                    const IpcPeers &pget, hipStream_t st) {
+                    const IpcPeers &pget, int grid_cap, hipStream_t st) {
   exchange_t<float>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
-                    pput, pget, st);
+                    pput, pget, grid_cap, st);
 }
 
 void ipc_allreduce(double *val, int op, const IpcReduce &r, unsigned long long *err,

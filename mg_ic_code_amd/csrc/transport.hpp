@@ -68,14 +68,16 @@ struct IpcReduce {
 // index in pput), then nlo same-rank copy blocks (loc_items), then nge get
 // blocks (items: dst = local box, soff = offset in the sender's message, pad =
 // peer index in pget).  Every item is split into ipc_blocks(cells) blocks.
+// grid_cap > 0: at most that many workgroups, striding over the blocks (ranks
+// that share a device; see k_exchange).
 void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
                   const IpcBlock *blocks, int npu, int nlo, int nge, double *const *src_tab,
                   double *const *dst_tab, const IpcPeers &pput, const IpcPeers &pget,
-                  hipStream_t st);
+                  int grid_cap, hipStream_t st);
 void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
                     const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
                     float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
-                    const IpcPeers &pget, hipStream_t st);
+                    const IpcPeers &pget, int grid_cap, hipStream_t st);
 // in-place allreduce of one device double over all ranks (op 0 sum, 1 max),
 // reduced in rank order on every rank (identical results everywhere)
 void ipc_allreduce(double *val, int op, const IpcReduce &r, unsigned long long *err,
