@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_COPY_GBS = 6290.0  # measured float4 copy rate (MI355X_MICROARCH.md: ≈6.3 TB/s achievable)
 
 
 def parse():
@@ -226,15 +227,23 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": hb,
                 "traffic_GBps": round(hb / (avg_launch_ms * 1e-3) / 1e9, 1) if hb and launches else None,
+                # the guide's measured float4 copy rate: what the memory
+                # system delivers in practice, beside the 8 TB/s spec peak
+                "copy_rate_GBps": HBM_COPY_GBS,
+                "traffic_frac_of_copy_rate": (round(hb / (avg_launch_ms * 1e-3) / 1e9 / HBM_COPY_GBS, 4)
+                                              if hb and launches else None),
                 "traffic_detail": traffic,
                 "algorithmic_bytes_per_launch": compulsory,
                 "effective_GBps": round(effective, 1) if effective else None,
                 "note": "achieved/frac = algorithmic bytes per launch (32 B/cell: u, rhs, aCoef in, "
                         "u out, once per launch whatever its colour passes) / average launch time; "
                         "effective_GBps = SURVEY 8(d)'s 48 B/cell/colour-pass credit over the same "
-                        "time (exceeds the peak once a launch fuses passes); traffic = HBM bytes per "
-                        "fine-level smoother launch from two rocprofv3 --pmc passes (FETCH_SIZE x2 "
-                        "gfx950 correction, WRITE_SIZE) run by this bench on the same workload",
+                        "time (exceeds the peak once a launch fuses passes); traffic = bytes moved "
+                        "between L2 and the memory fabric per fine-level smoother launch (HBM plus "
+                        "Infinity-Cache hits, which FETCH_SIZE also counts) from two rocprofv3 --pmc "
+                        "passes (FETCH_SIZE x2 gfx950 correction, WRITE_SIZE) run by this bench on the "
+                        "same workload; copy_rate_GBps = the measured float4 copy rate of "
+                        "MI355X_MICROARCH.md (6.29 TB/s)",
                 "avg_launch_ms": round(avg_launch_ms, 5) if launches else None,
                 "timing": ("off" if args.no_roofline_events else
                            "HIP events on the operator stream, one pair per relax call "
