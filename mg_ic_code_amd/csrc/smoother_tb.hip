@@ -97,6 +97,15 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_NTW
 #define TB2_NTW 0
 #endif
+// TB2_STEADY 1 = fp32 launches run the chunk's inner steps as a copy of the
+// step without the z range / face tests and plane clamps, copy the
+// coefficient sets out of the load registers (reg_copy) and issue a static
+// number of u loads per step (see the pipeline loop); fp64 launches keep the
+// generic step (measured neutral there: they are bound by their memory
+// traffic, the fp32 launches more by their instruction stream)
+#ifndef TB2_STEADY
+#define TB2_STEADY 1
+#endif
 // TB2_ZIN_SHORT 0 = ZIN launches run sweep 1 through the generic passes
 #ifndef TB2_ZIN_SHORT
 #define TB2_ZIN_SHORT 1
@@ -167,6 +176,19 @@ struct TB2Coefs {
       : alpha((T)s.alpha), beta((T)s.beta), dxinv((T)s.dxinv), lamshift((T)s.lamshift),
         bval((T)s.bval) {}
 };
+// A register copy the compiler cannot coalesce (TB2_STEADY, fp32): the
+// coefficient sets are copied out of the in-flight load registers, so those
+// keep one register per step parity across the unrolled loop's back edge --
+// coalesced, the four steps' loads landed in four register sets and the back
+// edge moved two of them, which waited (vmcnt) for loads issued in the same
+// step and undid the two-step prefetch.
+__device__ __forceinline__ double reg_copy(double x) { return x; }
+__device__ __forceinline__ float reg_copy(float x) {
+  if (!TB2_STEADY) return x;
+  float y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
 template <class T> struct TB2Vec;
 template <> struct TB2Vec<double> { using type = double2; };
 template <> struct TB2Vec<float> { using type = float2; };
@@ -219,6 +241,11 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // a uniform 64-bit plane base + a 32-bit lane offset
   const long corner = -16 - 4 * sy;
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+  // (steady steps: every plane they touch lies inside [-4, nz + 3], no clamp)
+  auto plane_u = [&](const T *f, int p) {
+    if (TB2_PROBE_SKIP & 512) p = __builtin_amdgcn_readfirstlane(p & 1);
+    return reinterpret_cast<const char *>(f + corner + (long)p * sz);
+  };
   auto plane = [&](const T *f, int p) {  // corner of (clamped) plane p
     if (TB2_PROBE_SKIP & 512) p = __builtin_amdgcn_readfirstlane(p & 1);
     return reinterpret_cast<const char *>(f + corner + (long)clampi(p, -4, nz + 3) * sz);
@@ -371,6 +398,8 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 #define TB2_RES_LAMC 1
 #endif
   constexpr bool LAMC = RES && TB2_RES_LAMC;
+  // (SDY: the fp32 launch's steady-state options, TB2_STEADY)
+  constexpr bool SDY = TB2_STEADY && std::is_same<T, float>::value;
   T pu0[PFU][NL], pu1[PFU][NL];
   T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
@@ -388,16 +417,22 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     for (int j = 0; j < 4; ++j) Rr[j][i] = Ra[j][i] = Rl[j][i] = Br[j][i] = Ba[j][i] = Bl[j][i] = 0.0;
   }
 
-  auto fetch_u = [&](int t, int p, auto bc) {
+  // (sd: IC<1> in steady steps, which never meet a z face, a chunk end or a
+  // clamped plane -- see the loop)
+  auto fetch_u = [&](int t, int p, auto bc, auto sd) {
     constexpr int b = decltype(bc)::value;
     // a z ghost plane of a domain face loads the plane it images
-    const char *pl = plane(ui, p == zgl ? 0 : p == zgh ? nz - 1 : p);
+    const char *pl = decltype(sd)::value ? plane_u(ui, p) : plane(ui, p == zgl ? 0 : p == zgh ? nz - 1 : p);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if ((ZIN && !RES) || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
         pu0[b][i] = 0.0;
         pu1[b][i] = 0.0;
-      } else if (NL * NT <= CP || tid + i * NT < CP) {  // (whole waves past the plane skip)
+      } else if (NL * NT <= CP || SDY || tid + i * NT < CP) {
+        // (SDY: lanes past the plane load too -- from the plane's corner,
+        // loff 0 -- and put skips them, so every step issues a static number
+        // of loads and the waits for the loads of two steps ago do not also
+        // wait for the previous step's stores)
         const bool nt = NTW && i == 0;  // (the kernel picks NTW waves by their rows)
         const V v = nt ? at2n(pl, loff[t][i]) : at2(pl, loff[t][i]);
         pu0[b][i] = v.x;
@@ -408,10 +443,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // a z ghost plane of a domain face, fetched as the plane it images ->
   // ParseBC's images (RES: the loaded phi's, with the residual's BC).  (x / y
   // ghosts are never stored: see pass.)
-  auto image = [&](int p, auto bc) {
+  auto image = [&](int p, auto bc, auto sd) {
     constexpr int b = decltype(bc)::value;
     const TB2Ghosts<T> &G = RES ? gr : gg;
-    if (p == zgl || p == zgh) {
+    if (!decltype(sd)::value && (p == zgl || p == zgh)) {
       const int zf = p == -1 ? 4 : 5;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
@@ -430,9 +465,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       Bs[tid + i * NT] = pu1[b][i];
     }
   };
-  auto fetch_c = [&](int t, int p, auto bc) {
+  auto fetch_c = [&](int t, int p, auto bc, auto sd) {
     constexpr int b = decltype(bc)::value;
-    const char *pr = plane(rhs, p), *pa = plane(a, p);
+    constexpr bool SD = decltype(sd)::value;
+    const char *pr = SD ? plane_u(rhs, p) : plane(rhs, p), *pa = SD ? plane_u(a, p) : plane(a, p);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       if (TB2_PROBE_SKIP & 1) {
@@ -485,10 +521,12 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // +0 either way.  Sweep-1 black starts from its own u = 0 (the constant
   // lets x - 2*0 fold to x, exact).  Both skip the LDS reads they no longer
   // need.
-  auto pass = [&](auto zc, bool red, int W, int t, int k, int sk, const T (&cr)[NP],
+  auto pass = [&](auto zc, auto sd, bool red, int W, int t, int k, int sk, const T (&cr)[NP],
                   const T (&ca)[NP], const T (&cl)[NP]) {
     constexpr int ZC = decltype(zc)::value;
-    if ((unsigned)(k - kl[W]) > kw[W] || (TB2_PROBE_SKIP & 2)) return;  // uniform
+    constexpr bool SD = decltype(sd)::value;  // steady: k in range, not a z face plane
+    if (TB2_PROBE_SKIP & 2) return;
+    if (!SD && (unsigned)(k - kl[W]) > kw[W]) return;  // uniform
     // rows beyond ring W (distance > W from the tile) are never read once
     // this pass is done, so waves holding only such rows skip it
     if (NP == 1 && W < 3 && wv < 3 - W) return;  // (one pair per lane only)
@@ -504,7 +542,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       for (int i = 0; i < NP; ++i) v[i] = (T)0 - cl[i] * ((T)0 - cr[i]);
 #pragma unroll
       for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> 10) & 1 ? v[i] : (T)0;
-      const bool zl = k == zfl, zh = k == zfh;
+      const bool zl = !SD && k == zfl, zh = !SD && k == zfh;
       if (zl || zh) {
         T *Nz = zl ? Nm : Np;
         const int zf = zl ? 4 : 5;
@@ -551,7 +589,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     for (int i = 0; i < NP; ++i) v[i] = upd(uc[i], xm[i], xp[i], ym[i], yp[i], zm[i], zp[i], cr[i], ca[i], cl[i]);
 #pragma unroll
     for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> (red ? 10 : 11)) & 1 ? v[i] : uc[i];
-    const bool zl = k == zfl, zh = k == zfh;
+    const bool zl = !SD && k == zfl, zh = !SD && k == zfh;
     if (zl || zh) {  // z ghosts of the face plane (every lane: an element
                      // never updated owns its ghost alone)
       T *Nz = zl ? Nm : Np;
@@ -566,11 +604,13 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // an out-of-range offset, so every step issues exactly NP * 2 stores with
   // no branch around them and the next step waits vmcnt(2) for its loads
   // instead of vmcnt(0), which would also wait for these stores.
-  auto store = [&](int t, int k, int sl) {  // sl = es(k)
+  auto store = [&](int t, int k, int sl, auto sd) {  // sl = es(k)
     if (TB2_PROBE_SKIP & 4) return;
-    const bool kin = k >= z0 && k < z1;  // uniform
-    char *dst = ACC ? reinterpret_cast<char *>(acc + corner + (long)clampi(k, z0, z1 - 1) * sz)
-                    : reinterpret_cast<char *>(uo + corner + (long)clampi(k, z0, z1 - 1) * sz);
+    constexpr bool SD = decltype(sd)::value;
+    const bool kin = SD || (k >= z0 && k < z1);  // uniform
+    const int kk = SD ? k : clampi(k, z0, z1 - 1);
+    char *dst = ACC ? reinterpret_cast<char *>(acc + corner + (long)kk * sz)
+                    : reinterpret_cast<char *>(uo + corner + (long)kk * sz);
     const __amdgpu_buffer_rsrc_t rs = sweep::store_rsrc(dst);
     constexpr unsigned kDrop = sweep::kDrop;
 #pragma unroll
@@ -689,7 +729,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // The two passes of a phase touch disjoint planes; phase A reads black
   // cells only, phase B red ones.  Live ring planes p+1 .. p-5; plane p+1 is
   // written over plane p-7.
-  auto step = [&](auto tc, int p) {
+  auto step = [&](auto tc, auto sd, int p) {
     static_assert(!RES || PF == 2, "the fused residual keeps loads two steps ahead");
     // J: position in the 4-step unrolled loop; T / U: parity of p / of p +- 1;
     // coefficient sets live in slot J (made this step) .. slot J3 (made
@@ -698,6 +738,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     constexpr int J0 = J, J3 = (J + 1) & 3;
     constexpr int FB = PF == 2 ? (J & 1) : 0;  // in-flight register set consumed / refilled
     using ICF = IC<FB>;
+    using SDC = decltype(sd);
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
     TB2_STAMP(0, p);
     // coefficient sets: black of plane p-1 from the raw black element, red
@@ -707,26 +748,26 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       Br[J0][i] = rb[i];
       Ba[J0][i] = FAST ? ab[i] : s.alpha * ab[i];
       if constexpr (!LAMC) Bl[J0][i] = lam(Ba[J0][i]);
-      Rr[J0][i] = nr0[FB][i];
-      Ra[J0][i] = FAST ? na0[FB][i] : s.alpha * na0[FB][i];
+      Rr[J0][i] = reg_copy(nr0[FB][i]);
+      Ra[J0][i] = FAST ? reg_copy(na0[FB][i]) : s.alpha * na0[FB][i];
       if constexpr (!LAMC) Rl[J0][i] = lam(Ra[J0][i]);
-      rb[i] = nr1[FB][i];
-      ab[i] = na1[FB][i];
+      rb[i] = reg_copy(nr1[FB][i]);
+      ab[i] = reg_copy(na1[FB][i]);
     }
     const int E0 = es(p), P0 = ps(p);  // this step's slots derive from these
     TB2_STAMP(1, p);
     if constexpr (RES) {  // phi of plane p+2 into the phi ring (one u register set)
-      image(p + 2, IC<0>{});
+      image(p + 2, IC<0>{}, SDC{});
       put(padd(P0, 2), IC<0>{});
     } else {
-      image(p + 1, ICF{});
+      image(p + 1, ICF{}, SDC{});
       put(padd(P0, 1), ICF{});
     }
     TB2_STAMP(2, p);
-    if (PF == 2) fetch_c(PT, p + 2, ICF{});
-    else fetch_c(PU, p + 1, ICF{});
+    if (PF == 2) fetch_c(PT, p + 2, ICF{}, SDC{});
+    else fetch_c(PU, p + 1, ICF{}, SDC{});
     if constexpr (ACC) {
-      const char *pl = plane(acc, p - 3);
+      const char *pl = SDC::value ? plane_u(acc, p - 3) : plane(acc, p - 3);
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         ac0[i] = an0[i];
@@ -736,9 +777,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         an1[i] = v.y;
       }
     }
-    if constexpr (RES) fetch_u(PU, p + 3, IC<0>{});
-    else if (PF == 2) fetch_u(PU, p + 3, ICF{});
-    else fetch_u(PT, p + 2, ICF{});
+    if constexpr (RES) fetch_u(PU, p + 3, IC<0>{}, SDC{});
+    else if (PF == 2) fetch_u(PU, p + 3, ICF{}, SDC{});
+    else fetch_u(PT, p + 2, ICF{}, SDC{});
     TB2_STAMP(3, p);
     if (!(TB2_PROBE_SKIP & 256)) __syncthreads();
     TB2_STAMP(4, p);
@@ -769,52 +810,68 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     };
     T lt[NP];
     if constexpr (LAMC) lamv(Ra[J0], lt);
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], LAMC ? lt : Rl[J0]);
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, SDC{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], LAMC ? lt : Rl[J0]);
     if constexpr (LAMC) lamv(Ra[J3], lt);
-    pass(IC<0>{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], LAMC ? lt : Rl[J3]);
+    pass(IC<0>{}, SDC{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], LAMC ? lt : Rl[J3]);
     TB2_STAMP(5, p);
     if (!(TB2_PROBE_SKIP & 128)) __syncthreads();
     TB2_STAMP(6, p);
     if constexpr (LAMC) lamv(Ba[J0], lt);
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], LAMC ? lt : Bl[J0]);
+    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, SDC{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], LAMC ? lt : Bl[J0]);
     if constexpr (LAMC) lamv(Ba[J3], lt);
-    pass(IC<0>{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], LAMC ? lt : Bl[J3]);
+    pass(IC<0>{}, SDC{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], LAMC ? lt : Bl[J3]);
     TB2_STAMP(7, p);
-    store(PT, p - 4, eadd(E0, -4));
+    store(PT, p - 4, eadd(E0, -4), SDC{});
     TB2_STAMP(8, p);
   };
 
-  fetch_u(1, pstart - 1, IC<0>{});
-  image(pstart - 1, IC<0>{});
+  fetch_u(1, pstart - 1, IC<0>{}, IC<0>{});
+  image(pstart - 1, IC<0>{}, IC<0>{});
   put(ps(pstart - 1), IC<0>{});
-  fetch_u(0, pstart, IC<0>{});
-  image(pstart, IC<0>{});
+  fetch_u(0, pstart, IC<0>{}, IC<0>{});
+  image(pstart, IC<0>{}, IC<0>{});
   put(ps(pstart), IC<0>{});
-  fetch_u(1, pstart + 1, IC<0>{});
+  fetch_u(1, pstart + 1, IC<0>{}, IC<0>{});
   if constexpr (RES) {  // phi planes pstart-1 .. pstart+1 in the ring, r of plane pstart
-    image(pstart + 1, IC<0>{});
+    image(pstart + 1, IC<0>{}, IC<0>{});
     put(ps(pstart + 1), IC<0>{});
-    fetch_u(0, pstart + 2, IC<0>{});
-    fetch_c(0, pstart, IC<0>{});
-    fetch_c(1, pstart + 1, IC<1>{});
+    fetch_u(0, pstart + 2, IC<0>{}, IC<0>{});
+    fetch_c(0, pstart, IC<0>{}, IC<0>{});
+    fetch_c(1, pstart + 1, IC<1>{}, IC<0>{});
     __syncthreads();
     residual(0, pstart, IC<0>{}, ps(pstart - 1));
     __syncthreads();  // (step pstart's put overwrites phi plane pstart-1)
   } else {
-    fetch_c(0, pstart, IC<0>{});
+    fetch_c(0, pstart, IC<0>{}, IC<0>{});
     if (PF == 2) {
-      fetch_u(0, pstart + 2, IC<PF - 1>{});
-      fetch_c(1, pstart + 1, IC<PF - 1>{});
+      fetch_u(0, pstart + 2, IC<PF - 1>{}, IC<0>{});
+      fetch_c(1, pstart + 1, IC<PF - 1>{}, IC<0>{});
     }
   }
   // (up to three steps past pend: their passes and stores fall outside every
   // range test, their loads are clamped)
-  for (int p = pstart; p <= pend; p += 4) {
-    step(IC<0>{}, p);
-    step(IC<1>{}, p + 1);
-    step(IC<2>{}, p + 2);
-    step(IC<3>{}, p + 3);
+  // Steady 4-step groups (TB2_STEADY): steps p .. p+3 with z0 + 5 <= p and
+  // p + 3 <= z1 - 4.  Every pass of such a step is inside its z range (the
+  // tile pass needs p - 4 >= z0, the others less), none is on a domain face
+  // plane (p - 4 >= 1 > 0, p <= nz - 4 < nz - 1), the loaded planes p + 2,
+  // p + 3 are below z1 <= nz (no z ghost plane to image) and the stored plane
+  // p - 4 lies in [z0, z1): their range tests, face tests and plane clamps are
+  // compiled out.  pstart + 8 == z0 + 5, so the first steady group keeps the
+  // 4-step alignment of the register sets.
+  // (three loops: fill, steady, drain; the fill takes the first two groups)
+  auto group = [&](auto sd, int p) {
+    step(IC<0>{}, sd, p);
+    step(IC<1>{}, sd, p + 1);
+    step(IC<2>{}, sd, p + 2);
+    step(IC<3>{}, sd, p + 3);
+  };
+  const int ssh = z1 - 7;
+  int p = pstart;
+  if (!RES && SDY) {
+    for (; p < pstart + 8 && p <= pend; p += 4) group(IC<0>{}, p);
+    for (; p <= ssh; p += 4) group(IC<1>{}, p);
   }
+  for (; p <= pend; p += 4) group(IC<0>{}, p);
 }
 
 
