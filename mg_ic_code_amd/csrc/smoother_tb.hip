@@ -106,6 +106,11 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_STEADY
 #define TB2_STEADY 1
 #endif
+// TB2_STEADY_ZIN 1 = fp64 zero-input launches (no u stream, so less bound by
+// memory traffic) take the steady-state step too
+#ifndef TB2_STEADY_ZIN
+#define TB2_STEADY_ZIN 1
+#endif
 // TB2_ZIN_SHORT 0 = ZIN launches run sweep 1 through the generic passes
 #ifndef TB2_ZIN_SHORT
 #define TB2_ZIN_SHORT 1
@@ -399,7 +404,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 #endif
   constexpr bool LAMC = RES && TB2_RES_LAMC;
   // (SDY: the fp32 launch's steady-state options, TB2_STEADY)
-  constexpr bool SDY = TB2_STEADY && std::is_same<T, float>::value;
+  constexpr bool SDY = TB2_STEADY && (std::is_same<T, float>::value || (ZIN && TB2_STEADY_ZIN));
   T pu0[PFU][NL], pu1[PFU][NL];
   T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
