@@ -111,6 +111,14 @@ using IC = std::integral_constant<int, N>;
 #ifndef TB2_STEADY_ZIN
 #define TB2_STEADY_ZIN 1
 #endif
+// TB2_STEADY_ACC 1 = the fp64 phi += e launches too; TB2_STEADY_ALL
+// (measurement) = every fp64 launch
+#ifndef TB2_STEADY_ACC
+#define TB2_STEADY_ACC 1
+#endif
+#ifndef TB2_STEADY_ALL
+#define TB2_STEADY_ALL 0
+#endif
 // TB2_ZIN_SHORT 0 = ZIN launches run sweep 1 through the generic passes
 #ifndef TB2_ZIN_SHORT
 #define TB2_ZIN_SHORT 1
@@ -404,7 +412,8 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 #endif
   constexpr bool LAMC = RES && TB2_RES_LAMC;
   // (SDY: the fp32 launch's steady-state options, TB2_STEADY)
-  constexpr bool SDY = TB2_STEADY && (std::is_same<T, float>::value || (ZIN && TB2_STEADY_ZIN));
+  constexpr bool SDY = TB2_STEADY && (std::is_same<T, float>::value || (ZIN && TB2_STEADY_ZIN) ||
+                                      (ACC && TB2_STEADY_ACC) || TB2_STEADY_ALL);
   T pu0[PFU][NL], pu1[PFU][NL];
   T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
