@@ -346,6 +346,20 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   constexpr int NR = TY + 6, MAIN = 32 * NR;
   static_assert(NR % 2 == 0 && MAIN <= NT * NP, "row pairing needs an even row count");
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index (uniform)
+  // the passes a wave skips whole: those of ring W < wthr.  A main wave whose
+  // two rows both lie outside the box's updatable rows (a tile that overhangs
+  // a y domain face, e.g. the last, 6-row tile row at 512 / 22) updates
+  // nothing in any pass and skips them all (its elements keep their values,
+  // which is what the passes would write; TB2_SKIP_OUT)
+#ifndef TB2_SKIP_OUT
+#define TB2_SKIP_OUT 1
+#endif
+  int wthr = 3 - wv;
+  if (TB2_SKIP_OUT && 2 * wv < NR) {
+    const int ga = y0 - 3 + wv, gb = y0 - 3 + (NR - 1 - wv);
+    if ((ga < uylo || ga > uyhi) && (gb < uylo || gb > uyhi)) wthr = 4;
+  }
+  wthr = __builtin_amdgcn_readfirstlane(wthr);
   unsigned roff[2][NP];
   int yzo[2][NP], rinf[2][NP], ci[NP];
 #pragma unroll
@@ -543,7 +557,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     if (!SD && (unsigned)(k - kl[W]) > kw[W]) return;  // uniform
     // rows beyond ring W (distance > W from the tile) are never read once
     // this pass is done, so waves holding only such rows skip it
-    if (NP == 1 && W < 3 && wv < 3 - W) return;  // (one pair per lane only)
+    if (NP == 1 && W < wthr) return;  // (one pair per lane only)
     if ((TB2_PROBE_SKIP & 8) && red) return;
     if ((TB2_PROBE_SKIP & 16) && !red) return;
     T *X = (red ? R : B) + sk * SS;  // sk = es(k)
