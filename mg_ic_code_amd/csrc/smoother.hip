@@ -1145,14 +1145,17 @@ static void launch_block(T *u_out, T *u_in, const T *rhs, const T *a, const T *b
 }
 
 // boxes of at most this many cells take the block kernel (MGIC_BLOCK_MAX_CELLS;
-// 0 = never); MGIC_BLOCK_VARIANT picks its tile for measurement.  132^3, not
-// 128^3: the deep halo's grown boxes at the 64^3-per-rank level (130^3) run
-// 20 us per sweep here against 31 us streamed (one rank of the 8-GPU run:
-// 1.92 -> 1.87 ms per V-cycle)
+// 0 = never); MGIC_BLOCK_VARIANT picks its tile for measurement.  100^3: the
+// 128^3 bottom of the 512^3 V-cycle runs its sweep pairs through the
+// two-sweep kernel (two launches instead of four; V-cycle +0.1..0.6%, three
+// rounds, round 3), while the 64^3-per-rank bottom of the 8-GPU split and its
+// deep-halo grown boxes (68^3) keep the one-shot block kernel.  (Round 2's
+// 132^3 kept the grown 128^3-per-rank boxes here: 20 us per sweep against 31
+// streamed with single sweeps.)
 static long block_max_cells() {
   static long v = [] {
     const char *e = getenv("MGIC_BLOCK_MAX_CELLS");
-    return e ? atol(e) : 132L * 132 * 132;
+    return e ? atol(e) : 100L * 100 * 100;
   }();
   return v;
 }
