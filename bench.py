@@ -44,9 +44,6 @@ def parse():
     ap.add_argument("--boxes-per-rank", default="1,1,1",
                     help="split each rank's share into this many boxes (x,y,z) -- the multi-box "
                          "(exchange) path on one GPU")
-    ap.add_argument("--overlap", type=int, default=0,
-                    help="halo exchange overlapped with the sweep: 0 off, 1 auto (boxes >= 96^3), "
-                         "2 always")
     ap.add_argument("--deep-halo", type=int, default=-1,
                     help="4-deep ghost shells, two sweeps per exchange: 0 off, 1 every level, "
                          "2 levels of boxes <= 128^3; default 1 for N > 1 (RCCL exchanges: "
@@ -56,25 +53,23 @@ def parse():
                          "send/recv (rccl), or ipc with an RCCL fallback (auto, default)")
     ap.add_argument("--agglomerate-below", type=int, default=-1,
                     help="gather MG depths whose boxes have a side below this to one box on "
-                         "rank 0 (the coarsest levels solved on rank 0); 0 off; default 32 for "
-                         "N > 1 (DESIGN.md 6: at 3 levels the 8-GPU split's coarsest boxes are "
-                         "64^3 and stay distributed; deeper hierarchies gather from 16^3 down)")
+                         "rank 0 (the coarsest levels solved on rank 0); 0 off; default: "
+                         "agglomerate_default() (DESIGN.md 6)")
     ap.add_argument("--roofline-events", choices=("relax", "launch"), default="relax",
                     help="HIP events for the smoother roofline: one pair per relax call "
                          "(default; time / launches) or one pair per launch")
     ap.add_argument("--no-roofline-events", action="store_true",
-                    help="no events in the timed region (roofline fields null)")
-    ap.add_argument("--fused-residual", type=int, default=0,
-                    help="1: form each iteration's residual inside the next V-cycle's first "
-                         "two-sweep launch (SolverParams.fused_residual; measured slower, "
-                         "DESIGN.md 3); 0 (default): a separate residual launch")
+                    help="skip the second, event-instrumented timed region (roofline fields null)")
+    ap.add_argument("--no-bottom", action="store_true",
+                    help="skip the separately reported BiCGStab-bottom V-cycle timing")
     ap.add_argument("--norm-type", type=int, default=0,
                     help="per-iteration residual norm of AMRMultiGrid's stop test (params.txt:37-38, "
                          "m_normType 0 = max norm; -1 skips it)")
     ap.add_argument("--cpu-baseline-iters", type=int, default=10)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads for the all-cores CPU baseline (0: the CPUs this process may run "
-                         "on, capped by OMP_NUM_THREADS when that is set)")
+                         "on, capped by the cgroup CPU quota and by OMP_NUM_THREADS when set -- "
+                         "the job's CPU share on a shared GPU node); pinned one per CPU")
     ap.add_argument("--cpu-1core-iters", type=int, default=1,
                     help="V-cycle iterations of the 1-thread CPU baseline (0 skips it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -116,15 +111,14 @@ def main():
 
     bpr = tuple(int(v) for v in args.boxes_per_rank.split(","))
     case = build_case(mg, comm, world, args.size, args.levels, args.nsmooth, bpr,
-                      fused=0 if args.no_fused else 1, overlap=args.overlap,
+                      fused=0 if args.no_fused else 1,
                       deep_halo=(1 if world > 1 else 0) if args.deep_halo < 0 else args.deep_halo,
-                      agglomerate_below=(32 if world > 1 else 0) if args.agglomerate_below < 0
-                      else args.agglomerate_below, fused_residual=args.fused_residual)
+                      agglomerate_below=agglomerate_default(world, args.size, args.levels)
+                      if args.agglomerate_below < 0 else args.agglomerate_below)
     n = args.size
     boxes, grid, fa, frhs, fphi, fres = (case[k] for k in ("boxes", "grid", "fa", "frhs", "fphi",
                                                            "fres"))
     dom, dx, amg, op_params = case["dom"], case["dx"], case["amg"], case["op_params"]
-    fused_res = amg.fused_residual
     r0 = amg.init_residual(fphi, frhs, fres, norm_type=0)
     nt = args.norm_type
 
@@ -132,35 +126,51 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def timed(fn):
+        """fn() between barrier + device synchronize on both sides; the max
+        over ranks of the wall time"""
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, out
+
     # AMRMultiGrid::solve's loop body K times (amg.iterations: the same phi
-    # and norms as K iteration() calls, bit for bit; iteration i's residual is
-    # formed in iteration i+1's first pre-smoothing launch where the level
-    # allows)
+    # and norms as K iteration() calls, bit for bit)
     amg.iterations(fphi, frhs, fres, args.warmup, norm_type=nt)
     comm.synchronize()
+    # the headline: K AMRMultiGrid iterations -- the V-cycle, r = rhs - L(phi)
+    # and (norm_type >= 0) its norm for the stop test, read on the host each
+    # iteration -- with no instrumentation in the timed region
+    elapsed, hist = timed(lambda: amg.iterations(fphi, frhs, fres, args.steps, norm_type=nt))
 
+    # the roofline: K more iterations with a HIP event pair around every
+    # fine-level smoother relax (or launch) on the operator's stream
     fine_cells = max((b[3] - b[0] + 1) * (b[4] - b[1] + 1) * (b[5] - b[2] + 1) for b in boxes)
-    mg.prof_smoother(not args.no_roofline_events, fine_cells,
-                     per_relax=args.roofline_events == "relax")
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    # K AMRMultiGrid iterations: the V-cycle, r = rhs - L(phi) and
-    # (norm_type >= 0) its norm for the stop test, read on the host each
-    # iteration
-    hist = amg.iterations(fphi, frhs, fres, args.steps, norm_type=nt)
-    torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    launches, passes, smooth_ms = mg.prof_smoother_read()
-    mg.prof_smoother(False)
+    launches = passes = 0
+    smooth_ms = 0.0
+    elapsed_ev = None
+    if not args.no_roofline_events:
+        mg.prof_smoother(True, fine_cells, per_relax=args.roofline_events == "relax")
+        elapsed_ev, _ = timed(lambda: amg.iterations(fphi, frhs, fres, args.steps, norm_type=nt))
+        launches, passes, smooth_ms = mg.prof_smoother_read()
+        mg.prof_smoother(False)
     r_final = amg.init_residual(fphi, frhs, fres, norm_type=0)
-    if dist is not None:
-        import torch.distributed as dist_
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist_.all_reduce(t, op=dist_.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    # the bottom solve reported separately (SURVEY 8(d): "+ bottom (report
+    # separately)"): the same V-cycle with the reference's BiCGStab bottom
+    # (Main_PoissonSolver.cpp:103-117) at the coarsest depth instead of
+    # numMGsmooth GSRB sweeps, from phi = 0 on a second hierarchy
+    bottom = None
+    if not args.no_bottom:
+        bottom = bottom_timing(mg, case, args, timed, nt, elapsed / args.steps)
 
     # dominant kernel: the fine-level smoother; passes_per_launch = 1 (one
     # colour pass), 2 (fused sweep) or 4 (two fused sweeps per launch)
@@ -196,6 +206,10 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "timed_region": "K AMRMultiGrid iterations, no instrumentation (the roofline's "
+                            "event-timed iterations run after it, separately)",
+            "value_with_roofline_events": (round(args.steps / elapsed_ev, 4)
+                                           if elapsed_ev else None),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -214,7 +228,7 @@ def main():
                 if world > 1 else "single GPU",
                 "transport": transport,
                 "agglomerate_below": case["agglomerate_below"],
-                "residual_fused": fused_res,
+                "bottom_solver": f"{args.nsmooth} GSRB sweeps (the BiCGStab bottom: 'bottom')",
             },
             "roofline": {
                 "bound": "hbm",
@@ -247,10 +261,13 @@ def main():
                 "avg_launch_ms": round(avg_launch_ms, 5) if launches else None,
                 "timing": ("off" if args.no_roofline_events else
                            "HIP events on the operator stream, one pair per relax call "
-                           "(interval / launches)" if args.roofline_events == "relax"
-                           else "HIP events on the operator stream, one pair per launch"),
+                           "(interval / launches), in K iterations timed after the headline's"
+                           if args.roofline_events == "relax"
+                           else "HIP events on the operator stream, one pair per launch, in K "
+                                "iterations timed after the headline's"),
                 "launches_timed": launches,
             },
+            "bottom": bottom,
             "cpu_baseline": cpu,
             "residual_max_norm": {"initial": r0, "final": r_final},
             "norm_type_in_step": nt,
@@ -292,8 +309,16 @@ def make_comm(mg, torch, dist, rank, world, transport):
     return mg.Comm(rank, world, unique_id=bytes(uid.tolist())), "rccl"
 
 
-def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fused=1, overlap=0,
-               deep_halo=0, agglomerate_below=0, fused_residual=0):
+def agglomerate_default(world, n, levels):
+    """agglomerate_below for an N-rank run: MG depths whose boxes have a side
+    below this are gathered onto one box on rank 0 (the coarsest levels
+    solved on rank 0, north_star / Main_PoissonSolver.cpp:103-117); 0 on one
+    rank.  DESIGN.md 6 records the measurement this default follows."""
+    return 32 if world > 1 else 0
+
+
+def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fused=1,
+               deep_halo=0, agglomerate_below=0, bottom_solver=0):
     """The bench workload (BASELINE config C3 / C4): n^3 split over `world`
     ranks (z first), SetBinaryBH aCoef / rhs of params.txt at psi = 1 on
     device, bCoef = 1, phi = 0, the reference operator settings, and an
@@ -313,12 +338,10 @@ def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fu
     op_params = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
                                   bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
                                   coefficient_average_type=1, prolong_type=1, relax_mode=1,
-                                  fused_smoother=fused, overlap_exchange=overlap,
-                                  deep_halo=deep_halo)
+                                  fused_smoother=fused, deep_halo=deep_halo)
     fac = mg.defineOperatorFactory(grid, fa, fb, op_params)
     sp = mg.SolverParams(max_depth=levels - 1, n_pre=nsmooth, n_post=nsmooth, n_bottom=nsmooth,
-                         bottom_solver=0, agglomerate_below=agglomerate_below,
-                         fused_residual=fused_residual)
+                         bottom_solver=bottom_solver, agglomerate_below=agglomerate_below)
     amg = mg.AMRMultiGrid(fac, sp)
     assert amg.num_depths == levels, amg.num_depths
     return dict(dom=dom, boxes=boxes, owners=owners, dx=dx, grid=grid, fa=fa, fb=fb, frhs=frhs,
@@ -326,13 +349,47 @@ def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fu
                 agglomerate_below=agglomerate_below)
 
 
+def bottom_timing(mg, case, args, timed, nt, gsrb_ms):
+    """K V-cycle iterations with the BiCGStab bottom (bottom_solver = 1, the
+    reference's, Main_PoissonSolver.cpp:103-117: MultilevelLinearOp's
+    BiCGStab at the coarsest MG depth) on a second hierarchy over the same
+    operator factory, from phi = 0: ms per V-cycle beside the GSRB-bottom
+    headline, and the difference (the bottom's own cost)."""
+    amg = mg.AMRMultiGrid(case["fac"], mg.SolverParams(
+        max_depth=args.levels - 1, n_pre=args.nsmooth, n_post=args.nsmooth,
+        n_bottom=args.nsmooth, bottom_solver=1, agglomerate_below=case["agglomerate_below"]))
+    phi, res = mg.LevelData(case["grid"]), mg.LevelData(case["grid"])
+    phi.set_zero()
+    frhs = case["frhs"]
+    amg.init_residual(phi, frhs, res, norm_type=0)
+    amg.iterations(phi, frhs, res, max(1, args.warmup), norm_type=nt)
+    el, hist = timed(lambda: amg.iterations(phi, frhs, res, args.steps, norm_type=nt))
+    ms = el / args.steps * 1e3
+    out = {"solver": "BiCGStab (imax 80, eps 1e-6, restarts 5; preCond = lambda r + 2 GSRB)",
+           "depth": args.levels - 1,
+           "vcycles_per_s": round(args.steps / el, 4), "ms_per_vcycle": round(ms, 4),
+           "gsrb_bottom_ms_per_vcycle": round(gsrb_ms * 1e3, 4),
+           "bottom_delta_ms": round(ms - gsrb_ms * 1e3, 4),
+           "residual_norm_history": hist[-3:] if nt >= 0 else None}
+    del amg, phi, res
+    return out
+
+
 def host_cpus():
-    """(CPUs this process may run on, CPUs of the machine)."""
+    """(CPUs this process may run on, CPUs of the machine, the cgroup's CPU
+    quota in whole CPUs or None when unlimited)."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    return avail, os.cpu_count() or avail
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return avail, os.cpu_count() or avail, quota
 
 
 def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
@@ -343,12 +400,23 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
     n = args.size
     a = fa.download(0)
     rhs = frhs.download(0)
-    avail, machine = host_cpus()
+    avail, machine, quota = host_cpus()
     threads = args.cpu_threads
+    reason = "--cpu-threads"
     if threads <= 0:
-        threads = avail
-        if os.environ.get("OMP_NUM_THREADS"):
-            threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+        threads, reason = avail, "every CPU this process may run on"
+        if quota and quota < threads:
+            threads, reason = quota, "the cgroup CPU quota (/sys/fs/cgroup/cpu.max)"
+        omp = os.environ.get("OMP_NUM_THREADS")
+        if omp and omp.isdigit() and int(omp) < threads:
+            threads = int(omp)
+            reason = ("OMP_NUM_THREADS, which the GPU pool sets to the job's CPU share (16 host "
+                      "CPUs per GPU on a shared node; the machine's other CPUs belong to other "
+                      "jobs)")
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = list(range(avail))
     o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, nlevels=args.levels, avg_type=1,
                         prolong_type=1, bottom_solver=0, n_pre=args.nsmooth, n_post=args.nsmooth,
                         n_bottom=args.nsmooth)
@@ -361,12 +429,13 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
 
     def timed(nthreads, iters):
         oracle.set_threads(nthreads)
+        pinned = oracle.pin_threads(cpus[:nthreads])  # thread t on CPU t of this job's set
         t0 = time.perf_counter()
         for _ in range(iters):
             o.iteration(0)
-        return time.perf_counter() - t0, oracle.get_threads()
+        return time.perf_counter() - t0, oracle.get_threads(), pinned
 
-    dt, used = timed(threads, args.cpu_baseline_iters)
+    dt, used, pinned = timed(threads, args.cpu_baseline_iters)
     out = {
         "value": round(args.cpu_baseline_iters / dt, 6),
         "unit": "V-cycles/s",
@@ -374,16 +443,20 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
         "kind": "port",
         "sample": f"{args.cpu_baseline_iters} V-cycle iteration(s) of the same {n}^3 "
                   f"{args.levels}-level workload (oracle/mgic_oracle.c, OpenMP, -O3), {dt:.1f} s",
+        "cores_reason": reason,
+        "pinned_threads": pinned,
         "host_cpus_available": avail,
         "host_cpus_machine": machine,
+        "host_cpu_quota": quota,
     }
     if args.cpu_1core_iters > 0:
-        dt1, _ = timed(1, args.cpu_1core_iters)
+        dt1, _, _ = timed(1, args.cpu_1core_iters)
         out["one_core"] = {"value": round(args.cpu_1core_iters / dt1, 6), "unit": "V-cycles/s",
                            "cores": 1,
                            "sample": f"{args.cpu_1core_iters} V-cycle iteration(s), 1 thread, "
                                      f"{dt1:.1f} s"}
     oracle.set_threads(threads)
+    oracle.pin_threads(cpus, pin=False)  # release the threads to the whole set
     return out
 
 
@@ -409,14 +482,13 @@ def pmc_traffic(args):
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
             d = os.path.join(work, ctr)
-            # the two-sweep smoother launches (64 x 22 tiles), not the fused
-            # residual + sweeps launch (64 x 20 tiles)
+            # the two-sweep smoother launches
             cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", ctr, "--kernel-include-regex",
                    "k_gsrb_tb2<double, 64, 22", "-d", d, "-o", "p", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
                    "--size", str(args.size), "--levels", str(args.levels), "--nsmooth",
                    str(args.nsmooth), "--no-cpu-baseline", "--no-traffic",
-                   "--no-roofline-events", "--norm-type", str(args.norm_type)]
+                   "--no-roofline-events", "--no-bottom", "--norm-type", str(args.norm_type)]
             r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env,
                                timeout=200)
             if r.returncode != 0:
@@ -442,8 +514,7 @@ def pmc_traffic(args):
             "kernel": kname,
             "method": "this run: rocprofv3 --pmc FETCH_SIZE (x1024 x2, gfx950 half count) and "
                       "WRITE_SIZE (x1024) in separate child passes of the same workload, averaged "
-                      "over the fine-level two-sweep launches (64 x 22 tiles: plain, ACC, and the ZIN "
-                      "launch of iterations without a fused residual)"}
+                      "over the fine-level two-sweep launches (plain, ACC and ZIN)"}
 
 
 if __name__ == "__main__":

@@ -63,12 +63,6 @@ typedef struct {
   int relax_mode;               /* 1 GSRB (default), 4 Jacobi */
   int fused_smoother;           /* fused red+black sweep: 0 off (one launch per colour
                                    pass), 1 kernel by box size, 2 z-streaming, 3 3D blocks */
-  int overlap_exchange;         /* fused sweeps on exchanged layouts: boundary slabs +
-                                   ghost-shell exchange on a second stream, overlapping
-                                   the sweep.  0 off (default), 1 if every box >= 96^3,
-                                   2 always; boundary-first split (slabs swept first,
-                                   their exchange overlaps the interior sweep): 3 if
-                                   every box >= 64^3, 4 always */
   int deep_halo;                /* fused sweeps on exchanged layouts: 4-deep ghost shells,
                                    two sweeps per exchange (the first on the box grown by
                                    2 across exchanged faces).  0 off (default), 1 every
@@ -86,10 +80,6 @@ typedef struct {
   int bicg_imax;
   double bicg_eps, bicg_reps, bicg_small;
   int bicg_restarts, bicg_norm_type;
-  int fused_residual;    /* 1: AMRMultiGrid iterations form r = rhs - L(phi) inside the next
-                            V-cycle's first two-sweep launch (mgic_mg_iterations, the
-                            preconditioner); 0 (default): a separate residual launch, which
-                            measured faster */
 } mgic_mg_params;
 
 MGIC_API const char *mgic_version(void);
@@ -155,6 +145,11 @@ MGIC_API int mgic_plan_create(int rank, int size, const int domain[6], const int
 MGIC_API int mgic_plan_create_shell(int rank, int size, const int domain[6],
                                     const int periodic[3], int nboxes, const int *boxes,
                                     const int *owners, int depth, mgic_plan *out);
+/* the host-side tables transport `transport` (1 RCCL, 2 peer-mapped; the
+ * numbering of mgic_comm_transport) builds for this plan before executing
+ * it: 0, or an error when that transport cannot execute it (the peer-mapped
+ * transport takes at most 32 peers per plan; RCCL has no such limit) */
+MGIC_API int mgic_plan_check_transport(mgic_plan p, int transport);
 MGIC_API int mgic_plan_destroy(mgic_plan p);
 MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpack, int *n_peers);
 MGIC_API int mgic_plan_items(mgic_plan p, int which, long long *items);
@@ -265,9 +260,6 @@ MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_
  * one streaming pass fewer per iteration. */
 MGIC_API int mgic_mg_iterations(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                                 int count, int norm_type, int homogeneous, double *norms);
-/* *fused = 1 when mgic_mg_iterations / the preconditioner fuse the residual
- * into the first pre-smoothing launch on this hierarchy */
-MGIC_API int mgic_mg_fused_residual(mgic_mg mg, int *fused);
 MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
                                    mgic_field resid, int norm_type, int homogeneous,
                                    double *norm);
@@ -331,7 +323,9 @@ MGIC_API int mgic_amr_residual_field(mgic_amr a, int level, mgic_field *out); /*
 /* MultilevelLinearOp over the hierarchy (Main_PoissonSolver.cpp:103-117,
  * 169-170 with max_level > 0; [Chombo] semantics restated, see amr.hpp):
  * lhs = AMROperator on every level, covered coarse cells zeroed; dot =
- * sum_l dx_l^3 levelDot; norm 0 = max over levels, 1 / 2 = dx_l^3-weighted */
+ * sum_l dx_l^3 levelDot; norm 0 = max over levels, 1 / 2 = dx_l^3-weighted;
+ * dot and norm mask the covered coarse cells of x (MultilevelLinearOp's
+ * dotProduct / norm count each physical cell once, on its finest level) */
 MGIC_API int mgic_amr_apply_op(mgic_amr a, const mgic_field *lhs, const mgic_field *x,
                                int homogeneous);
 MGIC_API int mgic_amr_dot(mgic_amr a, const mgic_field *x, const mgic_field *y, double *out);

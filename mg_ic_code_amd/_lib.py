@@ -37,7 +37,6 @@ class OpParams(ctypes.Structure):
         ("prolong_type", c_int),
         ("relax_mode", c_int),
         ("fused_smoother", c_int),
-        ("overlap_exchange", c_int),
         ("deep_halo", c_int),
     ]
 
@@ -70,7 +69,6 @@ class MGParams(ctypes.Structure):
         ("bicg_small", c_double),
         ("bicg_restarts", c_int),
         ("bicg_norm_type", c_int),
-        ("fused_residual", c_int),
     ]
 
 
@@ -110,6 +108,7 @@ SIGNATURES = {
     "mgic_op_update_psi": [H, H, H],
     "mgic_plan_create": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PI, PI, c_int, c_int, PH],
     "mgic_plan_create_shell": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PH],
+    "mgic_plan_check_transport": [H, c_int],
     "mgic_plan_destroy": [H],
     "mgic_plan_sizes": [H, PI, PI, PI, PI],
     "mgic_plan_items": [H, c_int, PLL],
@@ -163,7 +162,6 @@ SIGNATURES = {
     "mgic_mg_one_cycle": [H, H, H],
     "mgic_mg_iteration": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_iterations": [H, H, H, H, c_int, c_int, c_int, PD],
-    "mgic_mg_fused_residual": [H, PI],
     "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_precondition": [H, H, H, c_int],
     "mgic_mg_fmg": [H, H, H, H, c_int, c_int, c_int, PD],

@@ -313,8 +313,6 @@ class OperatorParams:
     prolong_type: int = 1               # 0 piecewise constant, 1 linear
     relax_mode: int = 1                 # 1 GSRB, 4 Jacobi
     fused_smoother: int = 1             # 0 per-colour passes, 1 by size, 2 z-streaming, 3 3D blocks
-    overlap_exchange: int = 0           # halo exchange overlapped with the sweep: 0, 1 auto, 2 always
-    #                                     (redundant slabs); 3 auto, 4 always (boundary-first split)
     deep_halo: int = 0                  # 4-deep ghost shells, two sweeps per exchange: 0 off,
     #                                     1 every level, 2 levels of boxes <= 128^3
 
@@ -328,7 +326,6 @@ class OperatorParams:
         p.prolong_type = self.prolong_type
         p.relax_mode = self.relax_mode
         p.fused_smoother = self.fused_smoother
-        p.overlap_exchange = self.overlap_exchange
         p.deep_halo = self.deep_halo
         return p
 
@@ -351,7 +348,6 @@ class SolverParams:
     bicg_small: float = 1.0e-30
     bicg_restarts: int = 5
     bicg_norm_type: int = 2
-    fused_residual: int = 0  # 1: residual inside the next V-cycle's first launch
 
     def to_c(self) -> MGParams:
         p = MGParams()
@@ -604,14 +600,6 @@ class AMRMultiGrid:
         call("mgic_mg_iterations", self._h, phi.handle, rhs.handle, resid.handle, int(count),
              int(norm_type), int(bool(homogeneous)), out)
         return [out[i] for i in range(count)]
-
-    @property
-    def fused_residual(self) -> bool:
-        """iterations() / the preconditioner fuse the residual into the
-        first pre-smoothing launch on this hierarchy"""
-        v = ctypes.c_int()
-        call("mgic_mg_fused_residual", self._h, ctypes.byref(v))
-        return bool(v.value)
 
     def init_residual(self, phi: LevelData, rhs: LevelData, resid: LevelData, norm_type: int = 0,
                       homogeneous: bool = False) -> float:

@@ -296,6 +296,11 @@ double AMRSolver::compositeNorm(const std::vector<LevelData *> &x, int ord) {
   return norm(masked(x), ord);
 }
 
+double AMRSolver::compositeDot(const std::vector<LevelData *> &x,
+                               const std::vector<LevelData *> &y) {
+  return dotProduct(masked(x), y);
+}
+
 double AMRSolver::compositeSum(const std::vector<LevelData *> &x) {
   // computeSum: sum over the uncovered cells of every level, times dx_l^3
   // (the level sum as a dot product with a field of ones)

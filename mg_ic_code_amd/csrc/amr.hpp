@@ -97,6 +97,10 @@ class AMRSolver {
   // each level weighted by dx_l^3; ord 0 = max norm, 1 / 2 = L1 / L2
   double compositeNorm(const std::vector<LevelData *> &x, int ord);
   double compositeSum(const std::vector<LevelData *> &x);
+  // the dot product with x's covered coarse cells masked (the public entry
+  // point: its operands need not have zero covered cells); the solver's own
+  // dotProduct skips the mask where an operand's covered cells are zero
+  double compositeDot(const std::vector<LevelData *> &x, const std::vector<LevelData *> &y);
   // MultilevelLinearOp::preCond: e = 0 on every level, then `iters` AMR
   // V-cycle iterations on (e, r) with homogeneous physical BCs (r's covered
   // coarse cells are zero; e's are the average of the finer level after

@@ -76,7 +76,6 @@ OpParams to_op(const mgic_op_params *p) {
   o.prolong_type = p->prolong_type;
   o.relax_mode = p->relax_mode;
   o.fused_smoother = p->fused_smoother;
-  o.overlap_exchange = p->overlap_exchange;
   o.deep_halo = p->deep_halo;
   return o;
 }
@@ -97,7 +96,6 @@ MGParams to_mg(const mgic_mg_params *p) {
   m.bicg.small = p->bicg_small;
   m.bicg.numRestarts = p->bicg_restarts;
   m.bicg.normType = p->bicg_norm_type;
-  m.fused_residual = p->fused_residual;
   return m;
 }
 
@@ -201,7 +199,6 @@ MGIC_API void mgic_op_params_default(mgic_op_params *p) {
   p->prolong_type = o.prolong_type;
   p->relax_mode = o.relax_mode;
   p->fused_smoother = o.fused_smoother;
-  p->overlap_exchange = o.overlap_exchange;
   p->deep_halo = o.deep_halo;
 }
 
@@ -221,7 +218,6 @@ MGIC_API void mgic_mg_params_default(mgic_mg_params *p) {
   p->bicg_small = m.bicg.small;
   p->bicg_restarts = m.bicg.numRestarts;
   p->bicg_norm_type = m.bicg.normType;
-  p->fused_residual = m.fused_residual;
 }
 
 // ---------------------------------------------------------------- comm
@@ -395,6 +391,14 @@ MGIC_API int mgic_plan_create_shell(int rank, int size, const int domain[6],
     p->dst = p->src;
     p->plan = build_copy_plan(*p->src, *p->dst, false, false, false, depth);
     *out = p.release();
+  });
+}
+MGIC_API int mgic_plan_check_transport(mgic_plan p, int transport) {
+  return guard([&] {
+    NEED(p);
+    MGIC_CHECK(transport == 1 || transport == 2, "transport: 1 RCCL, 2 peer-mapped");
+    if (transport == 2) p->plan->finalize_ipc_host();
+    else p->plan->finalize_host();
   });
 }
 MGIC_API int mgic_plan_destroy(mgic_plan p) {
@@ -977,13 +981,6 @@ MGIC_API int mgic_mg_iterations(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic
     mg->amg.iterations(*phi->f, *rhs->f, *resid->f, count, norm_type, h != 0, norms);
   });
 }
-MGIC_API int mgic_mg_fused_residual(mgic_mg mg, int *fused) {
-  return guard([&] {
-    NEED(mg);
-    NEED(fused);
-    *fused = mg->amg.mg.fusedResidualApplies() ? 1 : 0;
-  });
-}
 MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                                    int norm_type, int h, double *norm) {
   return guard([&] {
@@ -1271,7 +1268,7 @@ MGIC_API int mgic_amr_dot(mgic_amr a, const mgic_field *x, const mgic_field *y, 
     NEED(x);
     NEED(y);
     NEED(out);
-    *out = a->amr.dotProduct(amr_fields(a, x), amr_fields(a, y));
+    *out = a->amr.compositeDot(amr_fields(a, x), amr_fields(a, y));
   });
 }
 MGIC_API int mgic_amr_norm(mgic_amr a, const mgic_field *x, int ord, double *out) {
@@ -1280,7 +1277,7 @@ MGIC_API int mgic_amr_norm(mgic_amr a, const mgic_field *x, int ord, double *out
     NEED(x);
     NEED(out);
     MGIC_CHECK(ord >= 0 && ord <= 2, "norm order must be 0, 1 or 2");
-    *out = a->amr.norm(amr_fields(a, x), ord);
+    *out = a->amr.compositeNorm(amr_fields(a, x), ord);
   });
 }
 MGIC_API int mgic_amr_composite_norm(mgic_amr a, const mgic_field *x, int ord, double *out) {

@@ -44,13 +44,6 @@ bool gsrb_sweep_fused_restrict_applies(const BoxArgs &g, const BoxArgs &cg, int 
 void gsrb_sweep_fused_restrict(double *u_out, double *u_in, const double *rhs, const double *a,
                                const double *b, const BoxArgs &g, const StencilCoefs &s,
                                double *rc, const BoxArgs &cg, hipStream_t st);
-// The same sweep, computed only on the cells within `depth` of each
-// exchanged face (bcm == 0): the part of u_out the neighbours' ghost shells
-// need.  Values are identical to gsrb_sweep_fused's, so it may run on a
-// second stream concurrently with the full sweep writing the same cells.
-void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const double *a,
-                      const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                      int depth, hipStream_t st);
 // Two consecutive red+black sweeps u_in -> u_out in one z-streaming launch
 // (temporal blocking, smoother_tb.hip): bit-identical to two
 // gsrb_sweep_fused calls; zero_in / acc as there.  Constant bCoef; domain
@@ -61,16 +54,6 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
                     hipStream_t st);
-// the first two-sweep launch of a V-cycle iteration with that iteration's
-// residual fused in: r_out = rhs - L(phi) under g_res's BC (VCCOMPUTERES3D)
-// and e_out = two sweeps from zero on r_out under g_hom's (homogeneous) BC,
-// one max |r| partial per block into partials[0, gsrb_sweep_tb2_res_blocks).
-// Bit-identical to residual_norm + gsrb_sweep_tb2(zero_in).  Boxes with only
-// domain faces, the two-sweep kernel's other conditions.
-long gsrb_sweep_tb2_res_blocks(const BoxArgs &g);
-void gsrb_sweep_tb2_res(double *e_out, double *r_out, const double *phi, const double *rhs,
-                        const double *a, const BoxArgs &g_hom, const BoxArgs &g_res,
-                        const StencilCoefs &s, double *partials, hipStream_t st);
 // the same two-sweep launch on fp32 fields (no phi += e)
 void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
                       const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st);

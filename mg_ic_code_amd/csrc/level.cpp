@@ -49,6 +49,12 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   MGIC_HIP(hipMalloc(&arena_, (size_t)size * 2 * arena_bytes_));
   MGIC_HIP(hipDeviceSynchronize());
   ipc_ = true;
+  {
+    const char *te = getenv("MGIC_IPC_TIMEOUT_S");
+    const double s = te ? atof(te) : 10.0;
+    // the 100 MHz constant clock (wall_clock64); at least 1 ms
+    timeout_ticks_ = (unsigned long long)(std::max(s, 1e-3) * 1e8);
+  }
   peer_sig_.assign(size, nullptr);
   peer_arena_.assign(size, nullptr);
   sent_.assign(size, 0);
@@ -58,7 +64,9 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   recvd_blocks_.assign(size, 0);
   peer_sig_[rank] = sig_;
   peer_arena_[rank] = arena_;
+  int colocated = 1;  // ranks on this GPU (this one included)
   if (size > 1) {
+    colocated = 0;
     struct Rec {
       hipIpcMemHandle_t sig, arena;
       unsigned long long arena_bytes;
@@ -80,14 +88,9 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
     all = recs.data();
     if (allgather(&mine, sizeof(Rec), all, user) != 0)
       throw Error(kState, "peer-mapped transport: host allgather failed");
-    // ranks sharing this GPU (one-GPU rehearsals): cap the exchange grids so
-    // that every such rank's exchange blocks fit on the device at once
-    int colocated = 0;
     for (int r = 0; r < size; ++r)
       colocated += recs[r].pci[0] == mine.pci[0] && recs[r].pci[1] == mine.pci[1] &&
                    recs[r].pci[2] == mine.pci[2];
-    const char *ce = getenv("MGIC_IPC_GRID_CAP");
-    grid_cap_ = ce ? atoi(ce) : (colocated > 1 ? std::max(8, 256 / (2 * colocated)) : 0);
     for (int r = 0; r < size; ++r) {
       MGIC_CHECK(recs[r].rank == r && recs[r].arena_bytes == arena_bytes_,
                  "peer-mapped transport: ranks disagree on the setup");
@@ -99,6 +102,34 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
       peer_arena_[r] = static_cast<char *>(pa);
     }
   }
+  // The exchange launch's grid (k_exchange): workgroups stride over the
+  // virtual blocks in ascending order, puts first, so a workgroup has done
+  // all its puts before its first get; and the grid is capped so that every
+  // workgroup of every rank on this GPU can be resident at once.  Then no get
+  // can hold a slot a put needs, whatever order the hardware dispatches
+  // workgroups in.  One workgroup per CU for one rank per GPU (grids of 64 ..
+  // 1024 measured alike on the 8-GPU share, profiles/r03m_share_ipc_cap_sweep.txt);
+  // ranks sharing a GPU split half the CUs (r03i rehearsals).
+  {
+    int dev = 0, ncu = 0;
+    MGIC_HIP(hipGetDevice(&dev));
+    MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    ncu = std::max(ncu, 8);
+    const char *ce = getenv("MGIC_IPC_GRID_CAP");
+    grid_cap_ = ce && atoi(ce) > 0 ? atoi(ce)
+                                   : (colocated > 1 ? std::max(8, ncu / (2 * colocated)) : ncu);
+  }
+}
+
+void Comm::ipc_barrier() {
+  if (!ipc_ || size_ == 1) return;
+  // an allreduce over the signal pages completes on a rank only after every
+  // rank has issued it, i.e. after every rank's earlier stream work (its
+  // exchanges' puts into this rank's arena and acks into its page) is done
+  if (!barrier_val_) MGIC_HIP(hipMalloc(&barrier_val_, sizeof(double)));
+  MGIC_HIP(hipMemsetAsync(barrier_val_, 0, sizeof(double), stream_));
+  allreduce(barrier_val_, 0);
+  ipc_check();
 }
 
 void Comm::ipc_send(int peer, long nblocks, void **slot, const unsigned long long **wait,
@@ -151,19 +182,15 @@ std::shared_ptr<Comm> Comm::host_only(int rank, int size) {
   return c;
 }
 
-hipStream_t Comm::side_stream() {
-  if (!side_) MGIC_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-  return side_;
-}
-
-hipEvent_t Comm::event(int i) {
-  if (!events_[i]) MGIC_HIP(hipEventCreateWithFlags(&events_[i], hipEventDisableTiming));
-  return events_[i];
-}
-
 Comm::~Comm() {
   if (nccl_) ncclCommDestroy(nccl_);
   if (ipc_) {
+    // no rank unmaps or frees its arena / signal page while a peer may still
+    // write into it (bounded: a peer that is gone times out the barrier)
+    try {
+      if (*h_err_ == 0) ipc_barrier();
+    } catch (...) {
+    }
     (void)hipDeviceSynchronize();
     for (int r = 0; r < size_; ++r) {
       if (r == rank_) continue;
@@ -173,10 +200,8 @@ Comm::~Comm() {
     if (sig_) (void)hipFree(sig_);
     if (arena_) (void)hipFree(arena_);
     if (h_err_) (void)hipHostFree(h_err_);
+    if (barrier_val_) (void)hipFree(barrier_val_);
   }
-  if (side_) (void)hipStreamDestroy(side_);
-  for (hipEvent_t e : events_)
-    if (e) (void)hipEventDestroy(e);
   if (d_partials_) (void)hipFree(d_partials_);
   if (d_result_) (void)hipFree(d_result_);
   if (h_result_) (void)hipHostFree(h_result_);
@@ -200,6 +225,7 @@ void Comm::allreduce(double *d_val, int op) {
     r.rank = rank_;
     r.count = ++red_count_;
     r.parity = (int)(r.count & 1);
+    r.timeout = timeout_ticks_;
     for (int q = 0; q < size_; ++q) r.sig[q] = peer_sig_[q];
     kern::ipc_allreduce(d_val, op, r, ipc_err(), stream_);
     return;
@@ -475,53 +501,76 @@ void CopyPlan::finalize() {
   d_local_ = upload_items(local_, max_local_);
   d_pack_ = upload_items(pack_, max_pack_);
   d_unpack_ = upload_items(unpack_, max_unpack_);
-  // the peer-mapped transport's tables: offsets within each peer's message,
-  // pad = the peer's index in send_peers_ / recv_peers_
+  final_ = true;
+}
+
+// The peer-mapped transport's tables, built on the plan's first execution
+// through that transport (an RCCL job never builds them, and the transport's
+// peer limit binds only plans it executes): offsets within each peer's
+// message, pad = the peer's index in send_peers_ / recv_peers_; one block
+// table for the one-launch exchange: put blocks, then the same-rank copies,
+// then get blocks, every item split into ipc_blocks(cells) blocks -- the same
+// split on the sending and the receiving side, so the block counts match per
+// message
+void CopyPlan::finalize_ipc_host() {
+  if (ipc_host_) return;
+  finalize_host();
+  ipc_pack_h_.clear();
+  ipc_unpack_h_.clear();
+  xblocks_h_.clear();
+  send_peers_.clear();
+  recv_peers_.clear();
   if (!pack_.empty() || !unpack_.empty()) {
-    std::vector<CopyItem> ip = pack_, iu = unpack_;
     for (auto &kv : send_cnt_) send_peers_.push_back(kv.first);
     for (auto &kv : recv_cnt_) recv_peers_.push_back(kv.first);
     MGIC_CHECK((int)send_peers_.size() <= kern::kMaxIpcPeers &&
                    (int)recv_peers_.size() <= kern::kMaxIpcPeers,
                "exchange plan: too many peers for the peer-mapped transport");
-    for (auto &it : ip) {
+    ipc_pack_h_ = pack_;
+    ipc_unpack_h_ = unpack_;
+    for (auto &it : ipc_pack_h_) {
       it.doff -= send_off_[it.pad];
       it.pad = (int)(std::find(send_peers_.begin(), send_peers_.end(), it.pad) - send_peers_.begin());
     }
-    for (auto &it : iu) {
+    for (auto &it : ipc_unpack_h_) {
       it.soff -= recv_off_[it.pad];
       it.pad = (int)(std::find(recv_peers_.begin(), recv_peers_.end(), it.pad) - recv_peers_.begin());
     }
-    long dummy = 0;
-    d_ipc_pack_ = upload_items(ip, dummy);
-    d_ipc_unpack_ = upload_items(iu, dummy);
-    // one block table for the one-launch exchange: put blocks, then the
-    // same-rank copies, then get blocks; every item split into
-    // ipc_blocks(cells) blocks -- the same split on the sending and the
-    // receiving side, so the block counts match per message
-    std::vector<kern::IpcBlock> tab;
     auto add = [&](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> *per) {
       if (per) per->assign(npeers, 0);
-      const size_t n0 = tab.size();
+      const size_t n0 = xblocks_h_.size();
       for (size_t i = 0; i < v.size(); ++i) {
         const long nb = kern::ipc_blocks((long)v[i].nx * v[i].ny * v[i].nz);
-        for (long b = 0; b < nb; ++b) tab.push_back({(int)i, (int)b});
+        for (long b = 0; b < nb; ++b) xblocks_h_.push_back({(int)i, (int)b});
         if (per) (*per)[v[i].pad] += nb;
       }
-      return (int)(tab.size() - n0);
+      return (int)(xblocks_h_.size() - n0);
     };
-    n_put_blocks_ = add(ip, send_peers_.size(), &send_blocks_);
+    n_put_blocks_ = add(ipc_pack_h_, send_peers_.size(), &send_blocks_);
     n_loc_blocks_ = add(local_, 0, nullptr);
-    n_get_blocks_ = add(iu, recv_peers_.size(), &recv_blocks_);
-    MGIC_HIP(hipMalloc(&d_xblocks_, sizeof(kern::IpcBlock) * tab.size()));
-    MGIC_HIP(hipMemcpy(d_xblocks_, tab.data(), sizeof(kern::IpcBlock) * tab.size(),
+    n_get_blocks_ = add(ipc_unpack_h_, recv_peers_.size(), &recv_blocks_);
+  }
+  ipc_host_ = true;
+}
+
+void CopyPlan::finalize_ipc() {
+  if (ipc_final_) return;
+  finalize();
+  finalize_ipc_host();
+  if (!xblocks_h_.empty()) {
+    long dummy = 0;
+    d_ipc_pack_ = upload_items(ipc_pack_h_, dummy);
+    d_ipc_unpack_ = upload_items(ipc_unpack_h_, dummy);
+    MGIC_HIP(hipMalloc(&d_xblocks_, sizeof(kern::IpcBlock) * xblocks_h_.size()));
+    MGIC_HIP(hipMemcpy(d_xblocks_, xblocks_h_.data(), sizeof(kern::IpcBlock) * xblocks_h_.size(),
                        hipMemcpyHostToDevice));
   }
-  final_ = true;
+  ipc_final_ = true;
 }
 
 template <class T>
 void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hipStream_t st) {
+  finalize_ipc();
   const size_t cap = comm.ipc_arena_bytes() / sizeof(T);
   for (auto &kv : send_cnt_)
     MGIC_CHECK((size_t)kv.second <= cap, "exchange message exceeds the transport arena "
@@ -529,6 +578,7 @@ void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hip
   kern::IpcPeers pput{}, pget{};
   pput.n = (int)send_peers_.size();
   pput.err = pget.err = comm.ipc_err();
+  pput.timeout = pget.timeout = comm.ipc_timeout_ticks();
   for (int q = 0; q < pput.n; ++q)
     comm.ipc_send(send_peers_[q], send_blocks_[q], &pput.buf[q], &pput.wait[q], &pput.wait_val[q],
                   &pput.count[q]);

@@ -57,27 +57,27 @@ class Comm {
   ncclComm_t nccl() const { return nccl_; }
   hipStream_t stream() const { return stream_; }
   void set_stream(hipStream_t s) { stream_ = s; }
-  // a second stream (created on first use) for halo work that overlaps the
-  // main stream's sweeps, and two reusable events to order the two
-  hipStream_t side_stream();
-  hipEvent_t event(int i);
   // in-place allreduce of one device double (op: 0 sum, 1 max)
   void allreduce(double *d_val, int op);
   // scratch for reductions (device partials + result, pinned host result)
   double *d_partials(int n);
   // reduction results (device) and their host copies (pinned): slots 0-1 for
-  // the operators' reductions, slot 2 for the max norm a fused-residual
-  // launch leaves behind while the rest of its V-cycle runs
+  // the operators' reductions
   static constexpr int kResultSlots = 4;
-  static constexpr int kFusedNormSlot = 2;
   double *d_result() const { return d_result_; }
   double *h_result() const { return h_result_; }
 
   // ---- peer-mapped transport (transport.hpp)
   size_t ipc_arena_bytes() const { return arena_bytes_; }
-  // workgroup cap of one exchange launch: 0 (none) unless ranks share a GPU
-  // (MGIC_IPC_GRID_CAP overrides)
+  // workgroup cap of one exchange launch: the CUs of the GPU, split among
+  // the ranks that share it (MGIC_IPC_GRID_CAP overrides); see the constructor
   int ipc_grid_cap() const { return grid_cap_; }
+  // bound of every device-side wait, in 100 MHz clock ticks
+  // (MGIC_IPC_TIMEOUT_S seconds, default 10)
+  unsigned long long ipc_timeout_ticks() const { return timeout_ticks_; }
+  // device-side barrier over the signal pages (returns once every rank's
+  // earlier stream work is done; raises if a wait timed out)
+  void ipc_barrier();
   // my next message to `peer` (nblocks put blocks): its slot in the peer's
   // arena, the acknowledgement count to wait for (the slot's previous
   // message consumed) and the peer's counter my blocks add to
@@ -102,14 +102,14 @@ class Comm {
   ncclComm_t nccl_ = nullptr;
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;
-  hipStream_t side_ = nullptr;
-  hipEvent_t events_[2] = {nullptr, nullptr};
   double *d_partials_ = nullptr;
   int n_partials_ = 0;
   double *d_result_ = nullptr;
   double *h_result_ = nullptr;
   bool ipc_ = false;
   int grid_cap_ = 0;
+  unsigned long long timeout_ticks_ = 1000000000ull;
+  double *barrier_val_ = nullptr;
   unsigned long long *sig_ = nullptr;            // my signal page (uncached)
   char *arena_ = nullptr;                        // my receive arena: size x 2 x arena_bytes_
   size_t arena_bytes_ = 0;
@@ -128,7 +128,11 @@ class CopyPlan {
  public:
   ~CopyPlan();
   void finalize_host();  // per-peer buffer offsets (host only)
-  void finalize();       // + upload item tables, allocate message buffers
+  void finalize();       // + upload the item tables (RCCL / local copies)
+  void finalize_ipc();   // + the peer-mapped transport's tables (on first use)
+  // the peer-mapped transport's host tables only (raises when the plan has
+  // more peers than that transport takes: kern::kMaxIpcPeers)
+  void finalize_ipc_host();
   // src_tab / dst_tab: device tables of valid-lo pointers per local box
   void execute(Comm &comm, double *const *src_tab, double *const *dst_tab, hipStream_t st);
   // the same copies on fp32 fields (same element offsets; messages in floats)
@@ -154,7 +158,9 @@ class CopyPlan {
   std::vector<long> send_blocks_, recv_blocks_;  // per peer of the lists above
   long max_local_ = 0, max_pack_ = 0, max_unpack_ = 0;
   double *sendbuf_ = nullptr, *recvbuf_ = nullptr;
-  bool final_ = false, host_final_ = false;
+  bool final_ = false, host_final_ = false, ipc_final_ = false, ipc_host_ = false;
+  std::vector<CopyItem> ipc_pack_h_, ipc_unpack_h_;
+  std::vector<kern::IpcBlock> xblocks_h_;
 };
 
 // DisjointBoxLayout + ProblemDomain + dx at one level.

@@ -370,63 +370,6 @@ static int sweeps_per_launch() {
   return v;
 }
 
-bool VariableCoeffPoissonOperator::overlapApplies() const {
-  if (prm.overlap_exchange != 1 && prm.overlap_exchange != 2) return false;
-  if (prm.overlap_exchange == 2) return true;
-  static const long min_cells = [] {
-    const char *e = getenv("MGIC_OVERLAP_MIN_CELLS");
-    return e ? atol(e) : 96L * 96 * 96;
-  }();
-  // decided on the global layout, so every rank issues the same sequence
-  // of RCCL calls on the same streams
-  for (const Box &b : grid->boxes)
-    if (b.ncells() < min_cells) return false;
-  return true;
-}
-
-// Boundary-first split of a sweep (overlap_exchange 3 / 4): the cells
-// within kSplitDepth of every exchanged face are swept first (one small
-// launch), the ghost-shell exchange of that result then runs on the side
-// stream while the main stream sweeps the rest of the box.  Every cell is
-// computed once, from the same old values as the whole-box sweep (the
-// interior sweep reads the slab cells of u_in as its shell), so results are
-// bit-identical.  Decided on the global layout (same RCCL sequence on every
-// rank): every box must leave a non-empty interior.
-static constexpr int kSplitDepth = 2;
-
-bool VariableCoeffPoissonOperator::splitApplies() const {
-  if (prm.overlap_exchange != 3 && prm.overlap_exchange != 4) return false;
-  static const long min_cells = [] {
-    const char *e = getenv("MGIC_SPLIT_MIN_CELLS");
-    return e ? atol(e) : 64L * 64 * 64;
-  }();
-  for (const Box &b : grid->boxes) {
-    if (prm.overlap_exchange == 3 && b.ncells() < min_cells) return false;
-    for (int d = 0; d < 3; ++d)
-      if (b.size(d) < 4 * kSplitDepth + 2) return false;
-  }
-  return true;
-}
-
-// the box minus kSplitDepth cells along every exchanged face: BoxArgs of
-// the interior and its element offset from the valid-lo corner
-static BoxArgs split_interior(const BoxArgs &g, long *off) {
-  BoxArgs a = g;
-  long o = 0;
-  const long st[3] = {1, g.sy, g.sz};
-  int *n[3] = {&a.nx, &a.ny, &a.nz};
-  for (int d = 0; d < 3; ++d) {
-    if (!g.bcm[2 * d]) {
-      *n[d] -= kSplitDepth;
-      a.glo[d] += kSplitDepth;
-      o += kSplitDepth * st[d];
-    }
-    if (!g.bcm[2 * d + 1]) *n[d] -= kSplitDepth;
-  }
-  *off = o;
-  return a;
-}
-
 // Deep halo (deep_halo = 1): a 4-deep ghost shell feeds two sweeps.  The
 // first sweeps the box grown by 2 across every exchanged face -- the
 // neighbours' cells within 2 of the face, recomputed from the shell with the
@@ -506,7 +449,6 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     }
   }
   LevelData *src = &dpsi, *dst = sweep_tmp_.get();
-  if (flags & kSrcInScratch) std::swap(src, dst);  // (the fused-residual launch's output)
   // two sweeps per launch (temporal blocking): on boxes with only domain
   // faces, or with exchanged faces in deep-halo mode (the kernel's rings run
   // onto the 4-deep shell, exchanged before every pair; rhs / coefficient
@@ -519,25 +461,12 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
   // the pair also takes the phi += e sweep
   const bool pair_acc = two;
   const bool want_out = halo && (flags & kHaloOut) && !acc;
-  const bool overlap = halo && per == 1 && overlapApplies();
-  const bool split = halo && per == 1 && !overlap && splitApplies();
-  const bool deep = deep_ok && per == 1 && !overlap && !split;
+  // (overlapping the exchange with the sweep on a second stream, by
+  // recomputed boundary slabs or a boundary-first split, measured slower
+  // with both transports and was removed in round 4: DESIGN.md 6)
+  const bool deep = deep_ok && per == 1;
   int vd = zero_in ? (1 << 20) : 0;  // deep: valid ghost-shell depth of src
   bool out_ready = false;            // deep: the last sweep left its face ghosts valid
-  // Overlapped halo: sweep i runs on the main stream over the whole box;
-  // meanwhile the side stream recomputes the cells within 2 of every
-  // exchanged face (the same values) and exchanges that ghost shell, so the
-  // exchange sweep i+1 needs is in flight while sweep i runs.  Ordering:
-  // side step i waits for main up to sweep i-1 (evM: its input complete), main
-  // sweep i+1 waits for side step i (evE: its input's shell filled, and
-  // side step i done reading the buffer sweep i+1 overwrites).
-  hipStream_t side = nullptr;
-  hipEvent_t evM = nullptr, evE = nullptr;
-  if (overlap || split) {
-    side = grid->comm->side_stream();
-    evM = grid->comm->event(0);
-    evE = grid->comm->event(1);
-  }
   // the last sweep restricts too (single sweep kernel over every box) when
   // it is a single sweep: with pairs, a separate restriction is cheaper than
   // splitting the last pair
@@ -551,7 +480,6 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
                       kern::gsrb_sweep_fused_restrict_applies(args_hom_[b], cg.box_args_plain(b),
                                                               prm.fused_smoother);
   }
-  bool side_pending = false;
   for (int it = 0; it < n;) {
     const bool zin = zero_in && it == 0;
     // a pair, unless it would swallow a special last sweep (+ restriction,
@@ -564,7 +492,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
         src->exchange_shell(st, kDeepDepth);
         vd = kDeepDepth;
       }
-    } else if (halo && !zin && (!(overlap || split) || it == 0)) {
+    } else if (halo && !zin) {
       src->exchange_shell(st, k == 2 ? kDeepDepth : 2);
     }
     // deep: sweep the grown box when the shell allows it and the result's
@@ -573,38 +501,6 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
     if (deep) {
       vd = grow;
       if (last) out_ready = grow > 0;
-    }
-    if (side_pending) {
-      MGIC_HIP(hipStreamWaitEvent(st, evE, 0));
-      side_pending = false;
-    }
-    // everything the main stream did so far (src's valid cells, the exposed
-    // first exchange, rhs/coefficient ghosts) is what the side step reads
-    if (overlap) MGIC_HIP(hipEventRecord(evM, st));
-    if (split && (!last || want_out)) {
-      // slabs of every local box (the local copies read neighbours' slabs),
-      // then their exchange on the side stream, then the interiors
-      for (int b = 0; b < grid->nlocal(); ++b)
-        kern::gsrb_sweep_slabs(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
-                               args_hom_[b], s, zin, kSplitDepth, st);
-      MGIC_HIP(hipEventRecord(evM, st));
-      MGIC_HIP(hipStreamWaitEvent(side, evM, 0));
-      if (last) dst->exchange(side);  // the face ghosts the caller wants
-      else dst->exchange_shell(side);
-      MGIC_HIP(hipEventRecord(evE, side));
-      side_pending = true;
-      for (int b = 0; b < grid->nlocal(); ++b) {
-        long o = 0;
-        const BoxArgs ia = split_interior(args_hom_[b], &o);
-        const long nc = (long)ia.nx * ia.ny * ia.nz;
-        prof_mark(st, nc, true, 2);
-        kern::gsrb_sweep_fused(dst->p[b] + o, src->p[b] + o, rhs.p[b] + o, m_aCoef->p[b] + o,
-                               m_bCoef->p[b] + o, ia, s, zin, nullptr, prm.fused_smoother, st);
-        prof_mark(st, nc, false, 2);
-      }
-      std::swap(src, dst);
-      it += k;
-      continue;
     }
     for (int b = 0; b < grid->nlocal(); ++b) {
       // the roofline instrumentation times the sweep kernels only (the
@@ -628,72 +524,19 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
                                sargs[b], s, zin, last && acc ? acc->p[b] : nullptr, skind, st);
       prof_mark(st, nc, false, 2 * k);
     }
-    if (overlap && (!last || want_out)) {
-      MGIC_HIP(hipStreamWaitEvent(side, evM, 0));
-      for (int b = 0; b < grid->nlocal(); ++b)
-        kern::gsrb_sweep_slabs(dst->p[b], src->p[b], rhs.p[b], m_aCoef->p[b], m_bCoef->p[b],
-                               args_hom_[b], s, zin, 2, side);
-      dst->exchange_shell(side);
-      MGIC_HIP(hipEventRecord(evE, side));
-      side_pending = true;
-    }
     std::swap(src, dst);
     it += k;
   }
   prof_flush();  // the interval ends with the relax
-  if (side_pending) MGIC_HIP(hipStreamWaitEvent(st, evE, 0));
   if (acc) return false;  // the last sweep went into acc; dpsi is scratch now
   if (src != &dpsi) {  // the result sits in the scratch buffer
     for (int b = 0; b < grid->nlocal(); ++b)
       kern::blas(0, dpsi.p[b], src->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
     if (want_out) dpsi.exchange(st);
-  } else if (want_out && !overlap && !split && !out_ready) {
+  } else if (want_out && !out_ready) {
     dpsi.exchange(st);
   }
   return restrict_last;
-}
-
-bool VariableCoeffPoissonOperator::fusedResidualApplies(int n) {
-  if (n < 2 || prm.relax_mode != 1 || cf || grid->has_memory_faces() ||
-      !fusedSmootherApplies() || sweeps_per_launch() != 2)
-    return false;
-  const StencilCoefs s = coefs();
-  for (int b = 0; b < grid->nlocal(); ++b)
-    if (!kern::gsrb_sweep_tb2_applies(args_hom_[b], s, prm.fused_smoother)) return false;
-  return true;
-}
-
-void VariableCoeffPoissonOperator::residualRelaxFromZero(LevelData &e, LevelData &r,
-                                                         LevelData &phi, const LevelData &rhs,
-                                                         int n, bool homogeneous, int normType,
-                                                         int slot, int flags) {
-  MGIC_CHECK(fusedResidualApplies(n), "the fused residual launch does not apply to this level");
-  check_same_layout(*grid, e, "correction");
-  check_same_layout(*grid, r, "residual");
-  check_same_layout(*grid, phi, "phi");
-  check_same_layout(*grid, rhs, "rhs");
-  resetLambda();  // .cpp:283
-  const hipStream_t st = stream();
-  const StencilCoefs s = coefs();
-  if (!sweep_tmp_) sweep_tmp_ = create();
-  Comm &c = *grid->comm;
-  long total = 0;
-  for (int b = 0; b < grid->nlocal(); ++b) total += kern::gsrb_sweep_tb2_res_blocks(args_hom_[b]);
-  double *parts = c.d_partials((int)std::max(1L, total));
-  long off = 0;
-  for (int b = 0; b < grid->nlocal(); ++b) {  // r = rhs - L(phi); two sweeps from zero on r
-    kern::gsrb_sweep_tb2_res(sweep_tmp_->p[b], r.p[b], phi.p[b], rhs.p[b], m_aCoef->p[b],
-                             args_hom_[b], args(b, homogeneous), s, parts + off, st);
-    off += kern::gsrb_sweep_tb2_res_blocks(args_hom_[b]);
-  }
-  if (normType == 0) finish_reduce(3, parts, (int)total, slot);
-  if (n > 2) {
-    fusedRelax(e, r, n - 2, false, nullptr, flags | kSrcInScratch);
-  } else {
-    for (int b = 0; b < grid->nlocal(); ++b)
-      kern::blas(0, e.p[b], sweep_tmp_->p[b], nullptr, 0.0, 0.0, args_plain_[b], st);
-    if (flags & kHaloOut) e.exchange(st);
-  }
 }
 
 void VariableCoeffPoissonOperator::relaxAccumulate(LevelData &e, const LevelData &r, int n,
@@ -1169,13 +1012,7 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
   // restricts in its last sweep
   Level &N = levels_[d + 1];
   LevelData &rc = N.agg ? *N.r_stage : *N.r;
-  if (d == 0 && fres_) {  // r = rhs - L(phi) fused into the first pre-smoothing launch
-    const FusedRes f = *fres_;
-    fres_ = nullptr;
-    op.residualRelaxFromZero(e, r, *f.phi, *f.rhs, prm.n_pre, f.hom, f.normType, f.slot,
-                             rf | kHaloOut);
-    op.restrictResidual(rc, e, r, false);
-  } else if (!op.relaxRestrict(e, r, prm.n_pre, e_zero, rf | kHaloOut, rc)) {
+  if (!op.relaxRestrict(e, r, prm.n_pre, e_zero, rf | kHaloOut, rc)) {
     op.restrictResidual(rc, e, r, false);
   }
   if (N.agg) N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
@@ -1194,25 +1031,6 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
     op.relaxAccumulate(e, r, prm.n_post, *phi_acc, rf);
   else
     op.relaxFlags(e, r, prm.n_post, rf | out);
-}
-
-bool MultiGrid::fusedResidualApplies() {
-  return prm.fused_residual && depths() >= 2 && op(0).fusedResidualApplies(prm.n_pre);
-}
-
-void MultiGrid::oneCycleResidualFromZero(LevelData &e, LevelData &r, LevelData &phi,
-                                         const LevelData &rhs, bool homogeneous, int normType,
-                                         int slot, LevelData *phi_acc) {
-  MGIC_CHECK(fusedResidualApplies(), "the fused residual does not apply to this hierarchy");
-  const FusedRes f{&phi, &rhs, homogeneous, normType, slot};
-  fres_ = &f;
-  try {
-    cycle(0, e, r, true, phi_acc);
-  } catch (...) {
-    fres_ = nullptr;
-    throw;
-  }
-  fres_ = nullptr;
 }
 
 void MultiGrid::fmg(LevelData &e0, LevelData &r0, LevelData &phi, int ncycles) {
@@ -1264,37 +1082,10 @@ double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &
 
 void AMRMultiGrid::iterations(LevelData &phi, const LevelData &rhs, LevelData &resid, int count,
                               int normType, bool homogeneous, double *norms) {
-  if (count <= 0) return;
-  if (!mg.fusedResidualApplies()) {
-    for (int i = 0; i < count; ++i) {
-      const double v = iteration(phi, rhs, resid, normType, homogeneous);
-      if (norms) norms[i] = v;
-    }
-    return;
+  for (int i = 0; i < count; ++i) {
+    const double v = iteration(phi, rhs, resid, normType, homogeneous);
+    if (norms) norms[i] = v;
   }
-  VariableCoeffPoissonOperator &op0 = mg.op(0);
-  Comm &c = *op0.grid->comm;
-  const hipStream_t st = op0.stream();
-  mg.oneCycleFromZeroInto(*corr_, resid, phi);  // iteration 1 on the current residual
-  for (int i = 1; i < count; ++i) {
-    // iteration i+1, whose first launch forms iteration i's residual
-    const int slot = Comm::kFusedNormSlot;  // (the bottom solver's reductions use 0-1)
-    mg.oneCycleResidualFromZero(*corr_, resid, phi, rhs, homogeneous, normType, slot, &phi);
-    double v = -1.0;
-    if (normType == 0) {  // the fused launch's max norm
-      MGIC_HIP(hipMemcpyAsync(c.h_result() + slot, c.d_result() + slot, sizeof(double),
-                              hipMemcpyDeviceToHost, st));
-      c.ipc_err_async(st);
-      MGIC_HIP(hipStreamSynchronize(st));
-      c.ipc_err_raise();
-      v = c.h_result()[slot];
-    } else if (normType > 0) {
-      v = op0.norm(resid, normType);  // resid is still iteration i's residual
-    }
-    if (norms) norms[i - 1] = v;
-  }
-  const double v = op0.residualNorm(resid, phi, rhs, homogeneous, normType);
-  if (norms) norms[count - 1] = v;
 }
 
 double AMRMultiGrid::fmg(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,
@@ -1312,12 +1103,7 @@ void AMRMultiGrid::precondition(LevelData &e, const LevelData &r, int iters) {
   // first cycle runs on r (its ghosts are the only cells it writes); the
   // residual after the last cycle is not needed
   LevelData &r0 = const_cast<LevelData &>(r);
-  const bool fused = iters > 1 && mg.fusedResidualApplies();
   for (int i = 0; i < iters; ++i) {
-    if (i > 0 && fused) {  // r - L(e) fused into the cycle's first launch
-      mg.oneCycleResidualFromZero(*corr_, *pre_resid_, e, r, true, -1, Comm::kFusedNormSlot, &e);
-      continue;
-    }
     if (i > 0) op0.residual(*pre_resid_, e, r, true);
     mg.oneCycleFromZeroInto(*corr_, i == 0 ? r0 : *pre_resid_, e);
   }

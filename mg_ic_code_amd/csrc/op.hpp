@@ -32,16 +32,6 @@ struct OpParams {
   int relax_mode = 1;                // [Chombo] s_relaxMode: 1 GSRB, 4 Jacobi
   int fused_smoother = 1;            // fused red+black sweep: 0 off (per-colour passes),
                                      // 1 by box size, 2 z-streaming kernel, 3 3D-block kernel
-  int overlap_exchange = 0;          // fused sweeps on exchanged layouts: compute the
-                                     // boundary slabs + ghost-shell exchange on a second
-                                     // stream while the main stream sweeps the box.
-                                     // 0 off (default: measured slower on one GPU, the
-                                     // slab sweeps cost more than the exchange they hide),
-                                     // 1 when every box has >= 96^3 cells, 2 always;
-                                     // boundary-first split (no redundant slabs: the
-                                     // main stream sweeps the slabs, then the interior
-                                     // while the side stream exchanges the slabs):
-                                     // 3 when every box has >= 64^3 cells, 4 always
   int deep_halo = 0;                 // fused sweeps on exchanged layouts: 4-deep ghost
                                      // shells, two sweeps per exchange (the first on the
                                      // box grown by 2 across exchanged faces); 0 off,
@@ -50,9 +40,7 @@ struct OpParams {
 
 // relax flags (MultiGrid::cycle): the caller exchanged rhs's ghost layer
 // already / wants the result's face ghosts exchanged on return
-enum RelaxFlags { kRhsHaloReady = 1, kHaloOut = 2, kSrcInScratch = 4 };
-// (kSrcInScratch: fusedRelax's input sits in the operator's sweep scratch
-// buffer, not in dpsi -- the fused-residual launch leaves it there)
+enum RelaxFlags { kRhsHaloReady = 1, kHaloOut = 2 };
 
 class VariableCoeffPoissonOperator {
  public:
@@ -165,8 +153,6 @@ class VariableCoeffPoissonOperator {
   // rhs) when the fused kernel can (returns whether it did)
   bool fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false,
                   LevelData *acc = nullptr, int flags = 0, LevelData *rst = nullptr);
-  bool overlapApplies() const;
-  bool splitApplies() const;
   bool deepApplies() const;
   // r's ghosts for the fused sweeps' rings (once per MultiGrid level visit):
   // face layer 1, or the 4-deep shell in deep-halo mode
@@ -179,16 +165,6 @@ class VariableCoeffPoissonOperator {
   void relaxFromZero(LevelData &e, const LevelData &r, int n, int flags = 0);
   // relax(e, r, n) with RelaxFlags
   void relaxFlags(LevelData &e, const LevelData &r, int n, int flags);
-  // r = rhs - L(phi) (residualI with `homogeneous`) and then e = 0;
-  // relax(e, r, n), the residual fused into the first two-sweep launch
-  // (gsrb_sweep_tb2_res; bit-identical to residualI + relaxFromZero).  The
-  // max norm of r (normType 0) is reduced into the communicator's result
-  // slot `slot` on the stream (read it after a synchronisation); other
-  // norm types are taken by a separate pass.  Call only when
-  // fusedResidualApplies(n).
-  void residualRelaxFromZero(LevelData &e, LevelData &r, LevelData &phi, const LevelData &rhs,
-                             int n, bool homogeneous, int normType, int slot, int flags = 0);
-  bool fusedResidualApplies(int n);
   // (e = 0 when zero_in;) relax(e, r, n); and, when the fused sweep can
   // fold it into its last pass, restrictResidual(resC, e, r) -- returns
   // whether the restriction was done (else the caller restricts)
@@ -257,7 +233,6 @@ struct MGParams {
   int bottom_solver = 1;       // 0: relax(n_bottom), 1: BiCGStab
   int cycles = 1;              // 1 = V-cycle
   int agglomerate_below = 0;   // gather to rank 0 when a box side < this (0 off)
-  int fused_residual = 0;      // residual inside the next V-cycle's first launch (1 on)
   BiCGStabParams bicg;
 };
 
@@ -278,14 +253,6 @@ class MultiGrid {
   void oneCycleFromZeroInto(LevelData &e, const LevelData &r, LevelData &phi) {
     cycle(0, e, const_cast<LevelData &>(r), true, &phi);
   }
-  // the V-cycle of an AMRMultiGrid iteration that starts from phi's
-  // residual: r = rhs - L(phi) (norm into result slot `slot`, see
-  // residualRelaxFromZero), e = 0; oneCycle(e, r); phi += e -- the residual
-  // fused into the first pre-smoothing launch (fusedResidualApplies) or
-  // computed first.  With phi_acc == nullptr, phi is only read.
-  void oneCycleResidualFromZero(LevelData &e, LevelData &r, LevelData &phi, const LevelData &rhs,
-                                bool homogeneous, int normType, int slot, LevelData *phi_acc);
-  bool fusedResidualApplies();
   // full multigrid from the residual r at depth 0: r_{d+1} = R(r_d) at every
   // depth, the bottom solve from zero, then per finer depth e_d = P e_{d+1}
   // and `ncycles` V-cycles on it; phi += e_0 (folded into the last sweep)
@@ -311,15 +278,6 @@ class MultiGrid {
   void cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
              bool halo_out = false);
   std::vector<Level> levels_;
-  // set by oneCycleResidualFromZero for the depth-0 pre-smoothing of that
-  // cycle: the residual's inputs
-  struct FusedRes {
-    LevelData *phi;
-    const LevelData *rhs;
-    bool hom;
-    int normType, slot;
-  };
-  const FusedRes *fres_ = nullptr;
 };
 
 // [Chombo] AMRMultiGrid on a single AMR level: iterations of

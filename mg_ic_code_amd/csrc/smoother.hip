@@ -625,50 +625,6 @@ __global__ __launch_bounds__(NT) void k_gsrb_block(T *__restrict__ uo,
                                               oz + (L / (ntx * nty)) * TZ);
 }
 
-// ---- the boundary slabs of a sweep in one launch -------------------------
-// The cells within `depth` of every exchanged face (the part of the sweep's
-// result a ghost-shell exchange reads), each face's slab tiled with a shape
-// thin across the face: x faces 4x16x8, y faces 32x2x8, z faces 32x8x2
-// tiles.  Same block_tile body (values identical to the whole-box sweep).
-struct SlabTab {
-  int nface;
-  int dir[6];
-  int o[6][3];
-  int nt[6][3];   // tiles per direction
-  int start[7];   // first block of each face
-};
-using BlkX = Blk<4, 16, 8, 256>;
-using BlkY = Blk<32, 2, 8, 256>;
-using BlkZ = Blk<32, 8, 2, 256>;
-constexpr int kSlabLds = BlkX::NREG > BlkY::NREG ? (BlkX::NREG > BlkZ::NREG ? BlkX::NREG : BlkZ::NREG)
-                                                 : (BlkY::NREG > BlkZ::NREG ? BlkY::NREG : BlkZ::NREG);
-
-template <class T, bool ZIN, bool BC>
-__global__ __launch_bounds__(256) void k_gsrb_slabs(T *__restrict__ uo, const T *__restrict__ ui,
-                                                    const T *__restrict__ rhs,
-                                                    const T *__restrict__ a,
-                                                    const T *__restrict__ b, const BoxArgs g,
-                                                    const StencilCoefs s, const SlabTab tab) {
-  __shared__ T R[kSlabLds];
-  __shared__ T B[kSlabLds];
-  const int bid = blockIdx.x;
-  int f = 0;
-  while (f + 1 < tab.nface && bid >= tab.start[f + 1]) ++f;
-  const int L = bid - tab.start[f];
-  const int tx = L % tab.nt[f][0], ty = (L / tab.nt[f][0]) % tab.nt[f][1];
-  const int tz = L / (tab.nt[f][0] * tab.nt[f][1]);
-  const int *o = tab.o[f];
-  if (tab.dir[f] == 0)
-    block_tile<T, 4, 16, 8, 256, ZIN, BC, false>(R, B, uo, nullptr, ui, rhs, a, b, g, s,
-                                                 o[0] + tx * 4, o[1] + ty * 16, o[2] + tz * 8);
-  else if (tab.dir[f] == 1)
-    block_tile<T, 32, 2, 8, 256, ZIN, BC, false>(R, B, uo, nullptr, ui, rhs, a, b, g, s,
-                                                 o[0] + tx * 32, o[1] + ty * 2, o[2] + tz * 8);
-  else
-    block_tile<T, 32, 8, 2, 256, ZIN, BC, false>(R, B, uo, nullptr, ui, rhs, a, b, g, s,
-                                                 o[0] + tx * 32, o[1] + ty * 8, o[2] + tz * 2);
-}
-
 // ---- last pre-smoothing sweep + restrictResidual in one pass -------------
 // The streaming sweep carried one stage deeper so that the residual of the
 // smoothed e can be restricted while its planes are still in LDS
@@ -1253,76 +1209,6 @@ void gsrb_sweep_fused_restrict(double *u_out, double *u_in, const double *rhs, c
                                const double *b, const BoxArgs &g, const StencilCoefs &s,
                                double *rc, const BoxArgs &cg, hipStream_t st) {
   launch_fused_rst<128, 16, 512>(u_out, u_in, rhs, a, b, g, s, rc, cg, st);
-}
-
-void gsrb_sweep_slabs(double *u_out, double *u_in, const double *rhs, const double *a,
-                      const double *b, const BoxArgs &g, const StencilCoefs &s, bool zero_in,
-                      int depth, hipStream_t st) {
-  static const int one_launch = [] {
-    const char *e = getenv("MGIC_SLABS_ONE_LAUNCH");
-    return e ? atoi(e) : 1;
-  }();
-  if (one_launch) {
-    constexpr int tile[3][3] = {{4, 16, 8}, {32, 2, 8}, {32, 8, 2}};
-    SlabTab tab{};
-    int nb = 0;
-    for (int face = 0; face < 6; ++face) {
-      if (g.bcm[face]) continue;  // a domain face: nobody reads a shell there
-      const int dir = face >> 1, side = face & 1;
-      const int n[3] = {g.nx, g.ny, g.nz};
-      int o[3] = {0, 0, 0}, e[3] = {g.nx, g.ny, g.nz};
-      const int d = depth < n[dir] ? depth : n[dir];
-      o[dir] = side == 0 ? 0 : n[dir] - d;
-      e[dir] = d;
-      const int x0 = o[0] & ~1;  // even x origin (16-B pairs)
-      e[0] += o[0] - x0;
-      o[0] = x0;
-      const int f = tab.nface++;
-      tab.dir[f] = dir;
-      tab.start[f] = nb;
-      int cnt = 1;
-      for (int k = 0; k < 3; ++k) {
-        tab.o[f][k] = o[k];
-        tab.nt[f][k] = (e[k] + tile[dir][k] - 1) / tile[dir][k];
-        cnt *= tab.nt[f][k];
-      }
-      nb += cnt;
-    }
-    tab.start[tab.nface] = nb;
-    if (nb == 0) return;
-    const dim3 grid((unsigned)nb), block(256);
-    if (zero_in && s.bconst)
-      k_gsrb_slabs<double, true, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s, tab);
-    else if (zero_in)
-      k_gsrb_slabs<double, true, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s, tab);
-    else if (s.bconst)
-      k_gsrb_slabs<double, false, true><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s, tab);
-    else
-      k_gsrb_slabs<double, false, false><<<grid, block, 0, st>>>(u_out, u_in, rhs, a, b, g, s, tab);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess)
-      throw Error(kHipErr, std::string("slab sweep launch: ") + hipGetErrorString(err));
-    return;
-  }
-  for (int face = 0; face < 6; ++face) {
-    if (g.bcm[face]) continue;  // a domain face: nobody reads a shell there
-    const int dir = face >> 1, side = face & 1;
-    const int n[3] = {g.nx, g.ny, g.nz};
-    int o[3] = {0, 0, 0}, e[3] = {g.nx, g.ny, g.nz};
-    const int d = depth < n[dir] ? depth : n[dir];
-    o[dir] = side == 0 ? 0 : n[dir] - d;
-    e[dir] = d;
-    if (dir == 0) {  // even x origin: widen the slab to the pair boundary
-      const int x0 = o[0] & ~1;
-      e[0] += o[0] - x0;
-      o[0] = x0;
-      launch_block<double, 4, 16, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
-    } else if (dir == 1) {
-      launch_block<double, 32, 2, 8, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
-    } else {
-      launch_block<double, 32, 8, 2, 256>(u_out, u_in, rhs, a, b, g, s, zero_in, nullptr, st, o, e);
-    }
-  }
 }
 
 }  // namespace kern

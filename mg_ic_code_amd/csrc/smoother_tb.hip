@@ -60,69 +60,20 @@ using sweep::bsel;
 template <int N>
 using IC = std::integral_constant<int, N>;
 
-// in-kernel time stamps for tools/tb2_probe.hip (diagnostic builds only)
-#ifndef TB2_STAMP
-#define TB2_STAMP(id, p) ((void)0)
-#endif
-// diagnostic builds of tools/tb2_probe.hip only: bit 0 skips the global
-// loads, bit 1 the colour passes, bit 2 the stores, bit 3 the red (phase A)
-// passes, bit 4 the black (phase B) passes, bit 5 replaces the update chain
-// by six adds of its inputs, bit 6 the divisions, bit 7 the barrier between
-// the red and the black phase, bit 8 the barrier before the red phase, bit 9
-// loads every plane from planes 0 / 1 (L2-resident: the same instructions
-// without the HBM stream), bit 10 drops every store (wrong results, timing)
-#ifndef TB2_PROBE_SKIP
-#define TB2_PROBE_SKIP 0
-#endif
-// measurement switches (A/B builds): TB2_NO_READ2 1 = x-neighbour pairs as
-// two ds_read_b64
-#ifndef TB2_NO_READ2
-#define TB2_NO_READ2 0
-#endif
-// TB2_PF2 1 = loads two steps ahead (plain / ZIN variants); TB2_STORE_CPOL =
-// cache-policy bits of the u_out stores (2 = nt, 16 = sc1: drop the line from L2)
-#ifndef TB2_PF2
-#define TB2_PF2 1
-#endif
-#ifndef TB2_STORE_CPOL
-#define TB2_STORE_CPOL 0
-#endif
-// TB2_NTW 1 = the waves whose loads cover only rows no other tile reads
-// (outside this tile's y halo and outside the y halos of the tiles above and
-// below) load u / rhs / aCoef non-temporally, keeping L2 for the halo lines
-// neighbouring tiles share; the choice is a template parameter of the tile
-// body (the waves run separate code), so no load is selected at run time.
-// (An earlier form selected per load and counted the neighbours' halo rows as
-// private: 1.39 vs 1.08 ms.)
-#ifndef TB2_NTW
-#define TB2_NTW 0
-#endif
-// TB2_STEADY 1 = fp32 launches run the chunk's inner steps as a copy of the
-// step without the z range / face tests and plane clamps, copy the
-// coefficient sets out of the load registers (reg_copy) and issue a static
-// number of u loads per step (see the pipeline loop); fp64 launches keep the
-// generic step (measured neutral there: they are bound by their memory
-// traffic, the fp32 launches more by their instruction stream)
-#ifndef TB2_STEADY
-#define TB2_STEADY 1
-#endif
-// TB2_STEADY_ZIN 1 = fp64 zero-input launches (no u stream, so less bound by
-// memory traffic) take the steady-state step too
-#ifndef TB2_STEADY_ZIN
-#define TB2_STEADY_ZIN 1
-#endif
-// TB2_STEADY_ACC 1 = the fp64 phi += e launches too; TB2_STEADY_ALL
-// (measurement) = every fp64 launch
-#ifndef TB2_STEADY_ACC
-#define TB2_STEADY_ACC 1
-#endif
-#ifndef TB2_STEADY_ALL
-#define TB2_STEADY_ALL 0
-#endif
-// TB2_ZIN_SHORT 0 = ZIN launches run sweep 1 through the generic passes
-#ifndef TB2_ZIN_SHORT
-#define TB2_ZIN_SHORT 1
-#endif
+// Chosen variants (each measured A/B; the rejected ones were
+// removed in round 4 -- their probe builds are in the git history):
+//   kPF2: loads two steps ahead in the plain / ZIN launches (ACC: one);
+//   SDY (steady step): the chunk's inner steps run a copy of the step without the z
+//     range / face tests and plane clamps, with the coefficient sets copied
+//     out of the load registers (reg_copy) and a static number of u loads per
+//     step -- for fp32, zero-input and phi += e launches (the plain fp64
+//     launch is bound by its memory traffic and keeps the generic step);
+//   kZinShort: zero-input launches run sweep-1 red / black without the LDS
+//     reads a zero input makes redundant;
+//   kSkipOut: waves whose rows all lie outside the box skip every pass.
+constexpr bool kPF2 = true;
+constexpr bool kZinShort = true;
+constexpr bool kSkipOut = true;
 
 // Geometry.  Rows of the LDS ring are SHIFTED pairings: in row y of plane k
 // pair m holds cells (X, X+1) with X = x0 - 6 + 2m + s, s = (x0 + y + k +
@@ -134,7 +85,7 @@ using IC = std::integral_constant<int, N>;
 //     red  (m):  x-1, x+1 = B[m-1], B[m];  y+-1, z+-1 = B[m-1+s] of that row / plane
 //     black(m):  x-1, x+1 = R[m], R[m+1];  y+-1, z+-1 = R[m+s]
 // (a neighbouring row or plane has the opposite shift).
-template <int TX, int TY, int NT, int NSL = 8>
+template <int TX, int TY, int NT>
 struct TB2 {
   static_assert(TX % 2 == 0, "TX must be even");
   static constexpr int PW = TX / 2 + 5;            // pairs per LDS row: X = x0-6+s .. x0+TX+2+s
@@ -142,10 +93,7 @@ struct TB2 {
   static constexpr int CP = PW * LH;               // pairs per plane
   static constexpr int SS = CP + 2 * PW + 2;       // slot stride: + a scratch row
   static constexpr int PAD = CP + PW + 1;          // write target of elements never updated
-  // ring slots: 8 (planes p+1 .. p-5 live); the fused-residual launch (RES)
-  // 9: the correction's planes p .. p-5 in slots 0-5 (plane mod 6) and the
-  // input phi's planes p .. p+2 in slots 6-8 (plane mod 3)
-  static constexpr int NS = NSL;
+  static constexpr int NS = 8;                     // ring slots: planes p+1 .. p-5 live
   static constexpr int UW = PW - 1;                // update pairs per row: m = 1 .. PW-1
   static constexpr int NRP = UW * (TY + 6);        // update pairs: rows y0-3 .. y0+TY+2
   static constexpr int NL = (CP + NT - 1) / NT;
@@ -189,7 +137,7 @@ struct TB2Coefs {
       : alpha((T)s.alpha), beta((T)s.beta), dxinv((T)s.dxinv), lamshift((T)s.lamshift),
         bval((T)s.bval) {}
 };
-// A register copy the compiler cannot coalesce (TB2_STEADY, fp32): the
+// A register copy the compiler cannot coalesce (steady steps, fp32): the
 // coefficient sets are copied out of the in-flight load registers, so those
 // keep one register per step parity across the unrolled loop's back edge --
 // coalesced, the four steps' loads landed in four register sets and the back
@@ -197,7 +145,6 @@ struct TB2Coefs {
 // step and undid the two-step prefetch.
 __device__ __forceinline__ double reg_copy(double x) { return x; }
 __device__ __forceinline__ float reg_copy(float x) {
-  if (!TB2_STEADY) return x;
   float y;
   asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
   return y;
@@ -209,29 +156,16 @@ template <> struct TB2Vec<float> { using type = float2; };
 // One tile (x0, y0) of the box, planes [z0, z1).  FAST: alpha == 1, beta ==
 // -1, bval == 1 (exact specialisation, see above); EDGE: the tile's rings
 // reach an x / y domain face (BC code compiled in).
-//
-// RES (with ZIN): the launch that starts an AMRMultiGrid iteration's
-// V-cycle also computes that iteration's residual.  ui is phi and rhs the
-// level's right-hand side; the residual r = rhs - L(phi) (VCCOMPUTERES3D,
-// .ChF:283-339, with the BC of gr) is formed from a 3-plane phi ring on
-// ring 3 of every plane one step before its sweep-1 red pass needs it as
-// the correction equation's right-hand side, carried in the coefficient
-// registers in place of the loaded rhs, and its tile cells are stored to ro
-// (the restriction and the later sweeps read it) while their max |r| goes
-// to *nmax.  Bit-identical to k_residual_z2 followed by the ZIN launch.
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE, bool RES,
-          bool NTW = false>
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE>
 __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                                          T *__restrict__ uo, double *__restrict__ acc,
                                          const T *__restrict__ ui,
                                          const T *__restrict__ rhs,
                                          const T *__restrict__ a, const BoxArgs &g,
                                          const StencilCoefs &s64, const TB2Ghosts<T> &gg, int x0,
-                                         int y0, int z0, int z1, int ef, T *__restrict__ ro,
-                                         const TB2Ghosts<T> &gr, double &nmax) {
+                                         int y0, int z0, int z1, int ef) {
   static_assert(!ACC || std::is_same<T, double>::value, "phi += e is folded into fp64 sweeps only");
-  static_assert(!RES || (ZIN && !ACC), "the fused residual starts a zero-input launch");
-  using F = TB2<TX, TY, NT, RES ? 9 : 8>;
+  using F = TB2<TX, TY, NT>;
   using V = typename TB2Vec<T>::type;
   const TB2Coefs<T> s(s64);
   constexpr int PW = F::PW, CP = F::CP, SS = F::SS, UW = F::UW, NRP = F::NRP, NL = F::NL,
@@ -256,11 +190,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
   // (steady steps: every plane they touch lies inside [-4, nz + 3], no clamp)
   auto plane_u = [&](const T *f, int p) {
-    if (TB2_PROBE_SKIP & 512) p = __builtin_amdgcn_readfirstlane(p & 1);
     return reinterpret_cast<const char *>(f + corner + (long)p * sz);
   };
   auto plane = [&](const T *f, int p) {  // corner of (clamped) plane p
-    if (TB2_PROBE_SKIP & 512) p = __builtin_amdgcn_readfirstlane(p & 1);
     return reinterpret_cast<const char *>(f + corner + (long)clampi(p, -4, nz + 3) * sz);
   };
   // the lane offset is laundered per access: otherwise the compiler hoists
@@ -271,48 +203,13 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     asm volatile("" : "+v"(off));
     return *reinterpret_cast<const V *>(base + off);
   };
-  typedef T VN __attribute__((ext_vector_type(2)));
-  auto at2n = [](const char *base, unsigned off) {  // non-temporal form
-    asm volatile("" : "+v"(off));
-    const VN n = __builtin_nontemporal_load(reinterpret_cast<const VN *>(base + off));
-    V v;
-    v.x = n.x;
-    v.y = n.y;
-    return v;
-  };
   auto boff = [&](int x, int y) {  // byte offset of cell (x, y) from the corner
     return (unsigned)(sizeof(T) * (16 + x + (long)(y + 4) * sy));
   };
-  // ring slot of plane q: es for the correction, ps for the loaded input
-  // (one ring of 8 slots; RES: slots 0-5 and 6-8, q >= pstart - 1 >= -4)
-  auto es = [](int q) -> int {
-    if constexpr (RES) return (q + 12) % 6;
-    else return q & 7;
-  };
-  auto ps = [](int q) -> int {
-    if constexpr (RES) return 6 + (q + 12) % 3;
-    else return q & 7;
-  };
-  // the slot of plane q + j from plane q's slot s0 (scalar adds and
-  // selects: the steps derive every slot from one es / ps per step)
-  auto eadd = [](int s0, int j) -> int {
-    if constexpr (RES) {
-      int v = s0 + j;
-      v = v < 0 ? v + 6 : v;
-      return v >= 6 ? v - 6 : v;
-    } else {
-      return (s0 + j) & 7;
-    }
-  };
-  auto padd = [](int s0, int j) -> int {  // j in 0 .. 2
-    if constexpr (RES) {
-      const int v = s0 + j;
-      return v >= 9 ? v - 3 : v;
-    } else {
-      return (s0 + j) & 7;
-    }
-  };
-
+  // ring slot of plane q (q >= pstart - 1 >= -4), and of plane q + j from
+  // plane q's slot s0 (the steps derive every slot from one slot per step)
+  auto es = [](int q) -> int { return q & 7; };
+  auto eadd = [](int s0, int j) -> int { return (s0 + j) & 7; };
   // ---- loads of u (slot c = LDS pair index), per plane parity t ----------
   // (ghost pairs of x / y domain faces load whatever the ghost cells hold:
   // no pass reads them, see pass)
@@ -350,12 +247,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // two rows both lie outside the box's updatable rows (a tile that overhangs
   // a y domain face, e.g. the last, 6-row tile row at 512 / 22) updates
   // nothing in any pass and skips them all (its elements keep their values,
-  // which is what the passes would write; TB2_SKIP_OUT)
-#ifndef TB2_SKIP_OUT
-#define TB2_SKIP_OUT 1
-#endif
+  // which is what the passes would write; kSkipOut)
   int wthr = 3 - wv;
-  if (TB2_SKIP_OUT && 2 * wv < NR) {
+  if (kSkipOut && 2 * wv < NR) {
     const int ga = y0 - 3 + wv, gb = y0 - 3 + (NR - 1 - wv);
     if ((ga < uylo || ga > uyhi) && (gb < uylo || gb > uyhi)) wthr = 4;
   }
@@ -415,20 +309,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // loads in flight, PF steps ahead (PF 1: u plane p+2 and rhs / aCoef of
   // plane p+1 while step p runs; PF 2: planes p+3 / p+2, one register set
   // per step parity)
-  constexpr int PF = (TB2_PF2 && !ACC) ? 2 : 1;
-  // (RES: the phi planes one step ahead only -- its registers are the
-  // tightest; PFU u register sets)
-  constexpr int PFU = RES ? 1 : PF;
-  // LAMC (RES): lambda is not carried in registers but recomputed where a
-  // pass needs it (two more divisions per step, 16 VGPRs fewer)
-#ifndef TB2_RES_LAMC
-#define TB2_RES_LAMC 1
-#endif
-  constexpr bool LAMC = RES && TB2_RES_LAMC;
-  // (SDY: the fp32 launch's steady-state options, TB2_STEADY)
-  constexpr bool SDY = TB2_STEADY && (std::is_same<T, float>::value || (ZIN && TB2_STEADY_ZIN) ||
-                                      (ACC && TB2_STEADY_ACC) || TB2_STEADY_ALL);
-  T pu0[PFU][NL], pu1[PFU][NL];
+  constexpr int PF = (kPF2 && !ACC) ? 2 : 1;
+  // (SDY: the steady-state step, kSteady above)
+  constexpr bool SDY = std::is_same<T, float>::value || ZIN || ACC;
+  T pu0[PF][NL], pu1[PF][NL];
   T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
@@ -453,7 +337,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     const char *pl = decltype(sd)::value ? plane_u(ui, p) : plane(ui, p == zgl ? 0 : p == zgh ? nz - 1 : p);
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      if ((ZIN && !RES) || (TB2_PROBE_SKIP & 1)) {  // the input is identically +0 (a freshly zeroed correction)
+      if (ZIN) {  // the input is identically +0 (a freshly zeroed correction)
         pu0[b][i] = 0.0;
         pu1[b][i] = 0.0;
       } else if (NL * NT <= CP || SDY || tid + i * NT < CP) {
@@ -461,25 +345,22 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         // loff 0 -- and put skips them, so every step issues a static number
         // of loads and the waits for the loads of two steps ago do not also
         // wait for the previous step's stores)
-        const bool nt = NTW && i == 0;  // (the kernel picks NTW waves by their rows)
-        const V v = nt ? at2n(pl, loff[t][i]) : at2(pl, loff[t][i]);
+        const V v = at2(pl, loff[t][i]);
         pu0[b][i] = v.x;
         pu1[b][i] = v.y;
       }
     }
   };
   // a z ghost plane of a domain face, fetched as the plane it images ->
-  // ParseBC's images (RES: the loaded phi's, with the residual's BC).  (x / y
-  // ghosts are never stored: see pass.)
+  // ParseBC's images.  (x / y ghosts are never stored: see pass.)
   auto image = [&](int p, auto bc, auto sd) {
     constexpr int b = decltype(bc)::value;
-    const TB2Ghosts<T> &G = RES ? gr : gg;
     if (!decltype(sd)::value && (p == zgl || p == zgh)) {
       const int zf = p == -1 ? 4 : 5;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
-        pu0[b][i] = ghost(G, zf, pu0[b][i]);
-        pu1[b][i] = ghost(G, zf, pu1[b][i]);
+        pu0[b][i] = ghost(gg, zf, pu0[b][i]);
+        pu1[b][i] = ghost(gg, zf, pu1[b][i]);
       }
     }
   };
@@ -499,26 +380,17 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     const char *pr = SD ? plane_u(rhs, p) : plane(rhs, p), *pa = SD ? plane_u(a, p) : plane(a, p);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      if (TB2_PROBE_SKIP & 1) {
-        nr0[b][i] = 0.5;
-        nr1[b][i] = 0.25;
-        na0[b][i] = -1.5;
-        na1[b][i] = -1.25;
-        continue;
-      }
-      const bool nt = NTW && NP == 1;
-      const V vr = nt ? at2n(pr, roff[t][i]) : at2(pr, roff[t][i]);
-      const V va = nt ? at2n(pa, roff[t][i]) : at2(pa, roff[t][i]);
+      const V vr = at2(pr, roff[t][i]);
+      const V va = at2(pa, roff[t][i]);
       nr0[b][i] = vr.x;
       nr1[b][i] = vr.y;
       na0[b][i] = va.x;
       na1[b][i] = va.y;
     }
   };
-  auto lam = [&](T aa) { return (TB2_PROBE_SKIP & 64) ? aa + s.lamshift : (T)1 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
+  auto lam = [&](T aa) { return (T)1 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
   auto upd = [&](T uc, T xm, T xp, T ym, T yp, T zm, T zp,
                  T rv, T aa, T lm) -> T {
-    if (TB2_PROBE_SKIP & 32) return ((uc + xm) + (xp + ym)) + ((yp + zm) + zp);
     const T tx = (xp + xm) - (T)2 * uc;
     const T ty = (yp + ym) - (T)2 * uc;
     const T tz = (zp + zm) - (T)2 * uc;
@@ -553,13 +425,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                   const T (&ca)[NP], const T (&cl)[NP]) {
     constexpr int ZC = decltype(zc)::value;
     constexpr bool SD = decltype(sd)::value;  // steady: k in range, not a z face plane
-    if (TB2_PROBE_SKIP & 2) return;
     if (!SD && (unsigned)(k - kl[W]) > kw[W]) return;  // uniform
     // rows beyond ring W (distance > W from the tile) are never read once
     // this pass is done, so waves holding only such rows skip it
     if (NP == 1 && W < wthr) return;  // (one pair per lane only)
-    if ((TB2_PROBE_SKIP & 8) && red) return;
-    if ((TB2_PROBE_SKIP & 16) && !red) return;
     T *X = (red ? R : B) + sk * SS;  // sk = es(k)
     T *N = (red ? B : R) + sk * SS;
     T *Nm = (red ? B : R) + eadd(sk, -1) * SS;
@@ -585,17 +454,8 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       const int c = ci[i];
       const int o = yzo[t][i] + (red ? 0 : 1);  // y / z neighbours: pair m-1+s (red), m+s (black)
       uc[i] = ZC == 2 ? (T)0 : X[c];
-#if TB2_NO_READ2
-      // separate ds_read_b64s: a ds_read2_b64 of the adjacent pair costs 8
-      // LDS cycles against 2 x 2
-      int cx = c + (red ? 0 : 1);
-      asm volatile("" : "+v"(cx));
-      xm[i] = N[c - (red ? 1 : 0)];
-      xp[i] = N[cx];
-#else
       xm[i] = N[c - (red ? 1 : 0)];
       xp[i] = N[c + (red ? 0 : 1)];
-#endif
       ym[i] = N[c + o - PW];
       yp[i] = N[c + o + PW];
       zm[i] = Nm[c + o];
@@ -633,7 +493,6 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // no branch around them and the next step waits vmcnt(2) for its loads
   // instead of vmcnt(0), which would also wait for these stores.
   auto store = [&](int t, int k, int sl, auto sd) {  // sl = es(k)
-    if (TB2_PROBE_SKIP & 4) return;
     constexpr bool SD = decltype(sd)::value;
     const bool kin = SD || (k >= z0 && k < z1);  // uniform
     const int kk = SD ? k : clampi(k, z0, z1 - 1);
@@ -654,103 +513,15 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       const unsigned off = roff[t][i];
       // both elements (st 3) as one pair store; a single one (st 1 / 2, the
       // tile's x edges) as an element store
-      unsigned o4 = st == 3 ? off : kDrop;
-      unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
-      if (TB2_PROBE_SKIP & 1024) {
-        asm volatile("" : "+v"(o4), "+v"(o2));
-        o4 |= kDrop;
-        o2 |= kDrop;
-      }
+      const unsigned o4 = st == 3 ? off : kDrop;
+      const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
       const T e = st == 1 ? w.x : w.y;
-      sweep::bstore<TB2_STORE_CPOL>(rs, w, o4);
-      sweep::bstore<TB2_STORE_CPOL>(rs, e, o2);
-    }
-  };
-  // RES: r = rhs - L(phi) on plane k, both elements of every pair of ring 3
-  // (the pairs sweep-1 red updates), from the phi ring; the loaded rhs of
-  // coefficient set b is replaced by r, which is what the sweeps of plane k
-  // solve against.  The expressions are k_residual_z2's (.ChF:312-336):
-  //   res = rhs - (alpha a) phi; ldpsi = ((L7 dxinv) beta) b; r = res + ldpsi
-  // with x / y domain-face neighbours as gr's ghosts of the cell (ParseBC of
-  // the residual's BC) and z ghost planes imaged in the ring.  The tile's
-  // cells of planes [z0, z1) are stored to ro and enter nmax.
-  auto residual = [&](int t, int k, auto bc, int sm) {  // sm = ps(k - 1)
-    constexpr int b = decltype(bc)::value;
-    if constexpr (RES) {
-      if ((unsigned)(k - kl[3]) > kw[3]) return;  // uniform: outside sweep-1 red's planes
-      const int sc = padd(sm, 1), sq = padd(sm, 2);
-      const T *Rc = R + sc * SS, *Bc = B + sc * SS;
-      const T *Rm = R + sm * SS, *Bm = B + sm * SS;
-      const T *Rq = R + sq * SS, *Bq = B + sq * SS;
-      auto res = [&](T c, T xm, T xp, T ym, T yp, T zm, T zp, T rv, T aa) -> T {
-        const T r0 = rv - s.alpha * aa * c;  // .ChF:314-316
-        const T tx = (xp + xm) - (T)2 * c;
-        const T ty = (yp + ym) - (T)2 * c;
-        const T tz = (zp + zm) - (T)2 * c;
-        T ld = (tx + ty) + tz;                   // .ChF:320-329
-        ld = ld * s.dxinv * s.beta * s.bval;     // .ChF:331
-        return r0 + ld;                          // .ChF:333
-      };
-      const bool kin = k >= z0 && k < z1;  // uniform
-      char *dst = reinterpret_cast<char *>(ro + corner + (long)clampi(k, z0, z1 - 1) * sz);
-      const __amdgpu_buffer_rsrc_t rs = sweep::store_rsrc(dst);
-      constexpr unsigned kDrop = sweep::kDrop;
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int c = ci[i], o = yzo[t][i];
-        // red element: black neighbours at pair m-1, m (x) and m-1+s (y, z)
-        const T u0 = Rc[c];
-        T xm0 = Bc[c - 1], xp0 = Bc[c], ym0 = Bc[c + o - PW], yp0 = Bc[c + o + PW];
-        const T zm0 = Bm[c + o], zp0 = Bq[c + o];
-        // black element: red neighbours at pair m, m+1 (x) and m+s (y, z)
-        const T u1 = Bc[c];
-        T xm1 = Rc[c], xp1 = Rc[c + 1], ym1 = Rc[c + o + 1 - PW], yp1 = Rc[c + o + 1 + PW];
-        const T zm1 = Rm[c + o + 1], zp1 = Rq[c + o + 1];
-        if (EDGE) {
-          const int f0 = rinf[t][i] & 15, f1 = (rinf[t][i] >> 4) & 15;
-          if (ef & 1) {
-            xm0 = (f0 & 1) ? ghost(gr, 0, u0) : xm0;
-            xm1 = (f1 & 1) ? ghost(gr, 0, u1) : xm1;
-          }
-          if (ef & 2) {
-            xp0 = (f0 & 2) ? ghost(gr, 1, u0) : xp0;
-            xp1 = (f1 & 2) ? ghost(gr, 1, u1) : xp1;
-          }
-          if (ef & 4) {
-            ym0 = (f0 & 4) ? ghost(gr, 2, u0) : ym0;
-            ym1 = (f1 & 4) ? ghost(gr, 2, u1) : ym1;
-          }
-          if (ef & 8) {
-            yp0 = (f0 & 8) ? ghost(gr, 3, u0) : yp0;
-            yp1 = (f1 & 8) ? ghost(gr, 3, u1) : yp1;
-          }
-        }
-        const T r0 = res(u0, xm0, xp0, ym0, yp0, zm0, zp0, nr0[b][i], na0[b][i]);
-        __builtin_amdgcn_sched_barrier(0);  // (one element's operands live at a time)
-        const T r1 = res(u1, xm1, xp1, ym1, yp1, zm1, zp1, nr1[b][i], na1[b][i]);
-        nr0[b][i] = r0;
-        nr1[b][i] = r1;
-        // the tile's cells: stored (static store count, as in store) and
-        // into the max norm
-        const int st = kin ? (rinf[t][i] >> 8) & 3 : 0;
-        const unsigned off = roff[t][i];
-        V w;
-        w.x = r0;
-        w.y = r1;
-        const unsigned o4 = st == 3 ? off : kDrop;
-        const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(T) : kDrop);
-        sweep::bstore<TB2_STORE_CPOL>(rs, w, o4);
-        sweep::bstore<TB2_STORE_CPOL>(rs, st == 1 ? r0 : r1, o2);
-        // (max as k_residual_z2 / red_op<3> take it: a > b ? a : b)
-        const double m0 = (st & 1) ? fabs((double)r0) : 0.0;
-        const double m1 = (st & 2) ? fabs((double)r1) : 0.0;
-        nmax = nmax > m0 ? nmax : m0;
-        nmax = nmax > m1 ? nmax : m1;
-      }
+      sweep::bstore(rs, w, o4);
+      sweep::bstore(rs, e, o2);
     }
   };
   // One pipeline step at plane p (t: its parity relative to pstart; ring
-  // slots es(q) / ps(q)), two barriers:
+  // slots es(q)), two barriers:
   //   phase A: sweep-1 red of plane p (ring 3), sweep-2 red of plane p-3 (ring 1)
   //   phase B: sweep-1 black of plane p-1 (ring 2), sweep-2 black of plane
   //            p-4 (the tile) + its store
@@ -758,7 +529,6 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   // cells only, phase B red ones.  Live ring planes p+1 .. p-5; plane p+1 is
   // written over plane p-7.
   auto step = [&](auto tc, auto sd, int p) {
-    static_assert(!RES || PF == 2, "the fused residual keeps loads two steps ahead");
     // J: position in the 4-step unrolled loop; T / U: parity of p / of p +- 1;
     // coefficient sets live in slot J (made this step) .. slot J3 (made
     // three steps ago, last use), so no register moves between steps
@@ -768,30 +538,22 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     using ICF = IC<FB>;
     using SDC = decltype(sd);
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
-    TB2_STAMP(0, p);
     // coefficient sets: black of plane p-1 from the raw black element, red
     // of plane p from its pair fetched last step (alpha * a, .ChF:107)
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       Br[J0][i] = rb[i];
       Ba[J0][i] = FAST ? ab[i] : s.alpha * ab[i];
-      if constexpr (!LAMC) Bl[J0][i] = lam(Ba[J0][i]);
+      Bl[J0][i] = lam(Ba[J0][i]);
       Rr[J0][i] = reg_copy(nr0[FB][i]);
       Ra[J0][i] = FAST ? reg_copy(na0[FB][i]) : s.alpha * na0[FB][i];
-      if constexpr (!LAMC) Rl[J0][i] = lam(Ra[J0][i]);
+      Rl[J0][i] = lam(Ra[J0][i]);
       rb[i] = reg_copy(nr1[FB][i]);
       ab[i] = reg_copy(na1[FB][i]);
     }
-    const int E0 = es(p), P0 = ps(p);  // this step's slots derive from these
-    TB2_STAMP(1, p);
-    if constexpr (RES) {  // phi of plane p+2 into the phi ring (one u register set)
-      image(p + 2, IC<0>{}, SDC{});
-      put(padd(P0, 2), IC<0>{});
-    } else {
-      image(p + 1, ICF{}, SDC{});
-      put(padd(P0, 1), ICF{});
-    }
-    TB2_STAMP(2, p);
+    const int E0 = es(p);  // this step's slots derive from this one
+    image(p + 1, ICF{}, SDC{});
+    put(eadd(E0, 1), ICF{});
     if (PF == 2) fetch_c(PT, p + 2, ICF{}, SDC{});
     else fetch_c(PU, p + 1, ICF{}, SDC{});
     if constexpr (ACC) {
@@ -805,80 +567,32 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
         an1[i] = v.y;
       }
     }
-    if constexpr (RES) fetch_u(PU, p + 3, IC<0>{}, SDC{});
-    else if (PF == 2) fetch_u(PU, p + 3, ICF{}, SDC{});
+    if (PF == 2) fetch_u(PU, p + 3, ICF{}, SDC{});
     else fetch_u(PT, p + 2, ICF{}, SDC{});
-    TB2_STAMP(3, p);
-    if (!(TB2_PROBE_SKIP & 256)) __syncthreads();
-    TB2_STAMP(4, p);
-    // RES: r of plane p+1 (phi planes p .. p+2 are in the phi ring) into the
-    // coefficient set that step p+1 turns into plane p+1's sweep-1 inputs
-    if constexpr (RES) {
-      residual(PU, p + 1, IC<FB ^ 1>{}, P0);
-      // a z ghost plane of the (zero) correction: its red elements image the
-      // black cells of the face plane, which are 0 until sweep-1 black reads
-      // them (the plain ZIN launch puts those images with the zero input;
-      // here the correction's slots are never put).  Its black elements are
-      // written by the face plane's sweep-1 red pass before any read.  (The
-      // slot's previous plane was last read in step p-1's black phase.)
-      if (p == zgl || p == zgh) {
-        const T g0 = ghost(gg, p == zgl ? 4 : 5, (T)0);
-        T *Rs = R + E0 * SS;
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-          if (NL * NT > CP && tid + i * NT >= CP) continue;
-          Rs[tid + i * NT] = g0;
-        }
-      }
-    }
-    // (LAMC: lambda recomputed from alpha*a where a pass needs it)
-    auto lamv = [&](const T(&aa)[NP], T(&out)[NP]) {
-#pragma unroll
-      for (int i = 0; i < NP; ++i) out[i] = lam(aa[i]);
-    };
-    T lt[NP];
-    if constexpr (LAMC) lamv(Ra[J0], lt);
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 1 : 0>{}, SDC{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], LAMC ? lt : Rl[J0]);
-    if constexpr (LAMC) lamv(Ra[J3], lt);
-    pass(IC<0>{}, SDC{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], LAMC ? lt : Rl[J3]);
-    TB2_STAMP(5, p);
-    if (!(TB2_PROBE_SKIP & 128)) __syncthreads();
-    TB2_STAMP(6, p);
-    if constexpr (LAMC) lamv(Ba[J0], lt);
-    pass(IC<(ZIN && TB2_ZIN_SHORT) ? 2 : 0>{}, SDC{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], LAMC ? lt : Bl[J0]);
-    if constexpr (LAMC) lamv(Ba[J3], lt);
-    pass(IC<0>{}, SDC{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], LAMC ? lt : Bl[J3]);
-    TB2_STAMP(7, p);
+    __syncthreads();
+    pass(IC<(ZIN && kZinShort) ? 1 : 0>{}, SDC{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], Rl[J0]);
+    pass(IC<0>{}, SDC{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], Rl[J3]);
+    __syncthreads();
+    pass(IC<(ZIN && kZinShort) ? 2 : 0>{}, SDC{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], Bl[J0]);
+    pass(IC<0>{}, SDC{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], Bl[J3]);
     store(PT, p - 4, eadd(E0, -4), SDC{});
-    TB2_STAMP(8, p);
   };
 
   fetch_u(1, pstart - 1, IC<0>{}, IC<0>{});
   image(pstart - 1, IC<0>{}, IC<0>{});
-  put(ps(pstart - 1), IC<0>{});
+  put(es(pstart - 1), IC<0>{});
   fetch_u(0, pstart, IC<0>{}, IC<0>{});
   image(pstart, IC<0>{}, IC<0>{});
-  put(ps(pstart), IC<0>{});
+  put(es(pstart), IC<0>{});
   fetch_u(1, pstart + 1, IC<0>{}, IC<0>{});
-  if constexpr (RES) {  // phi planes pstart-1 .. pstart+1 in the ring, r of plane pstart
-    image(pstart + 1, IC<0>{}, IC<0>{});
-    put(ps(pstart + 1), IC<0>{});
-    fetch_u(0, pstart + 2, IC<0>{}, IC<0>{});
-    fetch_c(0, pstart, IC<0>{}, IC<0>{});
-    fetch_c(1, pstart + 1, IC<1>{}, IC<0>{});
-    __syncthreads();
-    residual(0, pstart, IC<0>{}, ps(pstart - 1));
-    __syncthreads();  // (step pstart's put overwrites phi plane pstart-1)
-  } else {
-    fetch_c(0, pstart, IC<0>{}, IC<0>{});
-    if (PF == 2) {
-      fetch_u(0, pstart + 2, IC<PF - 1>{}, IC<0>{});
-      fetch_c(1, pstart + 1, IC<PF - 1>{}, IC<0>{});
-    }
+  fetch_c(0, pstart, IC<0>{}, IC<0>{});
+  if (PF == 2) {
+    fetch_u(0, pstart + 2, IC<PF - 1>{}, IC<0>{});
+    fetch_c(1, pstart + 1, IC<PF - 1>{}, IC<0>{});
   }
   // (up to three steps past pend: their passes and stores fall outside every
   // range test, their loads are clamped)
-  // Steady 4-step groups (TB2_STEADY): steps p .. p+3 with z0 + 5 <= p and
+  // Steady 4-step groups (SDY): steps p .. p+3 with z0 + 5 <= p and
   // p + 3 <= z1 - 4.  Every pass of such a step is inside its z range (the
   // tile pass needs p - 4 >= z0, the others less), none is on a domain face
   // plane (p - 4 >= 1 > 0, p <= nz - 4 < nz - 1), the loaded planes p + 2,
@@ -895,7 +609,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   };
   const int ssh = z1 - 7;
   int p = pstart;
-  if (!RES && SDY) {
+  if (SDY) {
     for (; p < pstart + 8 && p <= pend; p += 4) group(IC<0>{}, p);
     for (; p <= ssh; p += 4) group(IC<1>{}, p);
   }
@@ -903,7 +617,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 }
 
 
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool RES = false>
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST>
 __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  double *__restrict__ acc,
                                                  const T *__restrict__ ui,
@@ -911,10 +625,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  const T *__restrict__ a,
                                                  const BoxArgs g, const StencilCoefs s,
                                                  const TB2Ghosts<T> gg, int kc, int ntx, int nty,
-                                                 int nblocks, T *__restrict__ ro,
-                                                 const TB2Ghosts<T> gr,
-                                                 double *__restrict__ parts) {
-  using F = TB2<TX, TY, NT, RES ? 9 : 8>;
+                                                 int nblocks) {
+  using F = TB2<TX, TY, NT>;
   __shared__ T R[F::NS * F::SS];  // red element of every pair, one per ring slot
   __shared__ T B[F::NS * F::SS];  // black element
   const int L = sweep::xcd_tile(blockIdx.x, nblocks);
@@ -924,55 +636,22 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   // uniform: the x / y domain faces the tile's rings (3 cells) reach
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
-  double nmax = 0.0;  // RES: max |r| over this workgroup's tile cells
-  // TB2_NTW: the waves whose u rows (first load: pairs 64w .. 64w+63 of the
-  // plane, PW per row) and rhs / aCoef rows (update rows w and TY+5-w) all
-  // lie in rows no other tile reads: LDS rows 8 .. TY-1, update rows 6 .. TY-1
-  using F0 = TB2<TX, TY, NT>;
-  constexpr int kNtLo = (8 * F0::PW + 63) / 64 > 6 ? (8 * F0::PW + 63) / 64 : 6;
-  constexpr int kNtHi = (TY * F0::PW) / 64 - 1 < TY + 5 - 6 ? (TY * F0::PW) / 64 - 1 : TY - 1;
-  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const bool ntw = TB2_NTW && !RES && (NT / 64) >= kNtHi && wv >= kNtLo && wv <= kNtHi &&
-                   (TY + 5 - wv) <= TY - 1;
-  if (ef) {
-    if (ntw)
-      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, RES, true>(R, B, uo, acc, ui, rhs, a, g, s, gg,
-                                                               x0, y0, z0, z1, ef, ro, gr, nmax);
-    else
-      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
-                                                         z0, z1, ef, ro, gr, nmax);
-  } else {
-    if (ntw)
-      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, RES, true>(R, B, uo, acc, ui, rhs, a, g, s, gg,
-                                                                x0, y0, z0, z1, 0, ro, gr, nmax);
-    else
-      tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, RES>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0,
-                                                          y0, z0, z1, 0, ro, gr, nmax);
-  }
-  if constexpr (RES) {  // the workgroup's partial of the max norm
-    __shared__ double wmax[NT / 64];
-    for (int o = 32; o > 0; o >>= 1) {
-      const double v = __shfl_xor(nmax, o, 64);
-      nmax = nmax > v ? nmax : v;
-    }
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = nmax;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double m = wmax[0];
-      for (int w = 1; w < NT / 64; ++w) m = m > wmax[w] ? m : wmax[w];
-      parts[blockIdx.x] = m;
-    }
-  }
+  if (ef)
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
+                                                  z1, ef);
+  else
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
+                                                   z0, z1, 0);
 }
 
-template <class T, int TX, int TY, int NT, bool RES = false>
+template <class T, int TX, int TY, int NT>
 int tb2_resident_slots() {
   static const int slots = [] {
     int dev = 0, ncu = 0, per = 0;
     MGIC_HIP(hipGetDevice(&dev));
     MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     MGIC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per, k_gsrb_tb2<T, TX, TY, NT, RES, false, true, RES>, NT, 0));
+        &per, k_gsrb_tb2<T, TX, TY, NT, false, false, true>, NT, 0));
     return (per > 0 ? per : 1) * (ncu > 0 ? ncu : 1);
   }();
   return slots;
@@ -996,7 +675,7 @@ int tb2_choose_kc(int tiles, int nz, int slots) {
 }
 
 // the launch geometry of one two-sweep launch (tiles, z chunk, blocks)
-template <class T, int TX, int TY, int NT, bool RES = false>
+template <class T, int TX, int TY, int NT>
 struct TB2Geom {
   int ntx, nty, kc, nblocks;
   explicit TB2Geom(const BoxArgs &g) {
@@ -1012,7 +691,7 @@ struct TB2Geom {
       return e ? atoi(e) : 0;
     }();
     kc = kc_env >= 8 ? (kc_env < g.nz ? kc_env : g.nz)
-                     : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<T, TX, TY, NT, RES>());
+                     : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<T, TX, TY, NT>());
     nblocks = ntx * nty * ((g.nz + kc - 1) / kc);
   }
 };
@@ -1031,8 +710,7 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
         throw Error(kBadArg, "two-sweep launch: zero input under an inhomogeneous BC");
 #define MGIC_TB2(Z, A, FA)                                                                        \
   k_gsrb_tb2<T, TX, TY, NT, Z, A, FA><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, g, s, gg, \
-                                                              kc, ntx, nty, nblocks, nullptr, gg, \
-                                                              nullptr)
+                                                              kc, ntx, nty, nblocks)
   if (acc) {
     if constexpr (std::is_same<T, double>::value) {
       if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
@@ -1053,46 +731,7 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   if (e != hipSuccess) throw Error(kHipErr, std::string("two-sweep launch: ") + hipGetErrorString(e));
 }
 
-// the fused-residual launch (RES): 64 x 20 tiles, so that the 9-slot ring
-// (156 KB) fits the 160 KB of LDS (TB2_RES_TY: measurement builds; 18 has
-// one u load per lane)
-#ifndef TB2_RES_TY
-#define TB2_RES_TY 20
-#endif
-constexpr int kResTY = TB2_RES_TY;
-
 }  // namespace
-
-long gsrb_sweep_tb2_res_blocks(const BoxArgs &g) {
-  return TB2Geom<double, 64, kResTY, 1024, true>(g).nblocks;
-}
-
-void gsrb_sweep_tb2_res(double *e_out, double *r_out, const double *phi, const double *rhs,
-                        const double *a, const BoxArgs &g_hom, const BoxArgs &g_res,
-                        const StencilCoefs &s, double *partials, hipStream_t st) {
-  constexpr int TX = 64, TY = kResTY, NT = 1024;
-  const TB2Geom<double, TX, TY, NT, true> G(g_hom);
-  const dim3 grid((unsigned)G.nblocks), block(NT);
-  const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0;
-  const TB2Ghosts<double> gg = make_ghosts<double>(g_hom), gr = make_ghosts<double>(g_res);
-  for (int f = 0; f < 6; ++f) {
-    if (g_hom.bcm[f] == kBcMemory || g_res.bcm[f] == kBcMemory)
-      throw Error(kBadArg, "fused-residual launch: exchanged faces are not supported");
-    if (gg.c[f] != 0.0)
-      throw Error(kBadArg, "fused-residual launch: the correction's BC must be homogeneous");
-  }
-  if (fast)
-    k_gsrb_tb2<double, TX, TY, NT, true, false, true, true><<<grid, block, 0, st>>>(
-        e_out, nullptr, phi, rhs, a, g_hom, s, gg, G.kc, G.ntx, G.nty, G.nblocks, r_out, gr,
-        partials);
-  else
-    k_gsrb_tb2<double, TX, TY, NT, true, false, false, true><<<grid, block, 0, st>>>(
-        e_out, nullptr, phi, rhs, a, g_hom, s, gg, G.kc, G.ntx, G.nty, G.nblocks, r_out, gr,
-        partials);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess)
-    throw Error(kHipErr, std::string("fused-residual launch: ") + hipGetErrorString(e));
-}
 
 bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
   if (!s.bconst || kind == 0 || kind == 3) return false;
@@ -1104,23 +743,17 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
   return g.nx >= 8 && g.ny >= 8 && g.nz >= 8;
 }
 
-// tile shape (MGIC_TB2_VARIANT, measurement): a thread owns one x pair of
-// the update region ((TX/2 + 4) x (TY + 6) pairs <= NT) and carries its
-// coefficient sets in registers; 1024 threads = four waves per SIMD at 128
-// VGPRs.  0: 64 x 22 with 1024 threads (one pair each, 148 KB LDS),
-// 1: the same tile with 512 threads and two pairs each (measured 1.79 vs
-// 1.53 ms per 512^3 launch: fewer waves hide less of the pass latency).
-// 58 x 22 (one u load per lane, 924 busy lanes) measured 1.53 vs 1.36 ms:
-// a step costs about the same whatever the tile, so wide tiles win
+// tile shape: a thread owns one x pair of the update region ((TX/2 + 4) x
+// (TY + 6) pairs <= NT) and carries its coefficient sets in registers; 1024
+// threads = four waves per SIMD at 128 VGPRs, 64 x 22 tiles (148 KB LDS).
+// Measured and not kept: the same tile with 512 threads and two pairs each
+// (1.79 vs 1.53 ms per 512^3 launch: fewer waves hide less of the pass
+// latency); 58 x 22 (one u load per lane) 1.53 vs 1.36 ms -- a step costs
+// about the same whatever the tile, so wide tiles win
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
                     hipStream_t st) {
-  static const int v = [] {
-    const char *e = getenv("MGIC_TB2_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
-  if (v == 1) launch_tb2<double, 64, 22, 512>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
-  else launch_tb2<double, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+  launch_tb2<double, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
 }
 
 // fp32 (the mixed-precision V-cycle's smoother, BASELINE config C5): the same

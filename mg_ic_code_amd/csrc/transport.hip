@@ -35,14 +35,14 @@ __device__ __forceinline__ void st_word(unsigned long long *p, unsigned long lon
 // bounded poll of *w >= v; false on timeout (recorded in *err) or when an
 // earlier timeout of this rank is already recorded (fail fast, never hang)
 __device__ bool ipc_wait(const unsigned long long *w, unsigned long long v,
-                         unsigned long long *err) {
+                         unsigned long long *err, unsigned long long timeout) {
   if (ld_sys(w) >= v) return true;
   const unsigned long long t0 = wall_clock64();
   for (;;) {
     __builtin_amdgcn_s_sleep(1);
     if (ld_sys(w) >= v) return true;
     if (ld_sys(err) != 0) return false;
-    if (wall_clock64() - t0 > kIpcTimeoutTicks) {
+    if (wall_clock64() - t0 > timeout) {
       __hip_atomic_fetch_add(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
@@ -153,7 +153,7 @@ __device__ __forceinline__ void put_share(const CopyItem &it, int sub, T *const 
                                           const IpcPeers &pp, int &ok) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   const int p = __builtin_amdgcn_readfirstlane(it.pad);
-  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err);  // slot free
+  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err, pp.timeout);  // slot free
   __syncthreads();
   if (ok) {
     const T *src = src_tab[it.src] + it.soff;
@@ -179,7 +179,7 @@ __device__ __forceinline__ void get_share(const CopyItem &it, int sub, T *const 
                                           const IpcPeers &pp, int &ok) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   const int p = __builtin_amdgcn_readfirstlane(it.pad);
-  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err);  // message complete
+  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err, pp.timeout);  // message complete
   __syncthreads();
   if (ok) {
     T *dst = dst_tab[it.dst] + it.doff;
@@ -221,14 +221,12 @@ __device__ __forceinline__ void local_share(const CopyItem &it, int sub, T *cons
 
 // one exchange in one launch: virtual blocks [0, npu) put my messages (first,
 // so the peers can start), [npu, npu + nlo) copy the same-rank regions, the
-// rest get my messages.  Without a cap every virtual block is a workgroup,
-// dispatched in index order, so a get block that waits on this launch's own
-// put blocks (self messages) never holds back a put block that has not
-// started.  With a cap (ranks sharing one device, Comm::ipc_grid_cap) the
-// workgroups stride over the virtual blocks in ascending order: a workgroup
-// has done all its puts before its first get, and the capped grids of every
-// rank on the device fit on it at once beside the other ranks' kernels, so a
-// rank's get blocks cannot hold the CU slots its peers' put blocks need.
+// rest get my messages.  The workgroups stride over the virtual blocks in
+// ascending order, so a workgroup has done all its puts before its first
+// get, and the grid is capped (Comm::ipc_grid_cap) so that every rank's
+// exchange workgroups on a device fit on it at once: no get -- of a peer's
+// message or of this launch's own self messages -- can hold the CU slot of
+// a put that has not started, whatever order workgroups are dispatched in.
 template <class T>
 __global__ __launch_bounds__(256) void k_exchange(const CopyItem *__restrict__ put_items,
                                                   const CopyItem *__restrict__ loc_items,
@@ -260,7 +258,8 @@ __global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned
   for (int q = 0; q < r.size; ++q) st_word(r.sig[q] + kSigRedCnt + r.rank * kSigStride, r.count);
   unsigned long long *mine = r.sig[r.rank];
   bool ok = true;
-  for (int q = 0; q < r.size && ok; ++q) ok = ipc_wait(mine + kSigRedCnt + q * kSigStride, r.count, err);
+  for (int q = 0; q < r.size && ok; ++q)
+    ok = ipc_wait(mine + kSigRedCnt + q * kSigStride, r.count, err, r.timeout);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   if (!ok) return;
   double acc = __longlong_as_double(ld_sys(mine + kSigRedVal + r.parity * 1024));
@@ -286,7 +285,7 @@ static void exchange_t(const CopyItem *put_items, const CopyItem *loc_items,
                        const IpcPeers &pget, int grid_cap, hipStream_t st) {
   const int n = npu + nlo + nge;
   if (n <= 0) return;
-  const int g = grid_cap > 0 && grid_cap < n ? grid_cap : n;
+  const int g = grid_cap > 0 && grid_cap < n ? grid_cap : n;  // (the Comm always caps)
   k_exchange<T><<<dim3((unsigned)g), dim3(256), 0, st>>>(put_items, loc_items, get_items, blocks,
                                                          npu, nlo, n, src_tab, dst_tab, pput, pget);
   check_launch();

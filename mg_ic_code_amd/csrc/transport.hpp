@@ -16,7 +16,8 @@
 // Both sides split an item into blocks the same way (ipc_blocks), so the
 // counters count blocks; they are cumulative per (sender, receiver) pair, so
 // nothing is ever reset, and no ticket or last-block step is needed.  Every
-// poll is bounded in time and records a timeout in the error word
+// poll is bounded in time (MGIC_IPC_TIMEOUT_S, default 10 s) and records a
+// timeout in the error word
 // (Comm::ipc_check raises it on the host) instead of hanging the GPU.  The
 // same kernels serve a single process with self messages (tests).
 #pragma once
@@ -39,11 +40,11 @@ constexpr int kSigErr = 2064;        // timeouts observed by this rank
 constexpr int kSigRedCnt = 3072;     // red_cnt[r]: allreduce contributions of rank r
 constexpr int kSigRedVal = 4096;     // val[parity][r] at kSigRedVal + parity * 1024 + r * 16
 constexpr int kSigWords = 8192;      // 64 KB
-constexpr unsigned long long kIpcTimeoutTicks = 1000000000ull;  // 10 s of the 100 MHz clock
 
 struct IpcPeers {
   int n;                                         // peers of this launch
   unsigned long long *err;                       // my error word
+  unsigned long long timeout;                    // bound of every wait (100 MHz ticks)
   unsigned long long *count[kMaxIpcPeers];       // +1 per block when done (a peer's page)
   const unsigned long long *wait[kMaxIpcPeers];  // polled before a block copies (my page)
   unsigned long long wait_val[kMaxIpcPeers];
@@ -60,6 +61,7 @@ inline long ipc_blocks(long cells) { return (cells + kIpcBlockElems - 1) / kIpcB
 struct IpcReduce {
   int size, rank, parity;
   unsigned long long count;                    // this allreduce's number (1-based)
+  unsigned long long timeout;                  // bound of every wait (100 MHz ticks)
   unsigned long long *sig[kMaxIpcRanks];       // every rank's signal page (mine at [rank])
 };
 
@@ -68,8 +70,8 @@ struct IpcReduce {
 // index in pput), then nlo same-rank copy blocks (loc_items), then nge get
 // blocks (items: dst = local box, soff = offset in the sender's message, pad =
 // peer index in pget).  Every item is split into ipc_blocks(cells) blocks.
-// grid_cap > 0: at most that many workgroups, striding over the blocks (ranks
-// that share a device; see k_exchange).
+// At most grid_cap workgroups, striding over the blocks in ascending order
+// (every workgroup's puts before its gets; see k_exchange and Comm).
 void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
                   const IpcBlock *blocks, int npu, int nlo, int nge, double *const *src_tab,
                   double *const *dst_tab, const IpcPeers &pput, const IpcPeers &pget,

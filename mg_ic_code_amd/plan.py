@@ -75,6 +75,12 @@ class HostPlan:
                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)))
         return out
 
+    def check_transport(self, transport: str) -> None:
+        """Build the host tables `transport` ("rccl" / "ipc") executes this
+        plan with; raises when it cannot (the peer-mapped transport takes at
+        most 32 peers per plan)."""
+        _lib.call("mgic_plan_check_transport", self._h, {"rccl": 1, "ipc": 2}[transport])
+
     def geom(self, layout, n):
         """(sy, sz, origin, total) of local box n; layout 0 = src, 1 = dst."""
         g = (ctypes.c_longlong * 4)()

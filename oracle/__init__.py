@@ -106,6 +106,7 @@ _sig = {
                         POINTER(c_double), POINTER(c_double), POINTER(c_double)],
     "orc_set_threads": [c_int],
     "orc_get_threads": [],
+    "orc_pin_threads": [PI, c_int, c_int],
 }
 _res = {"orc_mg_create": ctypes.c_void_p, "orc_mg_dx": c_double, "orc_mg_iteration": c_double, "orc_mg_fmg": c_double,
         "orc_mg_init_residual": c_double, "orc_mg_norm": c_double, "orc_mg_dot": c_double}
@@ -113,7 +114,8 @@ for _n, _a in _sig.items():
     _f = getattr(_lib, _n)
     _f.argtypes = _a
     _f.restype = _res.get(_n, c_int if _n in ("orc_mg_nlevels", "orc_mg_bicgstab",
-                                               "orc_mg_last_bicg_iters", "orc_get_threads")
+                                               "orc_mg_last_bicg_iters", "orc_get_threads",
+                                               "orc_pin_threads")
                           else None)
 _lib.orc_mg_solve.restype = c_int
 
@@ -253,6 +255,13 @@ def set_threads(n: int) -> None:
 
 def get_threads() -> int:
     return _lib.orc_get_threads()
+
+
+def pin_threads(cpus, pin: bool = True) -> int:
+    """Pin OpenMP thread t to cpus[t] (pin) or release every thread to the
+    set `cpus` (the process's own CPUs); returns the threads set."""
+    arr = (c_int * max(1, len(cpus)))(*cpus)
+    return _lib.orc_pin_threads(arr, len(cpus), int(bool(pin)))
 
 
 class OracleMG:

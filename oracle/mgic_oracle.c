@@ -19,6 +19,7 @@
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
+#include <sched.h>
 #endif
 
 /* ------------------------------------------------------------------ */
@@ -1075,5 +1076,33 @@ int orc_get_threads(void) {
   return omp_get_max_threads();
 #else
   return 1;
+#endif
+}
+
+/* Pin OpenMP thread t of the next parallel regions to cpus[t % n] (n > 0),
+ * or release every thread to the process's CPU set cpus[0 .. n) (pin = 0):
+ * the CPU baseline's "all host cores, pinned" (SURVEY 8(d)).  Returns the
+ * number of threads whose affinity was set. */
+int orc_pin_threads(const int *cpus, int n, int pin) {
+#ifdef _OPENMP
+  if (n <= 0) return 0;
+  int done = 0;
+#pragma omp parallel reduction(+ : done)
+  {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (pin) {
+      CPU_SET(cpus[omp_get_thread_num() % n], &set);
+    } else {
+      for (int i = 0; i < n; ++i) CPU_SET(cpus[i], &set);
+    }
+    done += sched_setaffinity(0, sizeof(set), &set) == 0;
+  }
+  return done;
+#else
+  (void)cpus;
+  (void)n;
+  (void)pin;
+  return 0;
 #endif
 }

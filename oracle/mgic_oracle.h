@@ -195,6 +195,7 @@ void orc_output_vars(int kind, const orc_bh_params *p, const int *lo, const int 
 
 void orc_set_threads(int n);
 int orc_get_threads(void);
+int orc_pin_threads(const int *cpus, int n, int pin);
 
 #ifdef __cplusplus
 }

@@ -309,3 +309,26 @@ def test_bench_split_deep_halo_two_sweeps_match_single_box_oracle(world):
     o.level_gsrb(0, oracle.PHI, oracle.RHS)
     o.level_gsrb(0, oracle.PHI, oracle.RHS)
     assert np.array_equal(got, o.get(0, oracle.PHI, 0))
+
+
+def test_gather_plan_with_many_peers_is_rccl_executable():
+    # the coarse-level gather of a 40-rank job onto rank 0 receives from 39
+    # peers: RCCL executes such a plan (its tables are built whatever the
+    # peer count); the peer-mapped transport, whose launch tables hold at most
+    # 32 peers, refuses it -- and only a plan that transport executes builds
+    # its tables (an RCCL job must not trip the IPC peer limit)
+    from mg_ic_code_amd._lib import MgicError
+    world = 40
+    dom = (0, 0, 0, 79, 31, 15)
+    boxes = split_domain(dom, (10, 2, 2))
+    owners = list(range(world))
+    plan = HostPlan(0, world, dom, boxes, owners, dst_boxes=[dom], dst_owners=[0],
+                    with_valid=True, with_faces=False)
+    assert len(plan.peers) == world - 1
+    plan.check_transport("rccl")
+    with pytest.raises(MgicError, match="too many peers"):
+        plan.check_transport("ipc")
+    # a rank's own face-exchange plan (at most 26 neighbours) suits both
+    ex = HostPlan(5, world, dom, boxes, owners)
+    ex.check_transport("rccl")
+    ex.check_transport("ipc")

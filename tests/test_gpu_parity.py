@@ -138,7 +138,7 @@ def test_chf_dropin_op_res_restrict_bitwise(rng):
 # ----------------------------------------------------------------- operator level
 def build_pair(comm, rng, n, parts, *, alpha=1.0, beta=-1.0, avg=1, prolong=1, bc_lo=(0, 0, 0),
                bc_hi=(0, 0, 0), bc_value=0.0, periodic=(0, 0, 0), nlevels=3, bottom=0,
-               relax_mode=1, agglomerate_below=0, fused=1, bvar=True, overlap=1, deep=0):
+               relax_mode=1, agglomerate_below=0, fused=1, bvar=True, deep=0):
     dom = (0, 0, 0, n - 1, n - 1, n - 1)
     dx = 100.0 / n
     boxes = split_domain(dom, parts)
@@ -152,7 +152,7 @@ def build_pair(comm, rng, n, parts, *, alpha=1.0, beta=-1.0, avg=1, prolong=1, b
     fphi.set_zero()
     prm = mg.OperatorParams(alpha=alpha, beta=beta, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bc_value,
                             coefficient_average_type=avg, prolong_type=prolong,
-                            relax_mode=relax_mode, fused_smoother=fused, overlap_exchange=overlap,
+                            relax_mode=relax_mode, fused_smoother=fused,
                             deep_halo=deep)
     fac = mg.defineOperatorFactory(grid, fa, fb, prm)
     amg = mg.AMRMultiGrid(fac, mg.SolverParams(max_depth=nlevels - 1, bottom_solver=bottom,
@@ -250,11 +250,10 @@ def test_fill_bc_matches_oracle(comm, rng):
 @pytest.mark.parametrize("parts,prolong,avg", [((1, 1, 1), 1, 1), ((1, 1, 1), 0, 0),
                                                ((2, 2, 2), 1, 1), ((2, 1, 2), 0, 1)])
 @pytest.mark.parametrize("fused", [2, 3])  # z-streaming / 3D-block sweep kernel
-@pytest.mark.parametrize("overlap", [0, 2, 4])  # halo exchange on a second stream
-def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused, overlap):
+def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused):
     n = 32
     S = build_pair(comm, rng, n, parts, prolong=prolong, avg=avg, nlevels=3, bottom=0,
-                   fused=fused, overlap=overlap)
+                   fused=fused)
     amg, o = S["amg"], S["o"]
     assert amg.num_depths == 3
     amg.init_residual(S["fphi"], S["frhs"], S["fres"])
@@ -305,8 +304,7 @@ def test_vcycle_ragged_mixed_bc_bitwise(rng, comm, fused, bvar):
 
 @pytest.mark.parametrize("transport", ["rccl", "ipc"])
 @pytest.mark.parametrize("fused", [2, 3])
-@pytest.mark.parametrize("overlap", [0, 2, 4])
-def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, overlap, transport):
+def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, transport):
     # the remote path (RCCL pack -> send/recv -> unpack, or the peer-mapped
     # put / get kernels), exercised on one GPU by routing same-rank copies
     # through self messages
@@ -316,7 +314,7 @@ def test_vcycle_periodic_multibox_rccl_self_messages(rng, fused, overlap, transp
     out = []
     for c in (c_local, c_rccl):
         S = build_pair(c, np.random.default_rng(7), n, (2, 2, 2), periodic=(1, 1, 1), alpha=1.0,
-                       nlevels=3, bottom=0, fused=fused, overlap=overlap)
+                       nlevels=3, bottom=0, fused=fused)
         amg = S["amg"]
         amg.init_residual(S["fphi"], S["frhs"], S["fres"])
         norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
@@ -343,11 +341,9 @@ def test_bicgstab_bottom_within_tolerance(comm, rng):
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
 
 
-@pytest.mark.parametrize("overlap", [0, 2, 4])
-def test_agglomerated_hierarchy_matches_single_box(comm, rng, overlap):
+def test_agglomerated_hierarchy_matches_single_box(comm, rng):
     n = 32
-    S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16,
-                   overlap=overlap)
+    S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16)
     amg, o = S["amg"], S["o"]
     assert amg.num_depths == 5
     amg.init_residual(S["fphi"], S["frhs"], S["fres"])
@@ -372,14 +368,14 @@ def test_binary_bh_inputs_on_device(comm):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("fused,overlap", [(2, 0), (3, 2), (2, 2), (2, 4), (3, 4)])
-def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused, overlap):
+@pytest.mark.parametrize("fused", [2, 3])
+def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused):
     # 128^3: GPU single box == GPU 8 boxes == oracle, bit for bit
     n = 128
     res = []
     for parts in ((1, 1, 1), (2, 2, 2)):
         S = build_pair(comm, np.random.default_rng(11), n, parts, nlevels=3, bottom=0, bvar=False,
-                       fused=fused, overlap=overlap)
+                       fused=fused)
         amg = S["amg"]
         amg.init_residual(S["fphi"], S["frhs"], S["fres"])
         norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
@@ -392,30 +388,6 @@ def test_large_vcycle_single_vs_multibox_and_oracle(comm, fused, overlap):
     assert onorms == res[0][0]
     assert np.array_equal(o.get(0, oracle.PHI, 0), res[0][1])
     assert onorms[1] < onorms[0]
-
-
-@pytest.mark.parametrize("rccl", [False, True])
-def test_overlapped_halo_large_periodic_box_bitwise(rng, rccl):
-    # 192^3 periodic single box (six exchanged faces): the side-stream slab
-    # sweeps + ghost-shell exchange must reproduce the serial schedule bit for
-    # bit (a missing stream dependency shows up here as a changed result)
-    if rccl:
-        c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
-        c.set_self_messages(True)
-    else:
-        c = mg.Comm()
-    n = 192
-    out = []
-    for overlap in (0, 2, 4):
-        S = build_pair(c, np.random.default_rng(5), n, (1, 1, 1), periodic=(1, 1, 1), alpha=1.0,
-                       nlevels=3, bottom=0, bvar=False, overlap=overlap)
-        amg = S["amg"]
-        amg.init_residual(S["fphi"], S["frhs"], S["fres"])
-        norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(3)]
-        out.append((norms, S["fphi"].download(0)))
-    for r in out[1:]:
-        assert out[0][0] == r[0]
-        assert np.array_equal(out[0][1], r[1])
 
 
 @pytest.mark.parametrize("bvar", [True, False])
@@ -435,7 +407,7 @@ def test_deep_halo_vcycle_bitwise(rng, nsmooth, periodic, parts, n, fused, bvar)
         out = []
         for deep in (0, 1):
             S = build_pair(c, np.random.default_rng(9), n, parts, periodic=periodic, alpha=1.0,
-                           nlevels=3, bottom=0, fused=fused, overlap=0, deep=deep, bvar=bvar)
+                           nlevels=3, bottom=0, fused=fused, deep=deep, bvar=bvar)
             amg = mg.AMRMultiGrid(S["fac"], mg.SolverParams(max_depth=2, n_pre=nsmooth,
                                                             n_post=nsmooth, n_bottom=nsmooth,
                                                             bottom_solver=0))
@@ -449,31 +421,6 @@ def test_deep_halo_vcycle_bitwise(rng, nsmooth, periodic, parts, n, fused, bvar)
         o.init_residual(0)
         assert [o.iteration(0) for _ in range(2)] == out[0][0]
         assert np.array_equal(o.get(0, oracle.PHI, 0), out[0][1])
-
-
-@pytest.mark.parametrize("nsmooth", [1, 3])
-@pytest.mark.parametrize("periodic", [(0, 0, 0), (1, 0, 1)])
-def test_split_halo_sweeps_odd_counts_bitwise(rng, nsmooth, periodic):
-    # boundary-first split (overlap_exchange 4) with odd sweep counts (the
-    # result ends in the scratch buffer) on ragged multi-box layouts, local
-    # copies and RCCL self messages, against the serial schedule and oracle
-    n = 48
-    for c in (mg.Comm(), None):
-        if c is None:
-            c = mg.Comm(0, 1, unique_id=mg.Comm.unique_id(), force_rccl=True)
-            c.set_self_messages(True)
-        out = []
-        for overlap in (0, 4):
-            S = build_pair(c, np.random.default_rng(3), n, (2, 1, 3), periodic=periodic,
-                           alpha=1.0, nlevels=3, bottom=0, overlap=overlap)
-            amg = mg.AMRMultiGrid(S["fac"], mg.SolverParams(max_depth=2, n_pre=nsmooth,
-                                                            n_post=nsmooth, n_bottom=nsmooth,
-                                                            bottom_solver=0))
-            amg.init_residual(S["fphi"], S["frhs"], S["fres"])
-            norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(2)]
-            out.append((norms, download_global(S["fphi"], S["grid"], (n,) * 3)))
-        assert out[0][0] == out[1][0]
-        assert np.array_equal(out[0][1], out[1][1])
 
 
 @pytest.mark.parametrize("shape,lo", [((70, 20, 13), (0, 0, 0)), ((37, 9, 40), (3, -5, 7)),
@@ -723,19 +670,17 @@ print("two-sweep OK")
 """
 
 
-@pytest.mark.parametrize("spl,variant", [("1", "0"), ("2", "0"), ("2", "1")])
-def test_two_sweep_kernel_vcycle_bitwise(spl, variant):
-    # the two-sweep kernel and its alternatives (MGIC_SWEEPS_PER_LAUNCH, read
-    # once per process: a child process): 2 = smoother_tb.hip (the default;
-    # MGIC_TB2_VARIANT 1 = its 512-thread form with two pairs per lane, where
-    # whole waves never skip a pass), 1 = one sweep per launch throughout;
-    # odd and even sweep counts, ragged mixed-BC box and a cube, against the
-    # oracle bit for bit
+@pytest.mark.parametrize("spl", ["1", "2"])
+def test_two_sweep_kernel_vcycle_bitwise(spl):
+    # the two-sweep kernel and its alternative (MGIC_SWEEPS_PER_LAUNCH, read
+    # once per process: a child process): 2 = smoother_tb.hip (the default),
+    # 1 = one sweep per launch throughout; odd and even sweep counts, ragged
+    # mixed-BC box and a cube, against the oracle bit for bit
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MGIC_SWEEPS_PER_LAUNCH=spl, MGIC_TB2_VARIANT=variant)
+    env = dict(os.environ, MGIC_SWEEPS_PER_LAUNCH=spl)
     r = subprocess.run([sys.executable, "-c", _TWO_SWEEPS_CHILD, root], env=env,
                        capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -809,7 +754,7 @@ def test_full_size_512_vcycle_bitwise():
                            fused_smoother=1)
     amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, op),
                           mg.SolverParams(max_depth=2, n_pre=4, n_post=4, n_bottom=4,
-                                          bottom_solver=0, fused_residual=1))
+                                          bottom_solver=0))
     r0 = amg.init_residual(fphi, frhs, fres, norm_type=0)
     rg = [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(2)]
     oracle.set_threads(min(16, os.cpu_count() or 1))
@@ -825,13 +770,10 @@ def test_full_size_512_vcycle_bitwise():
     assert o.init_residual(0) == r0
     assert [o.iteration(0) for _ in range(2)] == rg
     assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
-    # iterations() with the fused residual (SolverParams.fused_residual):
-    # iteration 1's residual formed in iteration 2's first launch -- the same
-    # phi and norms, bit for bit
+    # iterations() (the bench's timed loop): the same phi and norms
     del o
     fphi2, fres2 = mg.LevelData(grid), mg.LevelData(grid)
     fphi2.set_zero()
-    assert amg.fused_residual
     assert amg.init_residual(fphi2, frhs, fres2, norm_type=0) == r0
     assert amg.iterations(fphi2, frhs, fres2, 2, norm_type=0) == rg
     assert np.array_equal(fphi2.download(0), fphi.download(0))
@@ -920,51 +862,3 @@ def test_full_size_512_eight_boxes_rccl_deep_halo_bitwise():
     for r in out[1:]:
         assert out[0][0] == r[0]
         assert np.array_equal(out[0][1], r[1])
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape,bc,bval,kind", [
-    ((104, 72, 40), "mixed", 1.0, 2),     # ragged tiles, inhomogeneous Dirichlet / Neumann
-    ((96, 80, 72), "dirichlet", 1.0, 2),  # homogeneous, the reference's BC
-    ((72, 48, 40), "mixed", 2.0, 2),      # bCoef = 2 (the non-specialised expressions; lambda
-                                          # ignores b, .cpp:234-243, so this one diverges)
-    ((160, 144, 112), "dirichlet", 1.0, 1),  # the default kernel choice (fine level streamed)
-], ids=["ragged-mixed", "dirichlet", "bconst2", "default-kind"])
-@pytest.mark.parametrize("norm_type", [0, 2])
-def test_fused_residual_iterations_bitwise(rng, shape, bc, bval, kind, norm_type):
-    # AMRMultiGrid::iterations: iteration i's residual r = rhs - L(phi) (and
-    # its max norm) formed inside iteration i+1's first two-sweep launch
-    # (gsrb_sweep_tb2_res) -- phi, the residual and every norm identical to
-    # the same number of iteration() calls (themselves bit-identical to the
-    # oracle: test_vcycle_iterations_bitwise, test_full_size_512_vcycle_bitwise)
-    nx, ny, nz = shape
-    dom = (0, 0, 0, nx - 1, ny - 1, nz - 1)
-    kw = dict(bc_lo=(0, 1, 0), bc_hi=(1, 0, 0), bc_value=0.125) if bc == "mixed" else {}
-    op = mg.OperatorParams(alpha=1.0, beta=-1.0, coefficient_average_type=1, prolong_type=1,
-                           relax_mode=1, fused_smoother=kind, **kw)
-    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
-    rhs = rng.uniform(-1.0, 1.0, (nz, ny, nx))
-    phi0 = rng.uniform(-0.5, 0.5, (nz, ny, nx))
-    runs = []
-    for pipelined in (False, True):
-        grid = mg.Grid(mg.Comm(), dom, [dom], 100.0 / nx)
-        fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
-        fa.upload(0, a)
-        fb.set_val(bval)
-        frhs.upload(0, rhs)
-        fphi.upload(0, phi0)
-        amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, op),
-                              mg.SolverParams(max_depth=2, n_pre=4, n_post=4, n_bottom=4,
-                                              bottom_solver=0, fused_residual=1))
-        assert amg.fused_residual  # the hierarchy takes the fused launch
-        h = [amg.init_residual(fphi, frhs, fres, norm_type=norm_type)]
-        if pipelined:
-            h += amg.iterations(fphi, frhs, fres, 3, norm_type=norm_type)
-        else:
-            h += [amg.iteration(fphi, frhs, fres, norm_type=norm_type) for _ in range(3)]
-        runs.append((h, fphi.download(0), fres.download(0)))
-    assert runs[0][0] == runs[1][0]
-    assert np.array_equal(runs[0][1], runs[1][1])
-    assert np.array_equal(runs[0][2], runs[1][2])
-    if bval == 1.0:
-        assert runs[1][0][-1] < runs[1][0][0]

@@ -31,7 +31,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240):
+def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, mode="vcycle"):
     port = free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONUNBUFFERED="1")
     procs = []
@@ -42,7 +42,8 @@ def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240):
         procs.append(subprocess.Popen(
             [sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), "--rank", str(r),
              "--world", str(world), "--port", str(port), "--n", str(n), "--levels", str(levels),
-             "--agglomerate-below", str(agglomerate_below), "--out", str(tmp_path)],
+             "--agglomerate-below", str(agglomerate_below), "--out", str(tmp_path),
+             "--mode", mode],
             stdout=log, stderr=subprocess.STDOUT, env=env))
     rcs = []
     try:
@@ -62,18 +63,24 @@ def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240):
     return out
 
 
-def single_box(n, levels, iters=2):
+def single_box(n, levels, iters=2, mode="vcycle"):
     import bench
     comm = mg.Comm()
     case = bench.build_case(mg, comm, 1, n, levels, 4)
     amg, fphi, frhs, fres = (case[k] for k in ("amg", "fphi", "frhs", "fres"))
-    norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
-    norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(iters)]
+    if mode == "mixed":
+        amg = mg.MixedMultiGrid(case["fac"], mg.SolverParams(
+            max_depth=levels - 1, n_pre=4, n_post=4, n_bottom=4, bottom_solver=0))
+        norms = [amg.init_residual(fphi, frhs, fres, 0), amg.fmg(fphi, frhs, fres, 0)]
+        norms += [amg.iteration(fphi, frhs, fres, 0) for _ in range(iters)]
+    else:
+        norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
+        norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(iters)]
     return norms, fphi.download(0)
 
 
-def check(out, n, levels, iters=2):
-    norms, phi = single_box(n, levels, iters)
+def check(out, n, levels, iters=2, mode="vcycle"):
+    norms, phi = single_box(n, levels, iters, mode)
     for o in out:
         assert str(o["transport"]) == "ipc"
         assert bool(o["checked"])  # commcheck.check_transport passed on every rank
@@ -99,6 +106,30 @@ def test_four_processes_with_agglomeration_bitwise(tmp_path):
     # gather / scatter plans run between processes too
     n, levels = 128, 3
     check(run_workers(tmp_path, 4, n, levels, agglomerate_below=17), n, levels)
+
+
+def test_eight_processes_bench_split_512_bitwise(tmp_path):
+    # BASELINE config C4 as bench.py --gpus 8 runs it: 512^3 as 2 x 2 x 2
+    # boxes of 256^3, one per process, deep halo (4-deep shells), 3 levels,
+    # the coarsest depth placed as bench.py places it (AGG_C4 below) -- all
+    # eight ranks on this box's one GPU, so the exchange grids are capped
+    # (csrc/level.cpp: every rank's exchange workgroups resident at once);
+    # phi and every residual norm bit-identical to the single box
+    import bench
+    n, levels = 512, 3
+    check(run_workers(tmp_path, 8, n, levels, agglomerate_below=bench.agglomerate_default(8, n,
+                                                                                          levels),
+                      timeout=420), n, levels)
+
+
+def test_four_processes_mixed_fmg_bitwise(tmp_path):
+    # BASELINE config C5's cycle between processes: the 4-level mixed fp32
+    # smoother / fp64 residual FMG and two V-cycles at 128^3 on bench.py's
+    # 4-rank split (1 x 2 x 2), fp32 messages through the peer-mapped
+    # transport -- phi and every norm bit-identical to the single box (itself
+    # bit-identical to oracle/mixed.py: test_mixed.py)
+    n, levels = 128, 4
+    check(run_workers(tmp_path, 4, n, levels, mode="mixed"), n, levels, mode="mixed")
 
 
 def test_transport_check_single_rank():

@@ -33,6 +33,12 @@ for s in ${STEPS_TO_RUN:-pytest_gpu smoke bench}; do
     bench8) run bench8 600 env MGIC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 \
               --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 8 \
               --steps "${BSTEPS:-20}" --warmup 2 ${BENCH2_ARGS:-} || exit $? ;;
+    bench8_agg0) run bench8_agg0 600 env MGIC_BENCH_DEVICE=0 python -m torch.distributed.run \
+              --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29520 bench.py \
+              --gpus 8 --steps "${BSTEPS:-20}" --warmup 2 --agglomerate-below 0 ${BENCH2_ARGS:-} || exit $? ;;
+    bench8_agg65) run bench8_agg65 600 env MGIC_BENCH_DEVICE=0 python -m torch.distributed.run \
+              --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29521 bench.py \
+              --gpus 8 --steps "${BSTEPS:-20}" --warmup 2 --agglomerate-below 65 ${BENCH2_ARGS:-} || exit $? ;;
     proxy) run proxy 600 python tools/rank_proxy.py ${PROXY_ARGS:-} || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -5,10 +5,10 @@ At N = 8 each rank owns one 256^3 box of the 512^3 domain and exchanges its
 faces with RCCL.  One GPU cannot run 8 RCCL ranks, so this times one 256^3
 box, periodic in every direction (all six faces exchanged, with itself),
 with the exchange routed through RCCL self send/recv (the pack -> grouped
-ncclSend/ncclRecv -> unpack path the ranks use).  It prints V-cycles/s for
-the given overlap mode; xGMI latency is not modelled.
+ncclSend/ncclRecv -> unpack path the ranks use) or the peer-mapped
+transport.  It prints V-cycles/s; xGMI latency is not modelled.
 
-usage: rank_proxy.py [--size 256] [--overlap 0|1|2] [--steps 30]
+usage: rank_proxy.py [--size 256] [--transport rccl|ipc] [--deep 1] [--steps 30]
 """
 import argparse
 import json
@@ -22,7 +22,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--overlap", type=int, default=0)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--levels", type=int, default=3)
@@ -65,7 +64,7 @@ def main():
     fphi.set_zero()
     op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, coefficient_average_type=1,
                            prolong_type=1, relax_mode=1, fused_smoother=1,
-                           overlap_exchange=args.overlap, deep_halo=args.deep)
+                           deep_halo=args.deep)
     fac = mg.defineOperatorFactory(grid, fa, fb, op)
     amg = mg.AMRMultiGrid(fac, mg.SolverParams(max_depth=args.levels - 1, n_pre=4, n_post=4,
                                                n_bottom=4, bottom_solver=0,
@@ -81,7 +80,7 @@ def main():
     dt = time.perf_counter() - t0
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
     print(json.dumps({"size": n, "shape": shp, "parts": parts,
-                      "agglomerate_below": args.agglomerate_below, "overlap": args.overlap, "deep": args.deep, "periodic": per,
+                      "agglomerate_below": args.agglomerate_below, "deep": args.deep, "periodic": per,
                       "transport": "local" if args.local else args.transport,
                       "vcycles_per_s": round(args.steps / dt, 2),
                       "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
