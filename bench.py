@@ -313,8 +313,17 @@ def agglomerate_default(world, n, levels):
     """agglomerate_below for an N-rank run: MG depths whose boxes have a side
     below this are gathered onto one box on rank 0 (the coarsest levels
     solved on rank 0, north_star / Main_PoissonSolver.cpp:103-117); 0 on one
-    rank.  DESIGN.md 6 records the measurement this default follows."""
-    return 32 if world > 1 else 0
+    rank.  N > 1: the coarsest depth always (its per-rank boxes, e.g. 64^3 at
+    the 8-GPU split's third level, go to one box on rank 0), and every depth
+    whose boxes are narrower than 32 cells.  DESIGN.md 6 records the
+    measurement: the 8-rank split gathered and distributed run alike
+    (profiles/r04a_rank_rehearsal_agg.jsonl)."""
+    if world <= 1:
+        return 0
+    from mg_ic_code_amd.decomposition import decompose
+    _, boxes, _ = decompose((n, n, n), world)
+    side = min(b[3 + d] - b[d] + 1 for b in boxes for d in range(3)) >> (levels - 1)
+    return max(32, side + 1)
 
 
 def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fused=1,
@@ -427,15 +436,27 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
     o.setup()
     o.init_residual(0)
 
-    def timed(nthreads, iters):
+    def timed(nthreads, iters, pin):
         oracle.set_threads(nthreads)
-        pinned = oracle.pin_threads(cpus[:nthreads])  # thread t on CPU t of this job's set
+        pinned = 0
+        if pin:  # thread t on CPU t of a set spread evenly over this job's CPUs
+            step = max(1, len(cpus) // max(1, nthreads))
+            pinned = oracle.pin_threads(cpus[::step][:nthreads])
+        else:
+            oracle.pin_threads(cpus, pin=False)
         t0 = time.perf_counter()
         for _ in range(iters):
             o.iteration(0)
         return time.perf_counter() - t0, oracle.get_threads(), pinned
 
-    dt, used, pinned = timed(threads, args.cpu_baseline_iters)
+    # pinned (one thread per CPU, spread over the job's CPU set) and left to
+    # the scheduler: on a node shared with other jobs the scheduler can move
+    # threads off busy CPUs, so both are timed and the faster one reported
+    dtp, used, npin = timed(threads, args.cpu_baseline_iters, True)
+    dtu, _, _ = timed(threads, args.cpu_baseline_iters, False)
+    vp = round(args.cpu_baseline_iters / dtp, 6)
+    vu = round(args.cpu_baseline_iters / dtu, 6)
+    dt, pinned = (dtp, npin) if dtp <= dtu else (dtu, 0)
     out = {
         "value": round(args.cpu_baseline_iters / dt, 6),
         "unit": "V-cycles/s",
@@ -445,12 +466,14 @@ def cpu_baseline(args, grid, fa, frhs, dom, dx, np):
                   f"{args.levels}-level workload (oracle/mgic_oracle.c, OpenMP, -O3), {dt:.1f} s",
         "cores_reason": reason,
         "pinned_threads": pinned,
+        "value_pinned": vp,
+        "value_unpinned": vu,
         "host_cpus_available": avail,
         "host_cpus_machine": machine,
         "host_cpu_quota": quota,
     }
     if args.cpu_1core_iters > 0:
-        dt1, _, _ = timed(1, args.cpu_1core_iters)
+        dt1, _, _ = timed(1, args.cpu_1core_iters, True)
         out["one_core"] = {"value": round(args.cpu_1core_iters / dt1, 6), "unit": "V-cycles/s",
                            "cores": 1,
                            "sample": f"{args.cpu_1core_iters} V-cycle iteration(s), 1 thread, "

@@ -175,6 +175,11 @@ struct StencilCoefs {
   // the field -- the same operand, so bit-identical, 8 B/cell less traffic
   int bconst = 0;
   double bval = 1.0;
+  // every lambda of the level (1 / (alpha a + 6 beta / dx^2), .cpp:234-243)
+  // lies in [2^-500, 2^500] in magnitude, one sign: the two-sweep kernel may
+  // form 1 / x with the division's own instruction sequence minus its
+  // scale / fix-up steps, which are identities there (the same bits)
+  int rcp_fast = 0;
 };
 
 }  // namespace mgic

@@ -138,6 +138,7 @@ StencilCoefs VariableCoeffPoissonOperator::coefs() {
   s.lamshift = 2.0 * 3 * m_beta / (m_dx * m_dx);    // .cpp:240
   s.bconst = b_const_ ? 1 : 0;
   s.bval = b_val_;
+  s.rcp_fast = rcp_fast_ ? 1 : 0;
   return s;
 }
 
@@ -286,9 +287,24 @@ void VariableCoeffPoissonOperator::resetLambda() {
   const double bmax = reduce(4, *m_bCoef, nullptr), bmin = -reduce(5, *m_bCoef, nullptr);
   b_const_ = bmax == bmin && std::isfinite(bmax);
   b_val_ = b_const_ ? bmax : 1.0;
+  rcp_fast_ = false;
   const StencilCoefs s = coefs();
   for (int n = 0; n < grid->nlocal(); ++n)
     kern::lambda(m_lambda->p[n], m_aCoef->p[n], args_plain_[n], s, stream());
+  // the range of lambda over every rank's cells (StencilCoefs::rcp_fast):
+  // the denominators the sweeps meet, ghost cells included, are some rank's
+  // valid cells
+  static const int allow = [] {
+    const char *e = getenv("MGIC_TB2_RCP");
+    return e ? atoi(e) : 1;
+  }();
+  if (allow) {
+    const double lmax = reduce(4, *m_lambda, nullptr), lmin = -reduce(5, *m_lambda, nullptr);
+    const double lo = std::ldexp(1.0, -500), hi = std::ldexp(1.0, 500);
+    auto ok = [&](double a, double b) { return a >= lo && b <= hi; };  // a <= b, both > 0
+    rcp_fast_ = std::isfinite(lmax) && std::isfinite(lmin) &&
+                ((lmin > 0.0 && ok(lmin, lmax)) || (lmax < 0.0 && ok(-lmax, -lmin)));
+  }
 }
 
 void VariableCoeffPoissonOperator::computeLambda() {

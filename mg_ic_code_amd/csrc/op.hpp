@@ -122,6 +122,7 @@ class VariableCoeffPoissonOperator {
   std::shared_ptr<CFLevel> cf;
   bool b_const_ = false;      // bCoef holds one value everywhere (all ranks)
   double b_val_ = 1.0;
+  bool rcp_fast_ = false;     // StencilCoefs::rcp_fast (lambda's range, all ranks)
 
 
  private:

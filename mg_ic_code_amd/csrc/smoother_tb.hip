@@ -149,13 +149,31 @@ __device__ __forceinline__ float reg_copy(float x) {
   asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
   return y;
 }
+// 1.0 / d correctly rounded, for a normal d of moderate exponent: the
+// instructions hipcc emits for an fp64 division with numerator 1 --
+// v_div_scale (twice), v_rcp, two Newton steps, q = 1 * r, the remainder,
+// v_div_fmas, v_div_fixup -- less the scale, the multiply by 1 and the
+// fix-up, which return their input unchanged for |d| in [2^-500, 2^500]
+// (StencilCoefs::rcp_fast, checked on the host over every lambda of the
+// level): the same operations on the same values, so the same bits
+// (.cpp:234-243), in 7 instructions instead of 11
+__device__ __forceinline__ double rcp_div1(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(e, r, r);
+}
 template <class T> struct TB2Vec;
 template <> struct TB2Vec<double> { using type = double2; };
 template <> struct TB2Vec<float> { using type = float2; };
 
 // One tile (x0, y0) of the box, planes [z0, z1).  FAST: alpha == 1, beta ==
-// -1, bval == 1 (exact specialisation, see above); EDGE: the tile's rings
-// reach an x / y domain face (BC code compiled in).
+// -1, bval == 1 (exact specialisation, see above), and for fp64 lambda by
+// rcp_div1; EDGE: the tile's rings reach an x / y domain face (BC code
+// compiled in).
 template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE>
 __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                                          T *__restrict__ uo, double *__restrict__ acc,
@@ -388,7 +406,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       na1[b][i] = va.y;
     }
   };
-  auto lam = [&](T aa) { return (T)1 / (aa + s.lamshift); };  // .cpp:234-243 (a*alpha == alpha*a)
+  auto lam = [&](T aa) {  // .cpp:234-243 (a*alpha == alpha*a)
+    if constexpr (FAST && std::is_same<T, double>::value) return rcp_div1(aa + s.lamshift);
+    else return (T)1 / (aa + s.lamshift);
+  };
   auto upd = [&](T uc, T xm, T xp, T ym, T yp, T zm, T zp,
                  T rv, T aa, T lm) -> T {
     const T tx = (xp + xm) - (T)2 * uc;
@@ -702,7 +723,10 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   const TB2Geom<T, TX, TY, NT> G(g);
   const int ntx = G.ntx, nty = G.nty, kc = G.kc, nblocks = G.nblocks;
   const dim3 grid((unsigned)nblocks), block(NT);
-  const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0;
+  // FAST: the reference's constants (exact specialisation) and, for fp64,
+  // lambda in the fast reciprocal's range
+  const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0 &&
+                    (s.rcp_fast || !std::is_same<T, double>::value);
   const TB2Ghosts<T> gg = make_ghosts<T>(g);
   if (zero_in)  // the ZIN passes assume every ghost of a zero input is +-0
     for (int f = 0; f < 6; ++f)

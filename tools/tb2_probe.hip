@@ -36,10 +36,16 @@ int main(int argc, char **argv) {
   s.lamshift = (2 * 3) * s.beta / (s.dx * s.dx);
   s.bconst = 1;
   s.bval = 1.0;
+  s.rcp_fast = argc > 4 ? atoi(argv[4]) : 1;  // 0: lambda by fp64 division (the generic path)
   std::vector<double *> f(4);
   std::vector<double> h(geo.total);
+  // argv[5]: stagger the four arrays' bases by k * that many 128-B lines
+  // (L2 set / channel placement experiment)
+  const long stag = argc > 5 ? atol(argv[5]) : 0;
+  std::vector<double *> alloc(4);
   for (int k = 0; k < 4; ++k) {
-    MGIC_HIP(hipMalloc(&f[k], geo.total * sizeof(double)));
+    MGIC_HIP(hipMalloc(&alloc[k], geo.total * sizeof(double) + 4096 * 128));
+    f[k] = alloc[k] + k * stag * 16;
     for (long i = 0; i < geo.total; ++i)
       h[i] = k == 2 ? -1.0 - 0.5 * ((i * 2654435761u) % 1000) / 1000.0
                     : ((i * 40503u + k) % 2001) / 1000.0 - 1.0;
@@ -62,7 +68,8 @@ int main(int argc, char **argv) {
   MGIC_HIP(hipEventElapsedTime(&ms, e0, e1));
   ms /= reps;
   const double cells = (double)n * n * n;
-  printf("{\"n\": %d, \"zin\": %d, \"ms_per_launch\": %.4f, \"compulsory_GBps\": %.1f}\n", n, zin,
-         ms, (zin ? 24.0 : 32.0) * cells / (ms * 1e-3) / 1e9);
+  printf("{\"n\": %d, \"zin\": %d, \"rcp_fast\": %d, \"ms_per_launch\": %.4f, "
+         "\"compulsory_GBps\": %.1f}\n", n, zin, s.rcp_fast, ms,
+         (zin ? 24.0 : 32.0) * cells / (ms * 1e-3) / 1e9);
   return 0;
 }
