@@ -511,6 +511,43 @@ def test_two_sweep_relax_matches_oracle(comm, rng, shape, lo, nsweeps, coefs):
     assert np.array_equal(outs[0], o.get(0, oracle.PHI, 0))
 
 
+@pytest.mark.parametrize("big", [0.0, -1.0e160, -1.0e308])
+def test_two_sweep_lambda_range_guard(comm, rng, big):
+    # lambda = 1 / (alpha a + 6 beta / dx^2) by the short reciprocal
+    # (smoother_tb.hip: rcp_div1) only when the host finds every lambda of the
+    # level in [2^-500, 2^500]; a few cells with aCoef -1e160 (lambda ~ 1e-160)
+    # or -1e308 (lambda subnormal, where the division's scale / fix-up steps
+    # matter) turn the specialised body off.  Bit-identical to the oracle's
+    # division either way (alpha = 1, beta = -1, b = 1: the FAST candidate).
+    shape = (70, 44, 30)
+    nx, ny, nz = shape
+    dom = (0, 0, 0, nx - 1, ny - 1, nz - 1)
+    dx = 0.7
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    if big:
+        a.flat[rng.choice(a.size, 37, replace=False)] = big
+    b = np.ones((nz, ny, nx))
+    rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    u0 = rng.uniform(-1, 1, (nz, ny, nx))
+    grid = mg.Grid(comm, dom, [dom], dx)
+    fa, fb, fr, fu = (mg.LevelData(grid) for _ in range(4))
+    fa.upload(0, a)
+    fb.upload(0, b)
+    fr.upload(0, rhs)
+    fu.upload(0, u0)
+    prm = mg.OperatorParams(alpha=1.0, beta=-1.0, fused_smoother=2)
+    op = mg.defineOperatorFactory(grid, fa, fb, prm).AMRnewOp()
+    op.relax(fu, fr, 4)
+    o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, nlevels=1)
+    o.set(0, oracle.ACOEF, 0, a)
+    o.set(0, oracle.BCOEF, 0, b)
+    o.set(0, oracle.RHS, 0, rhs)
+    o.set(0, oracle.PHI, 0, u0)
+    o.setup()
+    o.relax(0, oracle.PHI, oracle.RHS, 4)
+    assert np.array_equal(fu.download(0), o.get(0, oracle.PHI, 0), equal_nan=True)
+
+
 # ------------------------------------------------- outer solve
 @pytest.mark.parametrize("parts", [(1, 1, 1), (2, 1, 2)])
 def test_mg_preconditioner_bitwise(comm, rng, parts):
