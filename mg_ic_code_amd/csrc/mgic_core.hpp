@@ -178,8 +178,10 @@ struct StencilCoefs {
   // every lambda of the level (1 / (alpha a + 6 beta / dx^2), .cpp:234-243)
   // lies in [2^-500, 2^500] in magnitude, one sign: the two-sweep kernel may
   // form 1 / x with the division's own instruction sequence minus its
-  // scale / fix-up steps, which are identities there (the same bits)
+  // scale / fix-up steps, which are identities there (the same bits);
+  // rcp_fast32: the same for the fp32 sweeps (|lambda| in [2^-60, 2^60])
   int rcp_fast = 0;
+  int rcp_fast32 = 0;
 };
 
 }  // namespace mgic

@@ -139,6 +139,7 @@ StencilCoefs VariableCoeffPoissonOperator::coefs() {
   s.bconst = b_const_ ? 1 : 0;
   s.bval = b_val_;
   s.rcp_fast = rcp_fast_ ? 1 : 0;
+  s.rcp_fast32 = rcp_fast32_ ? 1 : 0;
   return s;
 }
 
@@ -287,7 +288,7 @@ void VariableCoeffPoissonOperator::resetLambda() {
   const double bmax = reduce(4, *m_bCoef, nullptr), bmin = -reduce(5, *m_bCoef, nullptr);
   b_const_ = bmax == bmin && std::isfinite(bmax);
   b_val_ = b_const_ ? bmax : 1.0;
-  rcp_fast_ = false;
+  rcp_fast_ = rcp_fast32_ = false;
   const StencilCoefs s = coefs();
   for (int n = 0; n < grid->nlocal(); ++n)
     kern::lambda(m_lambda->p[n], m_aCoef->p[n], args_plain_[n], s, stream());
@@ -300,10 +301,15 @@ void VariableCoeffPoissonOperator::resetLambda() {
   }();
   if (allow) {
     const double lmax = reduce(4, *m_lambda, nullptr), lmin = -reduce(5, *m_lambda, nullptr);
-    const double lo = std::ldexp(1.0, -500), hi = std::ldexp(1.0, 500);
-    auto ok = [&](double a, double b) { return a >= lo && b <= hi; };  // a <= b, both > 0
-    rcp_fast_ = std::isfinite(lmax) && std::isfinite(lmin) &&
-                ((lmin > 0.0 && ok(lmin, lmax)) || (lmax < 0.0 && ok(-lmax, -lmin)));
+    // |lambda| in [2^-e, 2^e], one sign (a <= b, both > 0 in ok)
+    auto within = [&](int e) {
+      const double lo = std::ldexp(1.0, -e), hi = std::ldexp(1.0, e);
+      auto ok = [&](double a, double b) { return a >= lo && b <= hi; };
+      return std::isfinite(lmax) && std::isfinite(lmin) &&
+             ((lmin > 0.0 && ok(lmin, lmax)) || (lmax < 0.0 && ok(-lmax, -lmin)));
+    };
+    rcp_fast_ = within(500);
+    rcp_fast32_ = within(60);
   }
 }
 

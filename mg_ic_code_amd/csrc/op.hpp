@@ -123,6 +123,7 @@ class VariableCoeffPoissonOperator {
   bool b_const_ = false;      // bCoef holds one value everywhere (all ranks)
   double b_val_ = 1.0;
   bool rcp_fast_ = false;     // StencilCoefs::rcp_fast (lambda's range, all ranks)
+  bool rcp_fast32_ = false;   // StencilCoefs::rcp_fast32
 
 
  private:
