@@ -397,7 +397,7 @@ MGIC_API int mgic_plan_check_transport(mgic_plan p, int transport) {
   return guard([&] {
     NEED(p);
     MGIC_CHECK(transport == 1 || transport == 2, "transport: 1 RCCL, 2 peer-mapped");
-    if (transport == 2) p->plan->finalize_ipc_host();
+    if (transport == 2) p->plan->finalize_ipc_host(kern::kIpcBlockElemsDefault);
     else p->plan->finalize_host();
   });
 }

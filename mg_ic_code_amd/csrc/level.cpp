@@ -54,6 +54,10 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
     const double s = te ? atof(te) : 10.0;
     // the 100 MHz constant clock (wall_clock64); at least 1 ms
     timeout_ticks_ = (unsigned long long)(std::max(s, 1e-3) * 1e8);
+    const char *be = getenv("MGIC_IPC_BLOCK_ELEMS");
+    if (be && atol(be) > 0) block_elems_ = atol(be);
+    MGIC_CHECK(block_elems_ >= 512 && block_elems_ <= (1 << 20) && block_elems_ % 512 == 0,
+               "MGIC_IPC_BLOCK_ELEMS must be a multiple of 512 in [512, 2^20]");
   }
   peer_sig_.assign(size, nullptr);
   peer_arena_.assign(size, nullptr);
@@ -70,12 +74,14 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
     struct Rec {
       hipIpcMemHandle_t sig, arena;
       unsigned long long arena_bytes;
+      long block_elems;
       int rank;
       int pci[3];  // domain, bus, device of this rank's GPU
     } mine{}, *all = nullptr;
     MGIC_HIP(hipIpcGetMemHandle(&mine.sig, sig_));
     MGIC_HIP(hipIpcGetMemHandle(&mine.arena, arena_));
     mine.arena_bytes = arena_bytes_;
+    mine.block_elems = block_elems_;
     mine.rank = rank;
     {
       int dev = 0;
@@ -92,7 +98,8 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
       colocated += recs[r].pci[0] == mine.pci[0] && recs[r].pci[1] == mine.pci[1] &&
                    recs[r].pci[2] == mine.pci[2];
     for (int r = 0; r < size; ++r) {
-      MGIC_CHECK(recs[r].rank == r && recs[r].arena_bytes == arena_bytes_,
+      MGIC_CHECK(recs[r].rank == r && recs[r].arena_bytes == arena_bytes_ &&
+                     recs[r].block_elems == block_elems_,
                  "peer-mapped transport: ranks disagree on the setup");
       if (r == rank) continue;
       void *ps = nullptr, *pa = nullptr;
@@ -509,11 +516,16 @@ void CopyPlan::finalize() {
 // peer limit binds only plans it executes): offsets within each peer's
 // message, pad = the peer's index in send_peers_ / recv_peers_; one block
 // table for the one-launch exchange: put blocks, then the same-rank copies,
-// then get blocks, every item split into ipc_blocks(cells) blocks -- the same
+// then get blocks, every item split into ipc_blocks(cells, per) blocks -- the same
 // split on the sending and the receiving side, so the block counts match per
 // message
-void CopyPlan::finalize_ipc_host() {
-  if (ipc_host_) return;
+void CopyPlan::finalize_ipc_host(long per) {
+  if (ipc_host_) {
+    MGIC_CHECK(per == ipc_per_, "exchange plan: executed with two transport block sizes");
+    return;
+  }
+  MGIC_CHECK(per >= 512 && per % 512 == 0, "transport block size must be a multiple of 512");
+  ipc_per_ = per;
   finalize_host();
   ipc_pack_h_.clear();
   ipc_unpack_h_.clear();
@@ -536,13 +548,13 @@ void CopyPlan::finalize_ipc_host() {
       it.soff -= recv_off_[it.pad];
       it.pad = (int)(std::find(recv_peers_.begin(), recv_peers_.end(), it.pad) - recv_peers_.begin());
     }
-    auto add = [&](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> *per) {
-      if (per) per->assign(npeers, 0);
+    auto add = [&](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> *by_peer) {
+      if (by_peer) by_peer->assign(npeers, 0);
       const size_t n0 = xblocks_h_.size();
       for (size_t i = 0; i < v.size(); ++i) {
-        const long nb = kern::ipc_blocks((long)v[i].nx * v[i].ny * v[i].nz);
+        const long nb = kern::ipc_blocks((long)v[i].nx * v[i].ny * v[i].nz, per);
         for (long b = 0; b < nb; ++b) xblocks_h_.push_back({(int)i, (int)b});
-        if (per) (*per)[v[i].pad] += nb;
+        if (by_peer) (*by_peer)[v[i].pad] += nb;
       }
       return (int)(xblocks_h_.size() - n0);
     };
@@ -553,10 +565,10 @@ void CopyPlan::finalize_ipc_host() {
   ipc_host_ = true;
 }
 
-void CopyPlan::finalize_ipc() {
+void CopyPlan::finalize_ipc(long per) {
   if (ipc_final_) return;
   finalize();
-  finalize_ipc_host();
+  finalize_ipc_host(per);
   if (!xblocks_h_.empty()) {
     long dummy = 0;
     d_ipc_pack_ = upload_items(ipc_pack_h_, dummy);
@@ -570,7 +582,7 @@ void CopyPlan::finalize_ipc() {
 
 template <class T>
 void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hipStream_t st) {
-  finalize_ipc();
+  finalize_ipc(comm.ipc_block_elems());
   const size_t cap = comm.ipc_arena_bytes() / sizeof(T);
   for (auto &kv : send_cnt_)
     MGIC_CHECK((size_t)kv.second <= cap, "exchange message exceeds the transport arena "
@@ -588,12 +600,12 @@ void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hip
                   &pget.count[q]);
   if constexpr (std::is_same<T, double>::value)
     kern::ipc_exchange(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
-                       n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget,
-                       comm.ipc_grid_cap(), st);
+                       n_loc_blocks_, n_get_blocks_, (int)ipc_per_, src_tab, dst_tab, pput,
+                       pget, comm.ipc_grid_cap(), st);
   else
     kern::ipc_exchange_f(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
-                         n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput, pget,
-                         comm.ipc_grid_cap(), st);
+                         n_loc_blocks_, n_get_blocks_, (int)ipc_per_, src_tab, dst_tab, pput,
+                         pget, comm.ipc_grid_cap(), st);
 }
 
 void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_tab,

@@ -72,6 +72,9 @@ class Comm {
   // workgroup cap of one exchange launch: the CUs of the GPU, split among
   // the ranks that share it (MGIC_IPC_GRID_CAP overrides); see the constructor
   int ipc_grid_cap() const { return grid_cap_; }
+  // elements per exchange block (MGIC_IPC_BLOCK_ELEMS, a multiple of 512;
+  // every rank must use the same, checked at setup)
+  long ipc_block_elems() const { return block_elems_; }
   // bound of every device-side wait, in 100 MHz clock ticks
   // (MGIC_IPC_TIMEOUT_S seconds, default 10)
   unsigned long long ipc_timeout_ticks() const { return timeout_ticks_; }
@@ -108,6 +111,7 @@ class Comm {
   double *h_result_ = nullptr;
   bool ipc_ = false;
   int grid_cap_ = 0;
+  long block_elems_ = kern::kIpcBlockElemsDefault;
   unsigned long long timeout_ticks_ = 1000000000ull;
   double *barrier_val_ = nullptr;
   unsigned long long *sig_ = nullptr;            // my signal page (uncached)
@@ -129,10 +133,11 @@ class CopyPlan {
   ~CopyPlan();
   void finalize_host();  // per-peer buffer offsets (host only)
   void finalize();       // + upload the item tables (RCCL / local copies)
-  void finalize_ipc();   // + the peer-mapped transport's tables (on first use)
+  // + the peer-mapped transport's tables (on first use; per = elements per block)
+  void finalize_ipc(long per);
   // the peer-mapped transport's host tables only (raises when the plan has
   // more peers than that transport takes: kern::kMaxIpcPeers)
-  void finalize_ipc_host();
+  void finalize_ipc_host(long per);
   // src_tab / dst_tab: device tables of valid-lo pointers per local box
   void execute(Comm &comm, double *const *src_tab, double *const *dst_tab, hipStream_t st);
   // the same copies on fp32 fields (same element offsets; messages in floats)
@@ -154,6 +159,7 @@ class CopyPlan {
   CopyItem *d_ipc_pack_ = nullptr, *d_ipc_unpack_ = nullptr;
   kern::IpcBlock *d_xblocks_ = nullptr;  // put, local, get blocks of the one-launch exchange
   int n_put_blocks_ = 0, n_loc_blocks_ = 0, n_get_blocks_ = 0;
+  long ipc_per_ = 0;  // elements per block of the tables above
   std::vector<int> send_peers_, recv_peers_;
   std::vector<long> send_blocks_, recv_blocks_;  // per peer of the lists above
   long max_local_ = 0, max_pack_ = 0, max_unpack_ = 0;

@@ -2,13 +2,14 @@
 //
 // Hand-off protocol (MI355X_MICROARCH.md, inter-workgroup visibility, taken
 // to system scope because the reader can be another process or another GPU):
-//   producer block: payload stored write-through (sc0 sc1 buffer stores) ->
-//                   s_waitcnt vmcnt(0) in every wave -> workgroup barrier ->
-//                   one lane adds 1 to the consumer's counter (system scope);
-//   consumer block: one lane polls the counter (relaxed system-scope loads,
-//                   s_sleep, bounded) until it covers every block of the
-//                   message -> workgroup barrier -> payload read with
-//                   system-scope (sc0 sc1) loads, so no cached copy is used.
+//   producer:  payload stored write-through (sc0 sc1 buffer stores) ->
+//              s_waitcnt vmcnt(0) in every wave -> workgroup barrier -> one
+//              lane adds the workgroup's blocks to the consumer's counter
+//              (system scope);
+//   consumer:  one lane polls the counter (relaxed system-scope loads,
+//              s_sleep, bounded) until it covers every block of the message
+//              -> workgroup barrier -> payload read with system-scope
+//              (sc0 sc1) loads, so no cached copy is used.
 // tools/ipc_probe.hip measured the forms on one MI355X with two processes:
 // plain stores behind a single release lose words across XCDs; a release per
 // block is correct but 3x slower at 2-8 MB; write-through stores are correct
@@ -83,27 +84,19 @@ template <> __device__ __forceinline__ float ld_sys<float>(__amdgpu_buffer_rsrc_
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kSys));
 }
 
-// after every wave's memory operations are drained, one lane counts the block
-__device__ __forceinline__ void ipc_done(unsigned long long *count) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_fetch_add(count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // the element range [e0, e1) of an item this block moves, in pairs when every
 // row starts 2-aligned on both sides (the shells' x slabs are 2 or 4 wide)
 struct Share {
   bool pairs;
   unsigned w, ny, e0, e1;
 };
-__device__ __forceinline__ Share share_of(const CopyItem &it, int sub, bool pairs) {
+__device__ __forceinline__ Share share_of(const CopyItem &it, int sub, bool pairs, unsigned per) {
   Share s;
   s.pairs = pairs && (it.nx & 1) == 0;
   s.w = s.pairs ? (unsigned)it.nx / 2 : (unsigned)it.nx;
   s.ny = (unsigned)it.ny;
   const unsigned n = s.w * s.ny * (unsigned)it.nz;
-  const unsigned per = s.pairs ? (unsigned)kIpcBlockElems / 2 : (unsigned)kIpcBlockElems;
+  if (s.pairs) per /= 2;
   s.e0 = (unsigned)sub * per;
   s.e1 = min(n, s.e0 + per);
   return s;
@@ -149,66 +142,84 @@ __device__ __forceinline__ void move_share(unsigned e0, unsigned e1, Load load, 
 // put: a block's share of one item, field -> peer's message slot (rows packed:
 // pair t is message elements 2t, 2t+1)
 template <class T>
-__device__ __forceinline__ void put_share(const CopyItem &it, int sub, T *const *src_tab,
-                                          const IpcPeers &pp, int &ok) {
+__device__ __forceinline__ void put_share(const CopyItem &it, int sub, unsigned per,
+                                          T *const *src_tab, const IpcPeers &pp, int p) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
-  const int p = __builtin_amdgcn_readfirstlane(it.pad);
-  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err, pp.timeout);  // slot free
-  __syncthreads();
-  if (ok) {
-    const T *src = src_tab[it.src] + it.soff;
-    const Share s = share_of(it, sub, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
-                                          (it.doff & 1) == 0);
-    const Rows rw{s.w, s.ny, it.ssy, it.ssz};
-    const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
-    const long mo = it.doff;
-    if (s.pairs)
-      move_share<V>(s.e0, s.e1,
-                    [&](unsigned t) { return *reinterpret_cast<const V *>(src + rw.at(t, 2)); },
-                    [&](unsigned t, V v) { st_sys(r, (unsigned)((mo + 2 * (long)t) * sizeof(T)), v); });
-    else
-      move_share<T>(s.e0, s.e1, [&](unsigned t) { return src[rw.at(t, 1)]; },
-                    [&](unsigned t, T v) { st_sys(r, (unsigned)((mo + (long)t) * sizeof(T)), v); });
-  }
-  ipc_done(pp.count[p]);
+  const T *src = src_tab[it.src] + it.soff;
+  const Share s = share_of(it, sub, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
+                                        (it.doff & 1) == 0, per);
+  const Rows rw{s.w, s.ny, it.ssy, it.ssz};
+  const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
+  const long mo = it.doff;
+  if (s.pairs)
+    move_share<V>(s.e0, s.e1,
+                  [&](unsigned t) { return *reinterpret_cast<const V *>(src + rw.at(t, 2)); },
+                  [&](unsigned t, V v) { st_sys(r, (unsigned)((mo + 2 * (long)t) * sizeof(T)), v); });
+  else
+    move_share<T>(s.e0, s.e1, [&](unsigned t) { return src[rw.at(t, 1)]; },
+                  [&](unsigned t, T v) { st_sys(r, (unsigned)((mo + (long)t) * sizeof(T)), v); });
 }
 
 // get: a block's share of one item, my message slot -> field ghosts
 template <class T>
-__device__ __forceinline__ void get_share(const CopyItem &it, int sub, T *const *dst_tab,
-                                          const IpcPeers &pp, int &ok) {
+__device__ __forceinline__ void get_share(const CopyItem &it, int sub, unsigned per,
+                                          T *const *dst_tab, const IpcPeers &pp, int p) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
-  const int p = __builtin_amdgcn_readfirstlane(it.pad);
-  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err, pp.timeout);  // message complete
+  T *dst = dst_tab[it.dst] + it.doff;
+  const Share s = share_of(it, sub, pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz) &&
+                                        (it.soff & 1) == 0, per);
+  const Rows rw{s.w, s.ny, it.dsy, it.dsz};
+  const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
+  const long mo = it.soff;
+  if (s.pairs)
+    move_share<V>(s.e0, s.e1,
+                  [&](unsigned t) { return ld_sys<V>(r, (unsigned)((mo + 2 * (long)t) * sizeof(T))); },
+                  [&](unsigned t, V v) { *reinterpret_cast<V *>(dst + rw.at(t, 2)) = v; });
+  else
+    move_share<T>(s.e0, s.e1,
+                  [&](unsigned t) { return ld_sys<T>(r, (unsigned)((mo + (long)t) * sizeof(T))); },
+                  [&](unsigned t, T v) { dst[rw.at(t, 1)] = v; });
+}
+
+// A workgroup's wait for peer p's condition (slot free / message complete),
+// at most once per launch: the condition holds for the rest of the launch once
+// met, so `passed` (uniform, bit p) remembers it.  A timed-out wait skips the
+// copy; the block is still counted, so no peer waits on this one in turn.
+__device__ __forceinline__ bool wait_once(const IpcPeers &pp, int p, unsigned &passed, int &ok) {
+  if (passed >> p & 1u) return true;
+  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err, pp.timeout);
   __syncthreads();
-  if (ok) {
-    T *dst = dst_tab[it.dst] + it.doff;
-    const Share s = share_of(it, sub, pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz) &&
-                                          (it.soff & 1) == 0);
-    const Rows rw{s.w, s.ny, it.dsy, it.dsz};
-    const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
-    const long mo = it.soff;
-    if (s.pairs)
-      move_share<V>(s.e0, s.e1,
-                    [&](unsigned t) { return ld_sys<V>(r, (unsigned)((mo + 2 * (long)t) * sizeof(T))); },
-                    [&](unsigned t, V v) { *reinterpret_cast<V *>(dst + rw.at(t, 2)) = v; });
-    else
-      move_share<T>(s.e0, s.e1,
-                    [&](unsigned t) { return ld_sys<T>(r, (unsigned)((mo + (long)t) * sizeof(T))); },
-                    [&](unsigned t, T v) { dst[rw.at(t, 1)] = v; });
-  }
-  ipc_done(pp.count[p]);  // acknowledge to the sender
+  const bool go = ok != 0;
+  __syncthreads();  // (ok is rewritten by the next wait)
+  if (go) passed |= 1u << p;
+  return go;
+}
+
+// after every wave's memory operations are drained, one lane adds the
+// workgroup's blocks per peer to the peers' counters (one atomic per peer
+// and workgroup instead of one per block: the counters are single words that
+// every block of an exchange would otherwise contend on)
+__device__ __forceinline__ void count_blocks(unsigned *done, const IpcPeers &pp) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int q = 0; q < pp.n; ++q)
+      if (done[q]) {
+        __hip_atomic_fetch_add(pp.count[q], (unsigned long long)done[q], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        done[q] = 0;
+      }
 }
 
 // local: a block's share of a same-rank copy, field -> field
 template <class T>
-__device__ __forceinline__ void local_share(const CopyItem &it, int sub, T *const *src_tab,
-                                            T *const *dst_tab) {
+__device__ __forceinline__ void local_share(const CopyItem &it, int sub, unsigned per,
+                                            T *const *src_tab, T *const *dst_tab) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   const T *src = src_tab[it.src] + it.soff;
   T *dst = dst_tab[it.dst] + it.doff;
   const Share s = share_of(it, sub, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
-                                        pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz));
+                                        pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz), per);
   const Rows rs{s.w, s.ny, it.ssy, it.ssz}, rd{s.w, s.ny, it.dsy, it.dsz};
   if (s.pairs)
     move_share<V>(s.e0, s.e1,
@@ -232,20 +243,39 @@ __global__ __launch_bounds__(256) void k_exchange(const CopyItem *__restrict__ p
                                                   const CopyItem *__restrict__ loc_items,
                                                   const CopyItem *__restrict__ get_items,
                                                   const IpcBlock *__restrict__ blocks, int npu,
-                                                  int nlo, int nall, T *const *__restrict__ src_tab,
+                                                  int nlo, int nall, unsigned per,
+                                                  T *const *__restrict__ src_tab,
                                                   T *const *__restrict__ dst_tab,
                                                   const IpcPeers pput, const IpcPeers pget) {
   __shared__ int ok;
+  // blocks this workgroup has moved per peer and not yet counted (lane 0 only)
+  __shared__ unsigned done_put[kMaxIpcPeers], done_get[kMaxIpcPeers];
+  if (threadIdx.x == 0)
+    for (int q = 0; q < kMaxIpcPeers; ++q) done_put[q] = done_get[q] = 0;
+  unsigned passed_put = 0, passed_get = 0;  // (uniform)
+  bool puts_counted = false;
   for (int v = blockIdx.x; v < nall; v += gridDim.x) {  // (uniform per workgroup)
     const IpcBlock b = blocks[v];
-    if (v < npu)
-      put_share<T>(put_items[b.item], b.sub, src_tab, pput, ok);
-    else if (v < npu + nlo)
-      local_share<T>(loc_items[b.item], b.sub, src_tab, dst_tab);
-    else
-      get_share<T>(get_items[b.item], b.sub, dst_tab, pget, ok);
-    __syncthreads();  // (ok is rewritten by the next virtual block)
+    if (v < npu) {
+      const CopyItem &it = put_items[b.item];
+      const int p = __builtin_amdgcn_readfirstlane(it.pad);
+      if (wait_once(pput, p, passed_put, ok)) put_share<T>(it, b.sub, per, src_tab, pput, p);
+      if (threadIdx.x == 0) ++done_put[p];
+    } else if (v < npu + nlo) {
+      local_share<T>(loc_items[b.item], b.sub, per, src_tab, dst_tab);
+    } else {
+      if (!puts_counted) {  // my puts reach the peers before I wait on theirs
+        count_blocks(done_put, pput);
+        puts_counted = true;
+      }
+      const CopyItem &it = get_items[b.item];
+      const int p = __builtin_amdgcn_readfirstlane(it.pad);
+      if (wait_once(pget, p, passed_get, ok)) get_share<T>(it, b.sub, per, dst_tab, pget, p);
+      if (threadIdx.x == 0) ++done_get[p];
+    }
   }
+  if (!puts_counted) count_blocks(done_put, pput);
+  count_blocks(done_get, pget);  // acknowledgements to the senders
 }
 
 __global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned long long *err) {
@@ -281,28 +311,29 @@ inline void check_launch() {
 template <class T>
 static void exchange_t(const CopyItem *put_items, const CopyItem *loc_items,
                        const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
-                       T *const *src_tab, T *const *dst_tab, const IpcPeers &pput,
+                       int per, T *const *src_tab, T *const *dst_tab, const IpcPeers &pput,
                        const IpcPeers &pget, int grid_cap, hipStream_t st) {
   const int n = npu + nlo + nge;
   if (n <= 0) return;
   const int g = grid_cap > 0 && grid_cap < n ? grid_cap : n;  // (the Comm always caps)
   k_exchange<T><<<dim3((unsigned)g), dim3(256), 0, st>>>(put_items, loc_items, get_items, blocks,
-                                                         npu, nlo, n, src_tab, dst_tab, pput, pget);
+                                                         npu, nlo, n, (unsigned)per, src_tab,
+                                                         dst_tab, pput, pget);
   check_launch();
 }
 
 void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
-                  const IpcBlock *blocks, int npu, int nlo, int nge, double *const *src_tab,
-                  double *const *dst_tab, const IpcPeers &pput, const IpcPeers &pget,
-                  int grid_cap, hipStream_t st) {
-  exchange_t<double>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
+                  const IpcBlock *blocks, int npu, int nlo, int nge, int per,
+                  double *const *src_tab, double *const *dst_tab, const IpcPeers &pput,
+                  const IpcPeers &pget, int grid_cap, hipStream_t st) {
+  exchange_t<double>(put_items, loc_items, get_items, blocks, npu, nlo, nge, per, src_tab, dst_tab,
                      pput, pget, grid_cap, st);
 }
 void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
                     const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
-                    float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
+                    int per, float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
                     const IpcPeers &pget, int grid_cap, hipStream_t st) {
-  exchange_t<float>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
+  exchange_t<float>(put_items, loc_items, get_items, blocks, npu, nlo, nge, per, src_tab, dst_tab,
                     pput, pget, grid_cap, st);
 }
 

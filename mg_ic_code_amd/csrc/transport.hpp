@@ -8,11 +8,12 @@
 // An exchange (CopyPlan) is then two launches and no host round trip:
 //   put  -- each block copies its share of my boundary regions, with
 //           write-through (system-scope) 16-B stores, straight into the
-//           peer's arena slot, drains them and adds 1 to the peer's counter
-//           for me;
+//           peer's arena slot; a workgroup drains its stores and adds its
+//           blocks to the peer's counter for me before its first get;
 //   get  -- each block waits until the sender's counter covers the whole
-//           message, reads it with system-scope loads into my ghost cells and
-//           adds 1 to the sender's acknowledgement counter.
+//           message, reads it with system-scope loads into my ghost cells;
+//           the workgroup adds its blocks to the sender's acknowledgement
+//           counter when it ends.
 // Both sides split an item into blocks the same way (ipc_blocks), so the
 // counters count blocks; they are cumulative per (sender, receiver) pair, so
 // nothing is ever reset, and no ticket or last-block step is needed.  Every
@@ -55,8 +56,10 @@ struct IpcPeers {
 struct IpcBlock {
   int item, sub;
 };
-constexpr long kIpcBlockElems = 4096;  // elements per block (16 per thread)
-inline long ipc_blocks(long cells) { return (cells + kIpcBlockElems - 1) / kIpcBlockElems; }
+// elements per block: a job-wide constant (Comm::ipc_block_elems, checked
+// equal on every rank at setup), so both sides of a message split alike
+constexpr long kIpcBlockElemsDefault = 4096;
+inline long ipc_blocks(long cells, long per) { return (cells + per - 1) / per; }
 
 struct IpcReduce {
   int size, rank, parity;
@@ -69,16 +72,16 @@ struct IpcReduce {
 // (items: src = local box, doff = offset in the peer's message, pad = peer
 // index in pput), then nlo same-rank copy blocks (loc_items), then nge get
 // blocks (items: dst = local box, soff = offset in the sender's message, pad =
-// peer index in pget).  Every item is split into ipc_blocks(cells) blocks.
+// peer index in pget).  Every item is split into ipc_blocks(cells, per) blocks.
 // At most grid_cap workgroups, striding over the blocks in ascending order
 // (every workgroup's puts before its gets; see k_exchange and Comm).
 void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
-                  const IpcBlock *blocks, int npu, int nlo, int nge, double *const *src_tab,
-                  double *const *dst_tab, const IpcPeers &pput, const IpcPeers &pget,
-                  int grid_cap, hipStream_t st);
+                  const IpcBlock *blocks, int npu, int nlo, int nge, int per,
+                  double *const *src_tab, double *const *dst_tab, const IpcPeers &pput,
+                  const IpcPeers &pget, int grid_cap, hipStream_t st);
 void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
                     const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
-                    float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
+                    int per, float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
                     const IpcPeers &pget, int grid_cap, hipStream_t st);
 // in-place allreduce of one device double over all ranks (op 0 sum, 1 max),
 // reduced in rank order on every rank (identical results everywhere)
