@@ -43,9 +43,9 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   MGIC_HIP(hipHostMalloc(&h_err_, sizeof(unsigned long long), hipHostMallocDefault));
   *h_err_ = 0;
   // counters are polled across processes / devices: uncached memory
-  MGIC_HIP(hipExtMallocWithFlags((void **)&sig_, sizeof(unsigned long long) * kern::kSigWords,
+  MGIC_HIP(hipExtMallocWithFlags((void **)&sig_, sizeof(unsigned long long) * kern::sig_words(size),
                                  hipDeviceMallocUncached));
-  MGIC_HIP(hipMemset(sig_, 0, sizeof(unsigned long long) * kern::kSigWords));
+  MGIC_HIP(hipMemset(sig_, 0, sizeof(unsigned long long) * kern::sig_words(size)));
   MGIC_HIP(hipMalloc(&arena_, (size_t)size * 2 * arena_bytes_));
   MGIC_HIP(hipDeviceSynchronize());
   ipc_ = true;
@@ -65,7 +65,6 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   recvd_.assign(size, 0);
   sent_blocks_.assign(size, 0);
   sent_prev_.assign(size, 0);
-  recvd_blocks_.assign(size, 0);
   peer_sig_[rank] = sig_;
   peer_arena_[rank] = arena_;
   int colocated = 1;  // ranks on this GPU (this one included)
@@ -139,27 +138,28 @@ void Comm::ipc_barrier() {
   ipc_check();
 }
 
-void Comm::ipc_send(int peer, long nblocks, void **slot, const unsigned long long **wait,
-                    unsigned long long *wait_val, unsigned long long **count) {
+void Comm::ipc_send(int peer, long nblocks, kern::IpcPeers &pp, int q) {
   const unsigned long long m = sent_[peer]++;  // my message number m to peer (0-based)
-  *slot = peer_arena_[peer] + ((size_t)rank_ * 2 + (m & 1)) * arena_bytes_;
+  const size_t slot = (size_t)rank_ * 2 + (m & 1);
+  pp.buf[q] = peer_arena_[peer] + slot * arena_bytes_;
+  pp.flags[q] = peer_sig_[peer] + kern::kSigFlags + slot * kern::kMaxMsgBlocks;
+  pp.seq[q] = m + 1;
   // the slot last held message m - 2: wait until the peer has acknowledged
   // every block up to and including it (= the blocks sent before message m - 1)
-  *wait = sig_ + kern::kSigAck + peer * kern::kSigStride;
-  *wait_val = sent_prev_[peer];
-  *count = peer_sig_[peer] + kern::kSigArr + rank_ * kern::kSigStride;
+  pp.ack[q] = sig_ + kern::kSigAck + peer * kern::kSigStride;
+  pp.val[q] = sent_prev_[peer];
   sent_prev_[peer] = sent_blocks_[peer];
   sent_blocks_[peer] += (unsigned long long)nblocks;
 }
 
-void Comm::ipc_recv(int src, long nblocks, void **slot, const unsigned long long **wait,
-                    unsigned long long *wait_val, unsigned long long **count) {
+void Comm::ipc_recv(int src, kern::IpcPeers &pp, int q) {
   const unsigned long long m = recvd_[src]++;
-  *slot = arena_ + ((size_t)src * 2 + (m & 1)) * arena_bytes_;
-  recvd_blocks_[src] += (unsigned long long)nblocks;
-  *wait = sig_ + kern::kSigArr + src * kern::kSigStride;  // every block of message m delivered
-  *wait_val = recvd_blocks_[src];
-  *count = peer_sig_[src] + kern::kSigAck + rank_ * kern::kSigStride;
+  const size_t slot = (size_t)src * 2 + (m & 1);
+  pp.buf[q] = arena_ + slot * arena_bytes_;
+  pp.flags[q] = sig_ + kern::kSigFlags + slot * kern::kMaxMsgBlocks;
+  pp.seq[q] = m + 1;
+  pp.ack[q] = peer_sig_[src] + kern::kSigAck + rank_ * kern::kSigStride;
+  pp.val[q] = 0;
 }
 
 void Comm::ipc_err_async(hipStream_t st) {
@@ -516,9 +516,9 @@ void CopyPlan::finalize() {
 // peer limit binds only plans it executes): offsets within each peer's
 // message, pad = the peer's index in send_peers_ / recv_peers_; one block
 // table for the one-launch exchange: put blocks, then the same-rank copies,
-// then get blocks, every item split into ipc_blocks(cells, per) blocks -- the same
-// split on the sending and the receiving side, so the block counts match per
-// message
+// then get blocks, every item split into blocks of ipc_item_per(cells, per) -- the same
+// split on the sending and the receiving side, so a message's blocks and their
+// flags match
 void CopyPlan::finalize_ipc_host(long per) {
   if (ipc_host_) {
     MGIC_CHECK(per == ipc_per_, "exchange plan: executed with two transport block sizes");
@@ -548,19 +548,36 @@ void CopyPlan::finalize_ipc_host(long per) {
       it.soff -= recv_off_[it.pad];
       it.pad = (int)(std::find(recv_peers_.begin(), recv_peers_.end(), it.pad) - recv_peers_.begin());
     }
-    auto add = [&](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> *by_peer) {
+    // side: 0 puts (message offset doff), 1 same-rank copies (no flag), 2 gets
+    // (message offset soff); a message's blocks are numbered (flag) in the
+    // order of their first element in the message, the same on both sides
+    auto add = [&](const std::vector<CopyItem> &v, size_t npeers, std::vector<long> *by_peer,
+                   int side) {
       if (by_peer) by_peer->assign(npeers, 0);
       const size_t n0 = xblocks_h_.size();
+      std::vector<std::vector<std::pair<long, size_t>>> order(npeers);  // (offset, block)
       for (size_t i = 0; i < v.size(); ++i) {
-        const long nb = kern::ipc_blocks((long)v[i].nx * v[i].ny * v[i].nz, per);
-        for (long b = 0; b < nb; ++b) xblocks_h_.push_back({(int)i, (int)b});
+        const long cells = (long)v[i].nx * v[i].ny * v[i].nz;
+        const long pi = kern::ipc_item_per(cells, per), nb = kern::ipc_blocks(cells, pi);
+        const long mo = side == 0 ? v[i].doff : v[i].soff;
+        for (long b = 0; b < nb; ++b) {
+          if (side != 1) order[v[i].pad].push_back({mo + b * pi, xblocks_h_.size()});
+          xblocks_h_.push_back({(int)i, -1, (unsigned)(b * pi), (unsigned)std::min(cells, (b + 1) * pi)});
+        }
         if (by_peer) (*by_peer)[v[i].pad] += nb;
+      }
+      for (auto &o : order) {
+        MGIC_CHECK((long)o.size() <= kern::kMaxMsgBlocks,
+                   "exchange message has more blocks than the transport flags "
+                   "(raise MGIC_IPC_BLOCK_ELEMS)");
+        std::sort(o.begin(), o.end());
+        for (size_t f = 0; f < o.size(); ++f) xblocks_h_[o[f].second].flag = (int)f;
       }
       return (int)(xblocks_h_.size() - n0);
     };
-    n_put_blocks_ = add(ipc_pack_h_, send_peers_.size(), &send_blocks_);
-    n_loc_blocks_ = add(local_, 0, nullptr);
-    n_get_blocks_ = add(ipc_unpack_h_, recv_peers_.size(), &recv_blocks_);
+    n_put_blocks_ = add(ipc_pack_h_, send_peers_.size(), &send_blocks_, 0);
+    n_loc_blocks_ = add(local_, 0, nullptr, 1);
+    n_get_blocks_ = add(ipc_unpack_h_, recv_peers_.size(), &recv_blocks_, 2);
   }
   ipc_host_ = true;
 }
@@ -592,19 +609,17 @@ void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hip
   pput.err = pget.err = comm.ipc_err();
   pput.timeout = pget.timeout = comm.ipc_timeout_ticks();
   for (int q = 0; q < pput.n; ++q)
-    comm.ipc_send(send_peers_[q], send_blocks_[q], &pput.buf[q], &pput.wait[q], &pput.wait_val[q],
-                  &pput.count[q]);
+    comm.ipc_send(send_peers_[q], send_blocks_[q], pput, q);
   pget.n = (int)recv_peers_.size();
   for (int q = 0; q < pget.n; ++q)
-    comm.ipc_recv(recv_peers_[q], recv_blocks_[q], &pget.buf[q], &pget.wait[q], &pget.wait_val[q],
-                  &pget.count[q]);
+    comm.ipc_recv(recv_peers_[q], pget, q);
   if constexpr (std::is_same<T, double>::value)
     kern::ipc_exchange(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
-                       n_loc_blocks_, n_get_blocks_, (int)ipc_per_, src_tab, dst_tab, pput,
+                       n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput,
                        pget, comm.ipc_grid_cap(), st);
   else
     kern::ipc_exchange_f(d_ipc_pack_, d_local_, d_ipc_unpack_, d_xblocks_, n_put_blocks_,
-                         n_loc_blocks_, n_get_blocks_, (int)ipc_per_, src_tab, dst_tab, pput,
+                         n_loc_blocks_, n_get_blocks_, src_tab, dst_tab, pput,
                          pget, comm.ipc_grid_cap(), st);
 }
 

@@ -81,15 +81,14 @@ class Comm {
   // device-side barrier over the signal pages (returns once every rank's
   // earlier stream work is done; raises if a wait timed out)
   void ipc_barrier();
-  // my next message to `peer` (nblocks put blocks): its slot in the peer's
-  // arena, the acknowledgement count to wait for (the slot's previous
-  // message consumed) and the peer's counter my blocks add to
-  void ipc_send(int peer, long nblocks, void **slot, const unsigned long long **wait,
-                unsigned long long *wait_val, unsigned long long **count);
-  // my next message from `src` (nblocks blocks): its slot in my arena, the
-  // delivered-block count that completes it, the sender's ack counter
-  void ipc_recv(int src, long nblocks, void **slot, const unsigned long long **wait,
-                unsigned long long *wait_val, unsigned long long **count);
+  // my next message to `peer` (nblocks put blocks) into entry q of a put
+  // launch's peer table: its slot in the peer's arena, its flags in the
+  // peer's page and their value, the acknowledgement count that frees the slot
+  void ipc_send(int peer, long nblocks, kern::IpcPeers &pp, int q);
+  // my next message from `src` into entry q of a get launch's peer table: its
+  // slot in my arena, its flags in my page and their value, the sender's
+  // acknowledgement counter
+  void ipc_recv(int src, kern::IpcPeers &pp, int q);
   unsigned long long *ipc_err() const { return sig_ + kern::kSigErr; }
   // raise if a transport wait of this rank timed out (synchronizes the stream)
   void ipc_check();
@@ -120,8 +119,8 @@ class Comm {
   std::vector<unsigned long long *> peer_sig_;   // per rank (mine at [rank_])
   std::vector<char *> peer_arena_;
   std::vector<unsigned long long> sent_, recvd_;  // messages per peer so far
-  // cumulative blocks per peer: sent (after the last message / before it), received
-  std::vector<unsigned long long> sent_blocks_, sent_prev_, recvd_blocks_;
+  // cumulative blocks sent per peer (after the last message / before it)
+  std::vector<unsigned long long> sent_blocks_, sent_prev_;
   unsigned long long red_count_ = 0;
   unsigned long long *h_err_ = nullptr;          // pinned
 };

@@ -2,14 +2,16 @@
 //
 // Hand-off protocol (MI355X_MICROARCH.md, inter-workgroup visibility, taken
 // to system scope because the reader can be another process or another GPU):
-//   producer:  payload stored write-through (sc0 sc1 buffer stores) ->
-//              s_waitcnt vmcnt(0) in every wave -> workgroup barrier -> one
-//              lane adds the workgroup's blocks to the consumer's counter
-//              (system scope);
-//   consumer:  one lane polls the counter (relaxed system-scope loads,
-//              s_sleep, bounded) until it covers every block of the message
-//              -> workgroup barrier -> payload read with system-scope
-//              (sc0 sc1) loads, so no cached copy is used.
+//   producer:  a block's payload stored write-through (sc0 sc1 buffer
+//              stores) -> s_waitcnt vmcnt(0) in every wave -> workgroup
+//              barrier -> one lane stores the message number into the
+//              block's flag word in the consumer's page (system scope);
+//   consumer:  the matching block's lane polls that flag (relaxed
+//              system-scope loads, s_sleep, bounded) -> workgroup barrier ->
+//              payload read with system-scope (sc0 sc1) loads, so no cached
+//              copy is used.
+// Each get block waits for its own put block only, so the two halves of an
+// exchange overlap, and no two blocks poll or write the same word.
 // tools/ipc_probe.hip measured the forms on one MI355X with two processes:
 // plain stores behind a single release lose words across XCDs; a release per
 // block is correct but 3x slower at 2-8 MB; write-through stores are correct
@@ -90,15 +92,15 @@ struct Share {
   bool pairs;
   unsigned w, ny, e0, e1;
 };
-__device__ __forceinline__ Share share_of(const CopyItem &it, int sub, bool pairs, unsigned per) {
+__device__ __forceinline__ Share share_of(const CopyItem &it, const IpcBlock &b, bool pairs) {
   Share s;
   s.pairs = pairs && (it.nx & 1) == 0;
   s.w = s.pairs ? (unsigned)it.nx / 2 : (unsigned)it.nx;
   s.ny = (unsigned)it.ny;
   const unsigned n = s.w * s.ny * (unsigned)it.nz;
-  if (s.pairs) per /= 2;
-  s.e0 = (unsigned)sub * per;
-  s.e1 = min(n, s.e0 + per);
+  const unsigned sh = s.pairs ? 1 : 0;  // (block ranges are in elements, even for pairs)
+  s.e0 = b.e0 >> sh;
+  s.e1 = min(n, b.e1 >> sh);
   return s;
 }
 // a field region whose rows all start on a 16-B (double) / 8-B (float) pair
@@ -142,12 +144,12 @@ __device__ __forceinline__ void move_share(unsigned e0, unsigned e1, Load load, 
 // put: a block's share of one item, field -> peer's message slot (rows packed:
 // pair t is message elements 2t, 2t+1)
 template <class T>
-__device__ __forceinline__ void put_share(const CopyItem &it, int sub, unsigned per,
+__device__ __forceinline__ void put_share(const CopyItem &it, const IpcBlock &b,
                                           T *const *src_tab, const IpcPeers &pp, int p) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   const T *src = src_tab[it.src] + it.soff;
-  const Share s = share_of(it, sub, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
-                                        (it.doff & 1) == 0, per);
+  const Share s = share_of(it, b, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
+                                        (it.doff & 1) == 0);
   const Rows rw{s.w, s.ny, it.ssy, it.ssz};
   const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
   const long mo = it.doff;
@@ -162,12 +164,12 @@ __device__ __forceinline__ void put_share(const CopyItem &it, int sub, unsigned 
 
 // get: a block's share of one item, my message slot -> field ghosts
 template <class T>
-__device__ __forceinline__ void get_share(const CopyItem &it, int sub, unsigned per,
+__device__ __forceinline__ void get_share(const CopyItem &it, const IpcBlock &b,
                                           T *const *dst_tab, const IpcPeers &pp, int p) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   T *dst = dst_tab[it.dst] + it.doff;
-  const Share s = share_of(it, sub, pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz) &&
-                                        (it.soff & 1) == 0, per);
+  const Share s = share_of(it, b, pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz) &&
+                                        (it.soff & 1) == 0);
   const Rows rw{s.w, s.ny, it.dsy, it.dsz};
   const __amdgpu_buffer_rsrc_t r = rsrc(pp.buf[p]);
   const long mo = it.soff;
@@ -181,13 +183,13 @@ __device__ __forceinline__ void get_share(const CopyItem &it, int sub, unsigned 
                   [&](unsigned t, T v) { dst[rw.at(t, 1)] = v; });
 }
 
-// A workgroup's wait for peer p's condition (slot free / message complete),
-// at most once per launch: the condition holds for the rest of the launch once
-// met, so `passed` (uniform, bit p) remembers it.  A timed-out wait skips the
-// copy; the block is still counted, so no peer waits on this one in turn.
-__device__ __forceinline__ bool wait_once(const IpcPeers &pp, int p, unsigned &passed, int &ok) {
+// A workgroup's wait for peer p's slot to be free, at most once per launch:
+// the condition holds for the rest of the launch once met, so `passed`
+// (uniform, bit p) remembers it.  A timed-out wait skips the copy; the block
+// is still flagged, so no peer waits on this one in turn.
+__device__ __forceinline__ bool wait_slot(const IpcPeers &pp, int p, unsigned &passed, int &ok) {
   if (passed >> p & 1u) return true;
-  if (threadIdx.x == 0) ok = ipc_wait(pp.wait[p], pp.wait_val[p], pp.err, pp.timeout);
+  if (threadIdx.x == 0) ok = ipc_wait(pp.ack[p], pp.val[p], pp.err, pp.timeout);
   __syncthreads();
   const bool go = ok != 0;
   __syncthreads();  // (ok is rewritten by the next wait)
@@ -195,31 +197,47 @@ __device__ __forceinline__ bool wait_once(const IpcPeers &pp, int p, unsigned &p
   return go;
 }
 
-// after every wave's memory operations are drained, one lane adds the
-// workgroup's blocks per peer to the peers' counters (one atomic per peer
-// and workgroup instead of one per block: the counters are single words that
-// every block of an exchange would otherwise contend on)
-__device__ __forceinline__ void count_blocks(unsigned *done, const IpcPeers &pp) {
+// A get block's wait for its own flag: the sender's put block for the same
+// message range has landed (one word per block, so no two blocks poll or
+// write the same word)
+__device__ __forceinline__ bool wait_block(const IpcPeers &pp, int p, int flag, int &ok) {
+  if (threadIdx.x == 0) ok = ipc_wait(pp.flags[p] + flag, pp.seq[p], pp.err, pp.timeout);
+  __syncthreads();
+  const bool go = ok != 0;
+  __syncthreads();
+  return go;
+}
+
+// a put block's payload is drained from every wave, then one lane raises the
+// block's flag in the receiver's page
+__device__ __forceinline__ void flag_block(const IpcPeers &pp, int p, int flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) st_word(pp.flags[p] + flag, pp.seq[p]);
+}
+
+// after every wave's loads are drained, one lane adds the workgroup's
+// consumed blocks per sender to the senders' acknowledgement counters (one
+// atomic per sender and workgroup)
+__device__ __forceinline__ void ack_blocks(unsigned *done, const IpcPeers &pp) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
     for (int q = 0; q < pp.n; ++q)
-      if (done[q]) {
-        __hip_atomic_fetch_add(pp.count[q], (unsigned long long)done[q], __ATOMIC_RELAXED,
+      if (done[q])
+        __hip_atomic_fetch_add(pp.ack[q], (unsigned long long)done[q], __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-        done[q] = 0;
-      }
 }
 
 // local: a block's share of a same-rank copy, field -> field
 template <class T>
-__device__ __forceinline__ void local_share(const CopyItem &it, int sub, unsigned per,
+__device__ __forceinline__ void local_share(const CopyItem &it, const IpcBlock &b,
                                             T *const *src_tab, T *const *dst_tab) {
   using V = typename std::conditional<sizeof(T) == 8, double2, float2>::type;
   const T *src = src_tab[it.src] + it.soff;
   T *dst = dst_tab[it.dst] + it.doff;
-  const Share s = share_of(it, sub, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
-                                        pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz), per);
+  const Share s = share_of(it, b, pairable(src_tab[it.src], it.soff, it.ssy, it.ssz) &&
+                                        pairable(dst_tab[it.dst], it.doff, it.dsy, it.dsz));
   const Rows rs{s.w, s.ny, it.ssy, it.ssz}, rd{s.w, s.ny, it.dsy, it.dsz};
   if (s.pairs)
     move_share<V>(s.e0, s.e1,
@@ -243,39 +261,32 @@ __global__ __launch_bounds__(256) void k_exchange(const CopyItem *__restrict__ p
                                                   const CopyItem *__restrict__ loc_items,
                                                   const CopyItem *__restrict__ get_items,
                                                   const IpcBlock *__restrict__ blocks, int npu,
-                                                  int nlo, int nall, unsigned per,
+                                                  int nlo, int nall,
                                                   T *const *__restrict__ src_tab,
                                                   T *const *__restrict__ dst_tab,
                                                   const IpcPeers pput, const IpcPeers pget) {
   __shared__ int ok;
-  // blocks this workgroup has moved per peer and not yet counted (lane 0 only)
-  __shared__ unsigned done_put[kMaxIpcPeers], done_get[kMaxIpcPeers];
+  __shared__ unsigned done_get[kMaxIpcPeers];  // blocks consumed per sender (lane 0 only)
   if (threadIdx.x == 0)
-    for (int q = 0; q < kMaxIpcPeers; ++q) done_put[q] = done_get[q] = 0;
-  unsigned passed_put = 0, passed_get = 0;  // (uniform)
-  bool puts_counted = false;
+    for (int q = 0; q < kMaxIpcPeers; ++q) done_get[q] = 0;
+  unsigned passed = 0;  // peers whose slot this workgroup has seen free (uniform)
   for (int v = blockIdx.x; v < nall; v += gridDim.x) {  // (uniform per workgroup)
     const IpcBlock b = blocks[v];
     if (v < npu) {
       const CopyItem &it = put_items[b.item];
       const int p = __builtin_amdgcn_readfirstlane(it.pad);
-      if (wait_once(pput, p, passed_put, ok)) put_share<T>(it, b.sub, per, src_tab, pput, p);
-      if (threadIdx.x == 0) ++done_put[p];
+      if (wait_slot(pput, p, passed, ok)) put_share<T>(it, b, src_tab, pput, p);
+      flag_block(pput, p, b.flag);
     } else if (v < npu + nlo) {
-      local_share<T>(loc_items[b.item], b.sub, per, src_tab, dst_tab);
+      local_share<T>(loc_items[b.item], b, src_tab, dst_tab);
     } else {
-      if (!puts_counted) {  // my puts reach the peers before I wait on theirs
-        count_blocks(done_put, pput);
-        puts_counted = true;
-      }
       const CopyItem &it = get_items[b.item];
       const int p = __builtin_amdgcn_readfirstlane(it.pad);
-      if (wait_once(pget, p, passed_get, ok)) get_share<T>(it, b.sub, per, dst_tab, pget, p);
+      if (wait_block(pget, p, b.flag, ok)) get_share<T>(it, b, dst_tab, pget, p);
       if (threadIdx.x == 0) ++done_get[p];
     }
   }
-  if (!puts_counted) count_blocks(done_put, pput);
-  count_blocks(done_get, pget);  // acknowledgements to the senders
+  ack_blocks(done_get, pget);
 }
 
 __global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned long long *err) {
@@ -311,29 +322,29 @@ inline void check_launch() {
 template <class T>
 static void exchange_t(const CopyItem *put_items, const CopyItem *loc_items,
                        const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
-                       int per, T *const *src_tab, T *const *dst_tab, const IpcPeers &pput,
+                       T *const *src_tab, T *const *dst_tab, const IpcPeers &pput,
                        const IpcPeers &pget, int grid_cap, hipStream_t st) {
   const int n = npu + nlo + nge;
   if (n <= 0) return;
   const int g = grid_cap > 0 && grid_cap < n ? grid_cap : n;  // (the Comm always caps)
   k_exchange<T><<<dim3((unsigned)g), dim3(256), 0, st>>>(put_items, loc_items, get_items, blocks,
-                                                         npu, nlo, n, (unsigned)per, src_tab,
+                                                         npu, nlo, n, src_tab,
                                                          dst_tab, pput, pget);
   check_launch();
 }
 
 void ipc_exchange(const CopyItem *put_items, const CopyItem *loc_items, const CopyItem *get_items,
-                  const IpcBlock *blocks, int npu, int nlo, int nge, int per,
+                  const IpcBlock *blocks, int npu, int nlo, int nge,
                   double *const *src_tab, double *const *dst_tab, const IpcPeers &pput,
                   const IpcPeers &pget, int grid_cap, hipStream_t st) {
-  exchange_t<double>(put_items, loc_items, get_items, blocks, npu, nlo, nge, per, src_tab, dst_tab,
+  exchange_t<double>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
                      pput, pget, grid_cap, st);
 }
 void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
                     const CopyItem *get_items, const IpcBlock *blocks, int npu, int nlo, int nge,
-                    int per, float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
+                    float *const *src_tab, float *const *dst_tab, const IpcPeers &pput,
                     const IpcPeers &pget, int grid_cap, hipStream_t st) {
-  exchange_t<float>(put_items, loc_items, get_items, blocks, npu, nlo, nge, per, src_tab, dst_tab,
+  exchange_t<float>(put_items, loc_items, get_items, blocks, npu, nlo, nge, src_tab, dst_tab,
                     pput, pget, grid_cap, st);
 }
 
