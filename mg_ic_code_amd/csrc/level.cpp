@@ -113,8 +113,9 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   // all its puts before its first get; and the grid is capped so that every
   // workgroup of every rank on this GPU can be resident at once.  Then no get
   // can hold a slot a put needs, whatever order the hardware dispatches
-  // workgroups in.  One workgroup per CU for one rank per GPU (grids of 64 ..
-  // 1024 measured alike on the 8-GPU share, profiles/r03m_share_ipc_cap_sweep.txt);
+  // workgroups in.  Two workgroups per CU for one rank per GPU (a quarter of
+  // what fits: 8 per CU at the kernel's 8 waves per SIMD; 512 measured 0.8%
+  // faster than 256 on the 8-GPU share, profiles/r04l_exchange_cap_sweep.txt);
   // ranks sharing a GPU split half the CUs (r03i rehearsals).
   {
     int dev = 0, ncu = 0;
@@ -123,7 +124,7 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
     ncu = std::max(ncu, 8);
     const char *ce = getenv("MGIC_IPC_GRID_CAP");
     grid_cap_ = ce && atoi(ce) > 0 ? atoi(ce)
-                                   : (colocated > 1 ? std::max(8, ncu / (2 * colocated)) : ncu);
+                                   : (colocated > 1 ? std::max(8, ncu / (2 * colocated)) : 2 * ncu);
   }
 }
 
