@@ -150,6 +150,12 @@ MGIC_API int mgic_plan_create_shell(int rank, int size, const int domain[6],
  * it: 0, or an error when that transport cannot execute it (the peer-mapped
  * transport takes at most 32 peers per plan; RCCL has no such limit) */
 MGIC_API int mgic_plan_check_transport(mgic_plan p, int transport);
+/* the peer-mapped transport's block table of this plan (built as by
+ * mgic_plan_check_transport(p, 2)): *n put and get blocks; with rows != NULL,
+ * five values per block: side (0 put, 1 get), peer rank, flag, first element
+ * in the message, element count.  Both sides of a message must list the same
+ * (flag, first, count) rows: a get block waits for the put block of its flag */
+MGIC_API int mgic_plan_ipc_blocks(mgic_plan p, int *n, long long *rows);
 MGIC_API int mgic_plan_destroy(mgic_plan p);
 MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpack, int *n_peers);
 MGIC_API int mgic_plan_items(mgic_plan p, int which, long long *items);

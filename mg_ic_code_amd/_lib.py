@@ -109,6 +109,7 @@ SIGNATURES = {
     "mgic_plan_create": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PI, PI, c_int, c_int, PH],
     "mgic_plan_create_shell": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PH],
     "mgic_plan_check_transport": [H, c_int],
+    "mgic_plan_ipc_blocks": [H, PI, PLL],
     "mgic_plan_destroy": [H],
     "mgic_plan_sizes": [H, PI, PI, PI, PI],
     "mgic_plan_items": [H, c_int, PLL],

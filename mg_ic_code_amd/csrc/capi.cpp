@@ -416,6 +416,19 @@ MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpa
     if (n_peers) *n_peers = (int)peers.size();
   });
 }
+MGIC_API int mgic_plan_ipc_blocks(mgic_plan p, int *n, long long *rows) {
+  return guard([&] {
+    NEED(p);
+    NEED(n);
+    p->plan->finalize_ipc_host(kern::kIpcBlockElemsDefault);
+    const auto r = p->plan->ipc_block_rows();
+    *n = (int)r.size();
+    if (rows)
+      for (size_t i = 0; i < r.size(); ++i)
+        for (int c = 0; c < 5; ++c) rows[5 * i + c] = r[i][c];
+  });
+}
+
 MGIC_API int mgic_plan_items(mgic_plan p, int which, long long *items) {
   return guard([&] {
     NEED(p);

@@ -583,6 +583,20 @@ void CopyPlan::finalize_ipc_host(long per) {
   ipc_host_ = true;
 }
 
+std::vector<std::array<long long, 5>> CopyPlan::ipc_block_rows() const {
+  std::vector<std::array<long long, 5>> rows;
+  for (int v = 0; v < (int)xblocks_h_.size(); ++v) {
+    if (v >= n_put_blocks_ && v < n_put_blocks_ + n_loc_blocks_) continue;
+    const bool put = v < n_put_blocks_;
+    const kern::IpcBlock &b = xblocks_h_[v];
+    const CopyItem &it = put ? ipc_pack_h_[b.item] : ipc_unpack_h_[b.item];
+    const int peer = put ? send_peers_[it.pad] : recv_peers_[it.pad];
+    rows.push_back({put ? 0LL : 1LL, (long long)peer, (long long)b.flag,
+                    (long long)(put ? it.doff : it.soff) + b.e0, (long long)(b.e1 - b.e0)});
+  }
+  return rows;
+}
+
 void CopyPlan::finalize_ipc(long per) {
   if (ipc_final_) return;
   finalize();

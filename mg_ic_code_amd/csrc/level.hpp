@@ -11,6 +11,7 @@
 
 #include <rccl/rccl.h>
 
+#include <array>
 #include <map>
 
 #include "kernels.hpp"
@@ -137,6 +138,9 @@ class CopyPlan {
   // the peer-mapped transport's host tables only (raises when the plan has
   // more peers than that transport takes: kern::kMaxIpcPeers)
   void finalize_ipc_host(long per);
+  // after finalize_ipc_host: per put / get block {side (0 put, 1 get), peer
+  // rank, flag, first message element, element count}
+  std::vector<std::array<long long, 5>> ipc_block_rows() const;
   // src_tab / dst_tab: device tables of valid-lo pointers per local box
   void execute(Comm &comm, double *const *src_tab, double *const *dst_tab, hipStream_t st);
   // the same copies on fp32 fields (same element offsets; messages in floats)

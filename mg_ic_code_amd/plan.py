@@ -81,6 +81,17 @@ class HostPlan:
         most 32 peers per plan)."""
         _lib.call("mgic_plan_check_transport", self._h, {"rccl": 1, "ipc": 2}[transport])
 
+    def ipc_blocks(self) -> np.ndarray:
+        """The peer-mapped transport's put / get blocks: rows (side 0 put /
+        1 get, peer rank, flag, first message element, element count)."""
+        n = ctypes.c_int()
+        _lib.call("mgic_plan_ipc_blocks", self._h, ctypes.byref(n), None)
+        out = np.zeros((n.value, 5), dtype=np.int64)
+        if n.value:
+            _lib.call("mgic_plan_ipc_blocks", self._h, ctypes.byref(n),
+                      out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)))
+        return out
+
     def geom(self, layout, n):
         """(sy, sz, origin, total) of local box n; layout 0 = src, 1 = dst."""
         g = (ctypes.c_longlong * 4)()

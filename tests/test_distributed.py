@@ -332,3 +332,64 @@ def test_gather_plan_with_many_peers_is_rccl_executable():
     ex = HostPlan(5, world, dom, boxes, owners)
     ex.check_transport("rccl")
     ex.check_transport("ipc")
+
+
+def _message_rows(plans, world):
+    """{(sender, receiver): (put rows, get rows)} of every message, each as
+    sorted (flag, first element, count) tuples."""
+    msgs = {}
+    for r, plan in enumerate(plans):
+        for side, peer, flag, first, cnt in plan.ipc_blocks().tolist():
+            key = (r, peer) if side == 0 else (peer, r)
+            msgs.setdefault(key, ([], []))[side].append((flag, first, cnt))
+    return {k: (sorted(p), sorted(g)) for k, (p, g) in msgs.items()}
+
+
+@pytest.mark.parametrize("world,shell,periodic", [(2, 4, (0, 0, 0)), (4, 4, (0, 0, 0)),
+                                                  (8, 4, (0, 0, 0)), (8, 0, (0, 0, 0)),
+                                                  (8, 4, (1, 1, 1)), (3, 1, (1, 0, 1))])
+def test_ipc_message_blocks_agree_on_both_sides(world, shell, periodic):
+    # the peer-mapped transport's hand-off: get block f of a message waits for
+    # the flag of put block f, so both sides must split every message into the
+    # same blocks, numbered by message offset 0, 1, ... (bench.py's splits,
+    # shells and faces, periodic images as self messages, small edge items;
+    # world 3: six boxes, two per rank)
+    from mg_ic_code_amd.decomposition import decompose
+    n = 40
+    if world == 3:
+        dom = (0, 0, 0, 47, n - 1, n - 1)
+        boxes, owners = split_domain(dom, (3, 2, 1)), [0, 1, 2, 2, 1, 0]
+    else:
+        dom, boxes, owners = decompose((n, n, n), world)
+    plans = [HostPlan(r, world, dom, list(boxes), list(owners), periodic=periodic, shell=shell)
+             for r in range(world)]
+    msgs = _message_rows(plans, world)
+    assert msgs
+    for (s, r), (put, get) in msgs.items():
+        assert put == get, (s, r)
+        flags = [f for f, _, _ in put]
+        assert flags == list(range(len(put)))
+        firsts = [a for _, a, _ in put]
+        assert firsts == sorted(firsts) and firsts[0] == 0
+        # the blocks tile the message: contiguous, no gaps
+        assert all(a + c == b for (_, a, c), (_, b, _) in zip(put, put[1:]))
+        send = next(p for p in plans[s].peers if p["peer"] == r)
+        assert firsts[-1] + put[-1][2] == send["send_cnt"]
+
+
+def test_ipc_message_blocks_agree_for_the_gather_to_rank0():
+    # agglomeration: the coarse level's boxes gathered onto rank 0 and
+    # scattered back, the plans bench.py's N > 1 runs build
+    world = 8
+    dom = (0, 0, 0, 31, 31, 31)
+    boxes = split_domain(dom, (2, 2, 2))
+    owners = list(range(world))
+    gather = [HostPlan(r, world, dom, boxes, owners, dst_boxes=[dom], dst_owners=[0],
+                       with_valid=True, with_faces=False) for r in range(world)]
+    scatter = [HostPlan(r, world, dom, [dom], [0], boxes, owners, with_valid=True,
+                        with_faces=True) for r in range(world)]
+    for plans in (gather, scatter):
+        msgs = _message_rows(plans, world)
+        assert len(msgs) == world - 1
+        for (s, r), (put, get) in msgs.items():
+            assert put == get and [f for f, _, _ in put] == list(range(len(put)))
