@@ -658,7 +658,7 @@ __global__ __launch_bounds__(256) void k_bicg_p(double *__restrict__ p,
 
 template <int KIND>
 __global__ __launch_bounds__(RB) void k_reduce_final(const double *__restrict__ p, int n,
-                                                     double *__restrict__ out) {
+                                                     double *__restrict__ out, const HostPub pub) {
   __shared__ double sm[RB];
   double acc = red_init<KIND>();
   for (int t = threadIdx.x; t < n; t += RB) acc = red_op<KIND>(acc, p[t]);
@@ -668,7 +668,10 @@ __global__ __launch_bounds__(RB) void k_reduce_final(const double *__restrict__ 
     if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = sm[0];
+  if (threadIdx.x == 0) {
+    out[0] = sm[0];
+    publish(pub, sm[0]);
+  }
 }
 
 // max-type kinds (3, 4, 5): any order gives the same result, so a wide
@@ -676,7 +679,8 @@ __global__ __launch_bounds__(RB) void k_reduce_final(const double *__restrict__ 
 // thread loop above is latency bound: 16 K residual partials took 25 us)
 template <int KIND>
 __global__ __launch_bounds__(1024) void k_reduce_final_wide(const double *__restrict__ p, int n,
-                                                           double *__restrict__ out) {
+                                                           double *__restrict__ out,
+                                                           const HostPub pub) {
   static_assert(KIND >= 3, "order-independent reductions only");
   __shared__ double sm[16];
   double a0 = red_init<KIND>(), a1 = a0, a2 = a0, a3 = a0;
@@ -696,7 +700,12 @@ __global__ __launch_bounds__(1024) void k_reduce_final_wide(const double *__rest
     double m = sm[0];
     for (int w = 1; w < 16; ++w) m = red_op<KIND>(m, sm[w]);
     out[0] = m;
+    publish(pub, m);
   }
+}
+
+__global__ void k_publish(const double *__restrict__ v, const HostPub pub) {
+  if (threadIdx.x == 0) publish(pub, *v);
 }
 
 template <class T>
@@ -1296,16 +1305,23 @@ int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
   return (int)nb;
 }
 
-void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st) {
+void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st,
+                  const HostPub &pub) {
   switch (kind) {
-    case 0: k_reduce_final<0><<<1, RB, 0, st>>>(partials, n, out); break;
-    case 1: k_reduce_final<1><<<1, RB, 0, st>>>(partials, n, out); break;
-    case 2: k_reduce_final<2><<<1, RB, 0, st>>>(partials, n, out); break;
-    case 3: k_reduce_final_wide<3><<<1, 1024, 0, st>>>(partials, n, out); break;
-    case 4: k_reduce_final_wide<4><<<1, 1024, 0, st>>>(partials, n, out); break;
-    case 5: k_reduce_final_wide<5><<<1, 1024, 0, st>>>(partials, n, out); break;
+    case 0: k_reduce_final<0><<<1, RB, 0, st>>>(partials, n, out, pub); break;
+    case 1: k_reduce_final<1><<<1, RB, 0, st>>>(partials, n, out, pub); break;
+    case 2: k_reduce_final<2><<<1, RB, 0, st>>>(partials, n, out, pub); break;
+    case 3: k_reduce_final_wide<3><<<1, 1024, 0, st>>>(partials, n, out, pub); break;
+    case 4: k_reduce_final_wide<4><<<1, 1024, 0, st>>>(partials, n, out, pub); break;
+    case 5: k_reduce_final_wide<5><<<1, 1024, 0, st>>>(partials, n, out, pub); break;
     default: throw Error(kBadArg, "reduce: bad kind");
   }
+  check_launch();
+}
+
+void publish_result(const double *d_val, const HostPub &pub, hipStream_t st) {
+  if (!pub.val) return;
+  k_publish<<<1, 64, 0, st>>>(d_val, pub);
   check_launch();
 }
 

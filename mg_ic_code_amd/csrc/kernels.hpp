@@ -98,7 +98,35 @@ void blas(int kind, double *x, const double *y, const double *z, double s, doubl
 int reduce_partial(int kind, const double *x, const double *y, const BoxArgs &g,
                    double *partials, hipStream_t st);
 constexpr int kMaxPartsPerBox = 2048;
-void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st);
+// A reduction's result published by its last kernel straight into pinned,
+// host-coherent memory (Comm::host_pub): the value and, for the last result
+// of a readback, the peer-mapped transport's error word and then the sequence
+// number the host spins on (Comm::wait_results) -- no copy operation and no
+// stream synchronisation per readback.  val == nullptr: nothing is published.
+struct HostPub {
+  double *val = nullptr;
+  unsigned long long *seq = nullptr;
+  unsigned long long seqv = 0;
+  const unsigned long long *err_src = nullptr;  // device error word
+  unsigned long long *err_dst = nullptr;
+};
+__device__ __forceinline__ void publish(const HostPub &p, double v) {
+  if (!p.val) return;
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p.val),
+                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!p.seq) return;
+  if (p.err_dst)
+    __hip_atomic_store(p.err_dst,
+                       __hip_atomic_load(p.err_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __hip_atomic_store(p.seq, p.seqv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+void reduce_final(int kind, const double *partials, int n, double *out, hipStream_t st,
+                  const HostPub &pub = HostPub());
+// publish *d_val (after a collective on it)
+void publish_result(const double *d_val, const HostPub &pub, hipStream_t st);
 
 // BiCGStab's fused vector updates (bit-identical to the separate passes):
 // s = r + ca*v, e = e + cb*pt and the partials of reduction `kind` (1 sum|s|,

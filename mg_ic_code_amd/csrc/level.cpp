@@ -2,8 +2,10 @@
 #include "level.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <type_traits>
 
 namespace mgic {
@@ -19,7 +21,54 @@ Comm::Comm(int rank, int size, const ncclUniqueId *id, bool force_rccl)
     MGIC_NCCL(ncclCommInitRank(&nccl_, size, *id, rank));
   }
   MGIC_HIP(hipMalloc(&d_result_, kResultSlots * sizeof(double)));
-  MGIC_HIP(hipHostMalloc(&h_result_, kResultSlots * sizeof(double), hipHostMallocDefault));
+  alloc_host_block();
+}
+
+// results, staging word, error word and sequence number in one pinned,
+// host-coherent block: the GPU's stores reach the host without a copy
+void Comm::alloc_host_block() {
+  void *p = nullptr;
+  MGIC_HIP(hipHostMalloc(&p, (kResultSlots + 3) * sizeof(double), hipHostMallocCoherent));
+  h_result_ = static_cast<double *>(p);
+  for (int i = 0; i < kResultSlots + 1; ++i) h_result_[i] = 0.0;
+  h_err_ = reinterpret_cast<unsigned long long *>(h_result_ + kResultSlots + 1);
+  h_seq_ = h_err_ + 1;
+  *h_err_ = 0;
+  *h_seq_ = 0;
+}
+
+kern::HostPub Comm::host_pub(int slot, bool last) {
+  MGIC_CHECK(slot >= 0 && slot < kResultSlots, "result slot");
+  kern::HostPub p;
+  p.val = h_result_ + slot;
+  if (last) {
+    p.seq = h_seq_;
+    p.seqv = ++pub_count_;
+    if (ipc_) {
+      p.err_src = sig_ + kern::kSigErr;
+      p.err_dst = h_err_;
+    }
+  }
+  return p;
+}
+
+void Comm::wait_results(hipStream_t st) {
+  const unsigned long long want = pub_count_;
+  for (unsigned long long i = 0;; ++i) {
+    if (__atomic_load_n(h_seq_, __ATOMIC_ACQUIRE) >= want) break;
+    if ((i & 1023) == 1023) {
+      // a faulted or finished stream that never published: report, not spin
+      const hipError_t e = hipStreamQuery(st);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(h_seq_, __ATOMIC_ACQUIRE) >= want) break;
+        throw Error(kState, "reduction result was not published");
+      }
+      if (e != hipErrorNotReady) MGIC_HIP(e);
+      if (i > (1ull << 22)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    __builtin_ia32_pause();
+  }
+  ipc_err_raise();
 }
 
 // the peer-mapped transport: signal page + receive arena per rank, mapped by
@@ -39,9 +88,7 @@ Comm::Comm(int rank, int size, HostAllgather allgather, void *user, size_t arena
   MGIC_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   own_stream_ = true;
   MGIC_HIP(hipMalloc(&d_result_, kResultSlots * sizeof(double)));
-  MGIC_HIP(hipHostMalloc(&h_result_, kResultSlots * sizeof(double), hipHostMallocDefault));
-  MGIC_HIP(hipHostMalloc(&h_err_, sizeof(unsigned long long), hipHostMallocDefault));
-  *h_err_ = 0;
+  alloc_host_block();
   // counters are polled across processes / devices: uncached memory
   MGIC_HIP(hipExtMallocWithFlags((void **)&sig_, sizeof(unsigned long long) * kern::sig_words(size),
                                  hipDeviceMallocUncached));
@@ -207,7 +254,6 @@ Comm::~Comm() {
     }
     if (sig_) (void)hipFree(sig_);
     if (arena_) (void)hipFree(arena_);
-    if (h_err_) (void)hipHostFree(h_err_);
     if (barrier_val_) (void)hipFree(barrier_val_);
   }
   if (d_partials_) (void)hipFree(d_partials_);
@@ -225,8 +271,11 @@ double *Comm::d_partials(int n) {
   return d_partials_;
 }
 
-void Comm::allreduce(double *d_val, int op) {
-  if (size_ == 1) return;
+void Comm::allreduce(double *d_val, int op, const kern::HostPub &pub) {
+  if (size_ == 1) {
+    kern::publish_result(d_val, pub, stream_);
+    return;
+  }
   if (ipc_) {
     kern::IpcReduce r{};
     r.size = size_;
@@ -235,11 +284,12 @@ void Comm::allreduce(double *d_val, int op) {
     r.parity = (int)(r.count & 1);
     r.timeout = timeout_ticks_;
     for (int q = 0; q < size_; ++q) r.sig[q] = peer_sig_[q];
-    kern::ipc_allreduce(d_val, op, r, ipc_err(), stream_);
+    kern::ipc_allreduce(d_val, op, r, ipc_err(), pub, stream_);
     return;
   }
-  if (!nccl_) return;
-  MGIC_NCCL(ncclAllReduce(d_val, d_val, 1, ncclDouble, op == 1 ? ncclMax : ncclSum, nccl_, stream_));
+  if (nccl_)
+    MGIC_NCCL(ncclAllReduce(d_val, d_val, 1, ncclDouble, op == 1 ? ncclMax : ncclSum, nccl_, stream_));
+  kern::publish_result(d_val, pub, stream_);
 }
 
 // ------------------------------------------------------------------ Grid

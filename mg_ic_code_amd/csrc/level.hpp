@@ -58,8 +58,9 @@ class Comm {
   ncclComm_t nccl() const { return nccl_; }
   hipStream_t stream() const { return stream_; }
   void set_stream(hipStream_t s) { stream_ = s; }
-  // in-place allreduce of one device double (op: 0 sum, 1 max)
-  void allreduce(double *d_val, int op);
+  // in-place allreduce of one device double (op: 0 sum, 1 max); pub: the
+  // result also published to the host (host_pub)
+  void allreduce(double *d_val, int op, const kern::HostPub &pub = kern::HostPub());
   // scratch for reductions (device partials + result, pinned host result)
   double *d_partials(int n);
   // reduction results (device) and their host copies (pinned): slots 0-1 for
@@ -67,6 +68,15 @@ class Comm {
   static constexpr int kResultSlots = 4;
   double *d_result() const { return d_result_; }
   double *h_result() const { return h_result_; }
+  // a reduction's readback: the final kernel (or the allreduce) publishes
+  // result `slot` into h_result(); `last` also publishes the transport's error
+  // word and the sequence number wait_results() spins on
+  kern::HostPub host_pub(int slot, bool last);
+  // until the last host_pub(…, true) result has landed (host spin on pinned
+  // memory, no stream synchronisation); raises a transport timeout
+  void wait_results(hipStream_t st);
+  // staging word for a host -> device copy (synchronised by its caller)
+  double *h_stage() const { return h_result_ + kResultSlots; }
 
   // ---- peer-mapped transport (transport.hpp)
   size_t ipc_arena_bytes() const { return arena_bytes_; }
@@ -108,7 +118,12 @@ class Comm {
   double *d_partials_ = nullptr;
   int n_partials_ = 0;
   double *d_result_ = nullptr;
+  // pinned, host-coherent: kResultSlots results, a staging word, the error
+  // word and the published sequence number
   double *h_result_ = nullptr;
+  unsigned long long *h_seq_ = nullptr;
+  unsigned long long pub_count_ = 0;
+  void alloc_host_block();
   bool ipc_ = false;
   int grid_cap_ = 0;
   long block_elems_ = kern::kIpcBlockElemsDefault;

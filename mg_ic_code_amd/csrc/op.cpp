@@ -186,10 +186,7 @@ double VariableCoeffPoissonOperator::residualNorm(LevelData &lhs, LevelData &dps
     off += kern::residual_norm_blocks(a);
   }
   finish_reduce(3, parts, (int)total, 0);
-  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
-  c.ipc_err_async(st);
-  MGIC_HIP(hipStreamSynchronize(st));
-  c.ipc_err_raise();
+  c.wait_results(st);
   return c.h_result()[0];
 }
 
@@ -702,19 +699,25 @@ void VariableCoeffPoissonOperator::setVal(LevelData &lhs, double v) {
     kern::blas(5, lhs.p[n], nullptr, nullptr, v, 0.0, args_plain_[n], stream());
 }
 
-double VariableCoeffPoissonOperator::finish_reduce(int kind, double *parts, int total, int slot) {
+// the final step of a reduction into result slot `slot`, published to the
+// host by its last kernel (the final reduction on one rank, the allreduce on
+// several); `last`: the readback's last result (Comm::wait_results)
+void VariableCoeffPoissonOperator::finish_reduce(int kind, double *parts, int total, int slot,
+                                                 bool last) {
   Comm &c = *grid->comm;
   const hipStream_t st = stream();
   double *res = c.d_result() + slot;
+  const kern::HostPub pub = c.host_pub(slot, last);
+  const bool solo = c.size() == 1;
   if (total == 0) {  // no local cells: the identity of the reduction
-    c.h_result()[1] = kind >= 4 ? -HUGE_VAL : 0.0;  // pinned: safe for an async copy
-    MGIC_HIP(hipMemcpyAsync(res, c.h_result() + 1, sizeof(double), hipMemcpyHostToDevice, st));
-    MGIC_HIP(hipStreamSynchronize(st));
-  } else {
-    kern::reduce_final(kind, parts, total, res, st);
+    *c.h_stage() = kind >= 4 ? -HUGE_VAL : 0.0;
+    MGIC_HIP(hipMemcpyAsync(res, c.h_stage(), sizeof(double), hipMemcpyHostToDevice, st));
+    MGIC_HIP(hipStreamSynchronize(st));  // (the staging word is reused)
+    c.allreduce(res, kind >= 3 ? 1 : 0, pub);
+    return;
   }
-  c.allreduce(res, kind >= 3 ? 1 : 0);
-  return 0.0;
+  kern::reduce_final(kind, parts, total, res, st, solo ? pub : kern::HostPub());
+  if (!solo) c.allreduce(res, kind >= 3 ? 1 : 0, pub);
 }
 
 double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const LevelData *y) {
@@ -725,10 +728,7 @@ double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const 
   for (int n = 0; n < grid->nlocal(); ++n)
     total += kern::reduce_partial(kind, x.p[n], y ? y->p[n] : nullptr, args_plain_[n], parts + total, st);
   finish_reduce(kind, parts, total, 0);
-  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
-  c.ipc_err_async(st);
-  MGIC_HIP(hipStreamSynchronize(st));
-  c.ipc_err_raise();
+  c.wait_results(st);
   return c.h_result()[0];
 }
 
@@ -746,10 +746,7 @@ double VariableCoeffPoissonOperator::axpy2Norm(LevelData &s, const LevelData &r,
     total += kern::axpy2_reduce(kind, s.p[n], r.p[n], v.p[n], ca, e.p[n], pt.p[n], cb,
                                 args_plain_[n], parts + total, st);
   finish_reduce(kind, parts, total, 0);
-  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), sizeof(double), hipMemcpyDeviceToHost, st));
-  c.ipc_err_async(st);
-  MGIC_HIP(hipStreamSynchronize(st));
-  c.ipc_err_raise();
+  c.wait_results(st);
   const double x = c.h_result()[0];
   return kind == 2 ? std::sqrt(x) : x;
 }
@@ -772,12 +769,9 @@ void VariableCoeffPoissonOperator::dot2(const LevelData &t, const LevelData &s, 
                                      parts + cap + total, st);
     total += k;
   }
-  finish_reduce(0, parts, total, 0);
-  finish_reduce(0, parts + cap, total, 1);
-  MGIC_HIP(hipMemcpyAsync(c.h_result(), c.d_result(), 2 * sizeof(double), hipMemcpyDeviceToHost, st));
-  c.ipc_err_async(st);
-  MGIC_HIP(hipStreamSynchronize(st));
-  c.ipc_err_raise();
+  finish_reduce(0, parts, total, 0, false);
+  finish_reduce(0, parts + cap, total, 1, true);
+  c.wait_results(st);
   ts = c.h_result()[0];
   tt = c.h_result()[1];
 }

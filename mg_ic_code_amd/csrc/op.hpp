@@ -132,7 +132,7 @@ class VariableCoeffPoissonOperator {
   void build_args();
   double reduce(int kind, const LevelData &x, const LevelData *y);
   // partials (count `total`, per-box blocks) -> final -> allreduce -> host
-  double finish_reduce(int kind, double *parts, int total, int slot);
+  void finish_reduce(int kind, double *parts, int total, int slot, bool last = true);
   std::vector<BoxArgs> args_hom_, args_inhom_, args_plain_;
   // AMR level > 0 with isolated patches: args_hom_ with the coarse-fine
   // faces marked kBcCFHom, for the 3D-block fused sweep (cfFusedApplies)

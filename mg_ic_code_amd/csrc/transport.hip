@@ -289,7 +289,8 @@ __global__ __launch_bounds__(256) void k_exchange(const CopyItem *__restrict__ p
   ack_blocks(done_get, pget);
 }
 
-__global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned long long *err) {
+__global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned long long *err,
+                                const HostPub pub) {
   if (threadIdx.x != 0) return;
   const unsigned long long bits = __double_as_longlong(*val);
   const int slot = kSigRedVal + r.parity * 1024 + r.rank * kSigStride;
@@ -302,7 +303,10 @@ __global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned
   for (int q = 0; q < r.size && ok; ++q)
     ok = ipc_wait(mine + kSigRedCnt + q * kSigStride, r.count, err, r.timeout);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  if (!ok) return;
+  if (!ok) {  // the error word (set) goes to the host with the sequence number
+    publish(pub, __longlong_as_double(0x7ff8000000000000ll));
+    return;
+  }
   double acc = __longlong_as_double(ld_sys(mine + kSigRedVal + r.parity * 1024));
   for (int q = 1; q < r.size; ++q) {
     const double v =
@@ -310,6 +314,7 @@ __global__ void k_ipc_allreduce(double *val, int op, const IpcReduce r, unsigned
     acc = op == 1 ? (acc > v ? acc : v) : acc + v;
   }
   *val = acc;
+  publish(pub, acc);
 }
 
 inline void check_launch() {
@@ -349,8 +354,8 @@ void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
 }
 
 void ipc_allreduce(double *val, int op, const IpcReduce &r, unsigned long long *err,
-                   hipStream_t st) {
-  k_ipc_allreduce<<<1, 64, 0, st>>>(val, op, r, err);
+                   const HostPub &pub, hipStream_t st) {
+  k_ipc_allreduce<<<1, 64, 0, st>>>(val, op, r, err, pub);
   check_launch();
 }
 

@@ -26,6 +26,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "kernels.hpp"
 #include "mgic_core.hpp"
 
 namespace mgic {
@@ -101,8 +102,9 @@ void ipc_exchange_f(const CopyItem *put_items, const CopyItem *loc_items,
                     const IpcPeers &pget, int grid_cap, hipStream_t st);
 // in-place allreduce of one device double over all ranks (op 0 sum, 1 max),
 // reduced in rank order on every rank (identical results everywhere)
+// (pub: the result also published to the host, kernels.hpp)
 void ipc_allreduce(double *val, int op, const IpcReduce &r, unsigned long long *err,
-                   hipStream_t st);
+                   const HostPub &pub, hipStream_t st);
 
 }  // namespace kern
 }  // namespace mgic
