@@ -52,8 +52,8 @@ kern::HostPub Comm::host_pub(int slot, bool last) {
   return p;
 }
 
-void Comm::wait_results(hipStream_t st) {
-  const unsigned long long want = pub_count_;
+void Comm::wait_results(hipStream_t st, unsigned long long ticket) {
+  const unsigned long long want = ticket ? ticket : pub_count_;
   for (unsigned long long i = 0;; ++i) {
     if (__atomic_load_n(h_seq_, __ATOMIC_ACQUIRE) >= want) break;
     if ((i & 1023) == 1023) {

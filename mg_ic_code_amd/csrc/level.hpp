@@ -72,9 +72,11 @@ class Comm {
   // result `slot` into h_result(); `last` also publishes the transport's error
   // word and the sequence number wait_results() spins on
   kern::HostPub host_pub(int slot, bool last);
-  // until the last host_pub(…, true) result has landed (host spin on pinned
-  // memory, no stream synchronisation); raises a transport timeout
-  void wait_results(hipStream_t st);
+  // until the last host_pub(…, true) result (or the one of `ticket`, a
+  // last_ticket() value) has landed (host spin on pinned memory, no stream
+  // synchronisation); raises a transport timeout
+  void wait_results(hipStream_t st, unsigned long long ticket = 0);
+  unsigned long long last_ticket() const { return pub_count_; }
   // staging word for a host -> device copy (synchronised by its caller)
   double *h_stage() const { return h_result_ + kResultSlots; }
 

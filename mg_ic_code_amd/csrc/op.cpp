@@ -159,6 +159,21 @@ void VariableCoeffPoissonOperator::residualI(LevelData &lhs, LevelData &dpsi,
 double VariableCoeffPoissonOperator::residualNorm(LevelData &lhs, LevelData &dpsi,
                                                   const LevelData &rhs, bool homogeneous,
                                                   int normType) {
+  double now = 0.0;
+  const unsigned long long t = residualNormQueue(lhs, dpsi, rhs, homogeneous, normType, &now);
+  return t ? residualNormTake(t) : now;
+}
+
+double VariableCoeffPoissonOperator::residualNormTake(unsigned long long ticket) {
+  Comm &c = *grid->comm;
+  c.wait_results(stream(), ticket);
+  return c.h_result()[kNormSlot];
+}
+
+unsigned long long VariableCoeffPoissonOperator::residualNormQueue(LevelData &lhs, LevelData &dpsi,
+                                                                   const LevelData &rhs,
+                                                                   bool homogeneous, int normType,
+                                                                   double *now) {
   long total = 0;
   bool fused = normType == 0;
   for (int n = 0; fused && n < grid->nlocal(); ++n) {
@@ -168,7 +183,8 @@ double VariableCoeffPoissonOperator::residualNorm(LevelData &lhs, LevelData &dps
   }
   if (!fused) {
     residualI(lhs, dpsi, rhs, homogeneous);
-    return normType >= 0 ? norm(lhs, normType) : -1.0;
+    *now = normType >= 0 ? norm(lhs, normType) : -1.0;
+    return 0;
   }
   check_same_layout(*grid, lhs, "residual lhs");
   check_same_layout(*grid, dpsi, "residual dpsi");
@@ -185,9 +201,8 @@ double VariableCoeffPoissonOperator::residualNorm(LevelData &lhs, LevelData &dps
                         parts + off, st);
     off += kern::residual_norm_blocks(a);
   }
-  finish_reduce(3, parts, (int)total, 0);
-  c.wait_results(st);
-  return c.h_result()[0];
+  finish_reduce(3, parts, (int)total, kNormSlot);
+  return c.last_ticket();
 }
 
 void VariableCoeffPoissonOperator::preCond(LevelData &cor, const LevelData &res) {
@@ -440,7 +455,8 @@ static BoxArgs grow_exchanged(const BoxArgs &g, int d, long *off) {
 
 bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &rhs, int n,
                                               bool zero_in, LevelData *acc, int flags,
-                                              LevelData *rst) {
+                                              LevelData *rst,
+                                              const std::function<void()> *before_acc) {
   resetLambda();  // .cpp:283
   const hipStream_t st = stream();
   const StencilCoefs s = coefs();
@@ -521,6 +537,7 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
       vd = grow;
       if (last) out_ready = grow > 0;
     }
+    if (last && acc && before_acc) (*before_acc)();
     for (int b = 0; b < grid->nlocal(); ++b) {
       // the roofline instrumentation times the sweep kernels only (the
       // sweep+restriction launch moves other bytes)
@@ -559,13 +576,15 @@ bool VariableCoeffPoissonOperator::fusedRelax(LevelData &dpsi, const LevelData &
 }
 
 void VariableCoeffPoissonOperator::relaxAccumulate(LevelData &e, const LevelData &r, int n,
-                                                   LevelData &phi, int flags) {
+                                                   LevelData &phi, int flags,
+                                                   const std::function<void()> *before_acc) {
   if (n > 0 && prm.relax_mode == 1 && fusedSmootherApplies()) {
     check_same_layout(*grid, phi, "phi");
-    fusedRelax(e, r, n, false, &phi, flags);
+    fusedRelax(e, r, n, false, &phi, flags, nullptr, before_acc);
     return;
   }
   relax(e, r, n);
+  if (before_acc) (*before_acc)();
   incr(phi, e, 1.0);
 }
 
@@ -1000,7 +1019,7 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
 }
 
 void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
-                      bool halo_out) {
+                      bool halo_out, const std::function<void()> *before_phi) {
   VariableCoeffPoissonOperator &op = *levels_[d].op;
   const hipStream_t st = op.stream();
   // r's ghost layer once per level visit (the fused sweeps' red ring reads
@@ -1021,7 +1040,10 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
     } else {
       op.relaxFlags(e, r, prm.n_bottom, rf | out);
     }
-    if (phi_acc) op.incr(*phi_acc, e, 1.0);
+    if (phi_acc) {
+      if (before_phi) (*before_phi)();
+      op.incr(*phi_acc, e, 1.0);
+    }
     return;
   }
   // pre-smoothing leaves e's face ghosts exchanged for the restriction, or
@@ -1044,7 +1066,7 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
     op.prolongIncrementFilled(e, *N.e_stage);
   }
   if (phi_acc)  // phi += e folded into the last post-smoothing sweep
-    op.relaxAccumulate(e, r, prm.n_post, *phi_acc, rf);
+    op.relaxAccumulate(e, r, prm.n_post, *phi_acc, rf, before_phi);
   else
     op.relaxFlags(e, r, prm.n_post, rf | out);
 }
@@ -1098,10 +1120,26 @@ double AMRMultiGrid::iteration(LevelData &phi, const LevelData &rhs, LevelData &
 
 void AMRMultiGrid::iterations(LevelData &phi, const LevelData &rhs, LevelData &resid, int count,
                               int normType, bool homogeneous, double *norms) {
+  VariableCoeffPoissonOperator &op0 = mg.op(0);
+  // iteration i's norm is taken (host) once iteration i+1's V-cycle has been
+  // queued up to its first phi-writing launch -- the GPU runs that part while
+  // the host waits -- and before that launch is queued
+  int pending = -1;  // the iteration whose norm is not yet taken
+  unsigned long long ticket = 0;
+  double now = 0.0;
+  const std::function<void()> take = [&] {
+    if (pending < 0) return;
+    const double v = ticket ? op0.residualNormTake(ticket) : now;
+    if (norms) norms[pending] = v;
+    pending = -1;
+  };
   for (int i = 0; i < count; ++i) {
-    const double v = iteration(phi, rhs, resid, normType, homogeneous);
-    if (norms) norms[i] = v;
+    mg.oneCycleFromZeroInto(*corr_, resid, phi, &take);
+    take();  // (a V-cycle with no launch to hook)
+    ticket = op0.residualNormQueue(resid, phi, rhs, homogeneous, normType, &now);
+    pending = i;
   }
+  take();
 }
 
 double AMRMultiGrid::fmg(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,

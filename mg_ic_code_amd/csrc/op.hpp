@@ -56,6 +56,15 @@ class VariableCoeffPoissonOperator {
   // max norm (0) is taken inside the residual launch
   double residualNorm(LevelData &lhs, LevelData &dpsi, const LevelData &rhs, bool homogeneous,
                       int normType);
+  // the same, queued: returns a ticket for residualNormTake, or 0 with the
+  // value in *now when it was computed synchronously (normType 1 / 2, no
+  // fused residual) or not at all (normType < 0: -1).  The value travels in
+  // its own result slot (kNormSlot), so reductions queued after it (a
+  // BiCGStab bottom's) do not overwrite it before it is taken.
+  unsigned long long residualNormQueue(LevelData &lhs, LevelData &dpsi, const LevelData &rhs,
+                                       bool homogeneous, int normType, double *now);
+  double residualNormTake(unsigned long long ticket);
+  static constexpr int kNormSlot = 3;
   void residual(LevelData &lhs, LevelData &dpsi, const LevelData &rhs, bool homogeneous) {
     residualI(lhs, dpsi, rhs, homogeneous);
   }
@@ -153,15 +162,20 @@ class VariableCoeffPoissonOperator {
   // need not be zeroed).
   // rst != nullptr: the last sweep also writes restrictResidual(rst, result,
   // rhs) when the fused kernel can (returns whether it did)
+  // before_acc: called on the host right before the first launch that writes
+  // acc (nothing queued before it changes acc)
   bool fusedRelax(LevelData &dpsi, const LevelData &rhs, int n, bool zero_in = false,
-                  LevelData *acc = nullptr, int flags = 0, LevelData *rst = nullptr);
+                  LevelData *acc = nullptr, int flags = 0, LevelData *rst = nullptr,
+                  const std::function<void()> *before_acc = nullptr);
   bool deepApplies() const;
   // r's ghosts for the fused sweeps' rings (once per MultiGrid level visit):
   // face layer 1, or the 4-deep shell in deep-halo mode
   void rhsHalo(LevelData &r, hipStream_t st) const;
   // relax(e, r, n); phi += e -- the increment folded into the last fused
   // sweep (e is left as scratch in that case)
-  void relaxAccumulate(LevelData &e, const LevelData &r, int n, LevelData &phi, int flags = 0);
+  // (before_acc: as fusedRelax's, called before phi is first written)
+  void relaxAccumulate(LevelData &e, const LevelData &r, int n, LevelData &phi, int flags = 0,
+                       const std::function<void()> *before_acc = nullptr);
   // e = 0; relax(e, r, n) -- without zeroing e in memory when the fused
   // smoother applies (the first sweep does not read its input)
   void relaxFromZero(LevelData &e, const LevelData &r, int n, int flags = 0);
@@ -251,9 +265,11 @@ class MultiGrid {
   void oneCycleFromZero(LevelData &e, const LevelData &r) {
     cycle(0, e, const_cast<LevelData &>(r), true, nullptr);
   }
-  // e = 0; oneCycle(e, r); phi += e (e is scratch afterwards)
-  void oneCycleFromZeroInto(LevelData &e, const LevelData &r, LevelData &phi) {
-    cycle(0, e, const_cast<LevelData &>(r), true, &phi);
+  // e = 0; oneCycle(e, r); phi += e (e is scratch afterwards); before_phi:
+  // called on the host before the first launch that writes phi
+  void oneCycleFromZeroInto(LevelData &e, const LevelData &r, LevelData &phi,
+                            const std::function<void()> *before_phi = nullptr) {
+    cycle(0, e, const_cast<LevelData &>(r), true, &phi, false, before_phi);
   }
   // full multigrid from the residual r at depth 0: r_{d+1} = R(r_d) at every
   // depth, the bottom solve from zero, then per finer depth e_d = P e_{d+1}
@@ -278,7 +294,7 @@ class MultiGrid {
   // e_zero: treat e as zero on entry (it is zeroed or never read);
   // phi_acc: phi += e at the end (at depth 0 folded into the last sweep)
   void cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
-             bool halo_out = false);
+             bool halo_out = false, const std::function<void()> *before_phi = nullptr);
   std::vector<Level> levels_;
 };
 
@@ -307,10 +323,11 @@ class AMRMultiGrid {
                    bool homogeneous);
   // `count` iterations from the state iteration() / initResidual() leave
   // (resid = rhs - L(phi)); norms[i] = what the i-th iteration() call would
-  // return, bit for bit.  Iteration i+1's V-cycle computes iteration i's
-  // residual in its first launch when the fused residual applies, so the
-  // count includes the same residual evaluations as `count` iteration()
-  // calls (the last one separately).
+  // return, bit for bit (the same launches in the same order).  The host
+  // reads iteration i's norm while the GPU runs iteration i+1's V-cycle up
+  // to its first phi-writing launch, which is queued only after the read --
+  // the place a stop test on that norm would decide -- so the GPU does not
+  // idle between iterations.
   void iterations(LevelData &phi, const LevelData &rhs, LevelData &resid, int count,
                   int normType, bool homogeneous, double *norms);
   double initResidual(LevelData &phi, const LevelData &rhs, LevelData &resid, int normType,

@@ -265,6 +265,34 @@ def test_vcycle_iterations_bitwise(comm, rng, parts, prolong, avg, fused):
     assert np.array_equal(download_global(S["fphi"], S["grid"], (n,) * 3), o.get(0, oracle.PHI, 0))
 
 
+@pytest.mark.parametrize("parts,deep,bottom", [((1, 1, 1), 0, 0), ((1, 1, 1), 0, 1),
+                                                ((2, 2, 2), 1, 0), ((2, 2, 2), 1, 1)])
+@pytest.mark.parametrize("norm_type", [0, 1, -1])
+def test_pipelined_iterations_match_iteration_calls(comm, rng, parts, deep, bottom, norm_type):
+    # iterations() takes iteration i's norm on the host while iteration i+1's
+    # V-cycle runs up to its phi += e launch (queued only after the read):
+    # the same phi, residual and norms as iteration() calls -- with the
+    # BiCGStab bottom, whose reductions are published in between, in the
+    # deep-halo multi-box layout, and for norms taken outside the residual
+    # launch (1) or not at all (-1)
+    n = 32
+    S = build_pair(comm, rng, n, parts, nlevels=3, bottom=bottom, fused=1, deep=deep)
+    amg, grid = S["amg"], S["grid"]
+    amg.init_residual(S["fphi"], S["frhs"], S["fres"], norm_type=0)
+    want = [amg.iteration(S["fphi"], S["frhs"], S["fres"], norm_type=norm_type)
+            for _ in range(3)]
+    fphi2, fres2 = mg.LevelData(grid), mg.LevelData(grid)
+    fphi2.set_zero()
+    amg.init_residual(fphi2, S["frhs"], fres2, norm_type=0)
+    got = amg.iterations(fphi2, S["frhs"], fres2, 3, norm_type=norm_type)
+    assert got == want
+    if norm_type < 0:
+        assert got == [-1.0] * 3
+    shp = (n,) * 3
+    assert np.array_equal(download_global(fphi2, grid, shp), download_global(S["fphi"], grid, shp))
+    assert np.array_equal(download_global(fres2, grid, shp), download_global(S["fres"], grid, shp))
+
+
 @pytest.mark.parametrize("fused", [2, 3])
 @pytest.mark.parametrize("bvar", [False, True])
 def test_vcycle_ragged_mixed_bc_bitwise(rng, comm, fused, bvar):
