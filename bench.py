@@ -148,7 +148,9 @@ def main():
     comm.synchronize()
     # the headline: K AMRMultiGrid iterations -- the V-cycle, r = rhs - L(phi)
     # and (norm_type >= 0) its norm for the stop test, read on the host each
-    # iteration -- with no instrumentation in the timed region
+    # iteration before the next iteration's first phi-writing launch is
+    # queued (the GPU runs the next V-cycle's earlier part meanwhile) -- with
+    # no instrumentation in the timed region
     elapsed, hist = timed(lambda: amg.iterations(fphi, frhs, fres, args.steps, norm_type=nt))
 
     # the roofline: K more iterations with a HIP event pair around every
