@@ -37,6 +37,9 @@ def main():
                     help="split the box into this many boxes (all on this rank): the N-GPU "
                          "split's exchanges and gathers on one GPU")
     ap.add_argument("--agglomerate-below", type=int, default=0)
+    ap.add_argument("--norm-type", type=int, default=-1,
+                    help="per-iteration residual norm (bench.py takes 0, the stop test's max "
+                         "norm; -1: none, the proxy's default since round 1)")
     args = ap.parse_args()
     import mg_ic_code_amd as mg
     from mg_ic_code_amd.params import read_params_file
@@ -70,17 +73,16 @@ def main():
                                                n_bottom=4, bottom_solver=0,
                                                agglomerate_below=args.agglomerate_below))
     amg.init_residual(fphi, frhs, fres, norm_type=0)
-    for _ in range(args.warmup):
-        amg.iteration(fphi, frhs, fres, norm_type=-1)
+    amg.iterations(fphi, frhs, fres, args.warmup, norm_type=args.norm_type)
     comm.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        amg.iteration(fphi, frhs, fres, norm_type=-1)
+    amg.iterations(fphi, frhs, fres, args.steps, norm_type=args.norm_type)
     comm.synchronize()
     dt = time.perf_counter() - t0
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
     print(json.dumps({"size": n, "shape": shp, "parts": parts,
                       "agglomerate_below": args.agglomerate_below, "deep": args.deep, "periodic": per,
+                      "norm_type": args.norm_type,
                       "transport": "local" if args.local else args.transport,
                       "vcycles_per_s": round(args.steps / dt, 2),
                       "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
