@@ -260,10 +260,11 @@ MGIC_API int mgic_mg_iteration(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_
 /* `count` iterations (AMRMultiGrid::solve's loop body) from the state
  * mgic_mg_iteration / mgic_mg_init_residual leave; norms[i] (count values,
  * may be NULL) = what the i-th mgic_mg_iteration call would return, bit for
- * bit.  Iteration i+1's first pre-smoothing launch computes iteration i's
- * residual (and its max norm) when the level allows it (one box per rank, no
- * exchanged faces, two sweeps per launch): the same residual evaluations,
- * one streaming pass fewer per iteration. */
+ * bit (the same launches in the same order).  Iteration i's norm is read on
+ * the host after iteration i+1's V-cycle has been queued up to its first
+ * launch that writes phi and before that launch is queued -- where a stop
+ * test on the norm would decide -- so the device does not idle while the
+ * host reads it. */
 MGIC_API int mgic_mg_iterations(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                                 int count, int norm_type, int homogeneous, double *norms);
 MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
