@@ -594,8 +594,8 @@ class AMRMultiGrid:
     def iterations(self, phi: LevelData, rhs: LevelData, resid: LevelData, count: int,
                    norm_type: int = 0, homogeneous: bool = False) -> List[float]:
         """`count` iteration() calls (same phi, resid and norms, bit for bit);
-        iteration i+1's first launch computes iteration i's residual where the
-        level allows (mgic_mg_iterations)."""
+        iteration i's norm is read while iteration i+1's V-cycle runs up to
+        its first phi-writing launch (mgic_mg_iterations)."""
         out = (ctypes.c_double * max(1, count))()
         call("mgic_mg_iterations", self._h, phi.handle, rhs.handle, resid.handle, int(count),
              int(norm_type), int(bool(homogeneous)), out)
