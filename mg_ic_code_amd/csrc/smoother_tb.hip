@@ -45,6 +45,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "kernels.hpp"
@@ -186,8 +187,10 @@ template <> struct TB2Vec<float> { using type = float2; };
 
 // One tile (x0, y0) of the box, planes [z0, z1).  FAST: alpha == 1, beta ==
 // -1, bval == 1 (exact specialisation, see above), and lambda by rcp_div1;
-// EDGE: the tile's rings reach an x / y domain face (BC code compiled in).
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE>
+// EDGE: the tile's rings reach an x / y domain face (BC code compiled in);
+// UBC: every x / y domain face of the box has the same ghost rule (one
+// ghost per update instead of one per face).
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE, bool UBC>
 __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                                          T *__restrict__ uo, double *__restrict__ acc,
                                          const T *__restrict__ ui,
@@ -499,11 +502,21 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const int f = (rinf[t][i] >> (red ? 0 : 4)) & 15;
-        // ef: the domain faces this tile's rings reach (uniform)
-        if (ef & 1) xm[i] = (f & 1) ? ghost(gg, 0, uc[i]) : xm[i];
-        if (ef & 2) xp[i] = (f & 2) ? ghost(gg, 1, uc[i]) : xp[i];
-        if (ef & 4) ym[i] = (f & 4) ? ghost(gg, 2, uc[i]) : ym[i];
-        if (ef & 8) yp[i] = (f & 8) ? ghost(gg, 3, uc[i]) : yp[i];
+        if constexpr (UBC) {
+          // one rule for every x / y domain face (gg slot 0): one ghost of
+          // the cell's own value, selected into whichever neighbours it images
+          const T gv = ghost(gg, 0, uc[i]);
+          xm[i] = (f & 1) ? gv : xm[i];
+          xp[i] = (f & 2) ? gv : xp[i];
+          ym[i] = (f & 4) ? gv : ym[i];
+          yp[i] = (f & 8) ? gv : yp[i];
+        } else {
+          // ef: the domain faces this tile's rings reach (uniform)
+          if (ef & 1) xm[i] = (f & 1) ? ghost(gg, 0, uc[i]) : xm[i];
+          if (ef & 2) xp[i] = (f & 2) ? ghost(gg, 1, uc[i]) : xp[i];
+          if (ef & 4) ym[i] = (f & 4) ? ghost(gg, 2, uc[i]) : ym[i];
+          if (ef & 8) yp[i] = (f & 8) ? ghost(gg, 3, uc[i]) : yp[i];
+        }
       }
     }
     T v[NP];
@@ -651,7 +664,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 }
 
 
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST>
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool UBC>
 __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  double *__restrict__ acc,
                                                  const T *__restrict__ ui,
@@ -671,11 +684,11 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
   if (ef)
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,
-                                                  z1, ef);
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, UBC>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
+                                                       z0, z1, ef);
   else
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
-                                                   z0, z1, 0);
+    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, UBC>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0,
+                                                        y0, z0, z1, 0);
 }
 
 template <class T, int TX, int TY, int NT>
@@ -685,7 +698,7 @@ int tb2_resident_slots() {
     MGIC_HIP(hipGetDevice(&dev));
     MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     MGIC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per, k_gsrb_tb2<T, TX, TY, NT, false, false, true>, NT, 0));
+        &per, k_gsrb_tb2<T, TX, TY, NT, false, false, true, true>, NT, 0));
     return (per > 0 ? per : 1) * (ncu > 0 ? ncu : 1);
   }();
   return slots;
@@ -740,14 +753,34 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   // short reciprocal's range for T
   const bool fast = s.alpha == 1.0 && s.beta == -1.0 && s.bval == 1.0 &&
                     (std::is_same<T, double>::value ? s.rcp_fast : s.rcp_fast32);
-  const TB2Ghosts<T> gg = make_ghosts<T>(g);
+  TB2Ghosts<T> gg = make_ghosts<T>(g);
   if (zero_in)  // the ZIN passes assume every ghost of a zero input is +-0
     for (int f = 0; f < 6; ++f)
       if (g.bcm[f] != kBcMemory && gg.c[f] != (T)0)
         throw Error(kBadArg, "two-sweep launch: zero input under an inhomogeneous BC");
-#define MGIC_TB2(Z, A, FA)                                                                        \
-  k_gsrb_tb2<T, TX, TY, NT, Z, A, FA><<<grid, block, 0, st>>>(u_out, acc, u_in, rhs, a, g, s, gg, \
-                                                              kc, ntx, nty, nblocks)
+  // UBC: the x / y domain faces share one ghost rule (the reference's
+  // configuration: Dirichlet-0 everywhere); slot 0 then holds it
+  bool ubc = true;
+  int rep = -1;
+  for (int f = 0; f < 4; ++f) {
+    if (g.bcm[f] == kBcMemory) continue;
+    if (rep < 0) rep = f;
+    else ubc = ubc && gg.sgn[f] == gg.sgn[rep] &&
+               std::memcmp(&gg.c[f], &gg.c[rep], sizeof(T)) == 0;  // (signed zeros differ)
+  }
+  if (ubc && rep > 0) {
+    gg.sgn[0] = gg.sgn[rep];
+    gg.c[0] = gg.c[rep];
+  }
+#define MGIC_TB2(Z, A, FA)                                                                         \
+  do {                                                                                             \
+    if (ubc)                                                                                       \
+      k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, true><<<grid, block, 0, st>>>(                           \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks);                              \
+    else                                                                                           \
+      k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, false><<<grid, block, 0, st>>>(                          \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks);                              \
+  } while (0)
   if (acc) {
     if constexpr (std::is_same<T, double>::value) {
       if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
