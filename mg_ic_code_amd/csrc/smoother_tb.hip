@@ -187,10 +187,11 @@ template <> struct TB2Vec<float> { using type = float2; };
 
 // One tile (x0, y0) of the box, planes [z0, z1).  FAST: alpha == 1, beta ==
 // -1, bval == 1 (exact specialisation, see above), and lambda by rcp_div1;
-// EDGE: the tile's rings reach an x / y domain face (BC code compiled in);
-// UBC: every x / y domain face of the box has the same ghost rule (one
-// ghost per update instead of one per face).
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool EDGE, bool UBC>
+// EM: the x (3) / y (12) domain faces the tile's rings reach (BC code
+// compiled in for those; 0: an interior tile); UBC: every x / y domain face
+// of the box has the same ghost rule (one ghost per update instead of one
+// per face; without it EM is 15 and the faces come from ef).
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, int EM, bool UBC>
 __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                                          T *__restrict__ uo, double *__restrict__ acc,
                                          const T *__restrict__ ui,
@@ -498,18 +499,23 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       zm[i] = Nm[c + o];
       zp[i] = Np[c + o];
     }
-    if (EDGE) {
+    if constexpr (EM != 0) {
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const int f = (rinf[t][i] >> (red ? 0 : 4)) & 15;
         if constexpr (UBC) {
           // one rule for every x / y domain face (gg slot 0): one ghost of
-          // the cell's own value, selected into whichever neighbours it images
+          // the cell's own value, selected into whichever neighbours it
+          // images, for the directions whose faces the tile reaches
           const T gv = ghost(gg, 0, uc[i]);
-          xm[i] = (f & 1) ? gv : xm[i];
-          xp[i] = (f & 2) ? gv : xp[i];
-          ym[i] = (f & 4) ? gv : ym[i];
-          yp[i] = (f & 8) ? gv : yp[i];
+          if constexpr ((EM & 3) != 0) {
+            xm[i] = (f & 1) ? gv : xm[i];
+            xp[i] = (f & 2) ? gv : xp[i];
+          }
+          if constexpr ((EM & 12) != 0) {
+            ym[i] = (f & 4) ? gv : ym[i];
+            yp[i] = (f & 8) ? gv : yp[i];
+          }
         } else {
           // ef: the domain faces this tile's rings reach (uniform)
           if (ef & 1) xm[i] = (f & 1) ? ghost(gg, 0, uc[i]) : xm[i];
@@ -683,12 +689,15 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   // uniform: the x / y domain faces the tile's rings (3 cells) reach
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
-  if (ef)
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, true, UBC>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0,
-                                                       z0, z1, ef);
-  else
-    tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, false, UBC>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0,
-                                                        y0, z0, z1, 0);
+#define MGIC_TILE(EM)                                                                             \
+  tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, EM, UBC>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0, \
+                                                   z1, ef)
+  // (uniform) an x-face or a y-face tile runs only that direction's ghost code
+  if (!ef) MGIC_TILE(0);
+  else if (UBC && !(ef & 12)) MGIC_TILE(UBC ? 3 : 15);
+  else if (UBC && !(ef & 3)) MGIC_TILE(UBC ? 12 : 15);
+  else MGIC_TILE(15);
+#undef MGIC_TILE
 }
 
 template <class T, int TX, int TY, int NT>
