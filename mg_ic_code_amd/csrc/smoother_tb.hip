@@ -99,7 +99,8 @@ struct TB2 {
   static constexpr int NRP = UW * (TY + 6);        // update pairs: rows y0-3 .. y0+TY+2
   static constexpr int NL = (CP + NT - 1) / NT;
   static constexpr int NP = (NRP + NT - 1) / NT;
-  static constexpr int LDS_BYTES = 2 * NS * SS * 8;
+  static constexpr int RING = 2 * NS * SS + 2 * PW + 2;  // + what a PAD lane's reads overrun
+  static constexpr int LDS_BYTES = RING * 8;
 };
 
 // a ParseBC ghost as one add: ghost_of(mode, c, v) == (sign ^ v) + gc
@@ -192,8 +193,7 @@ template <> struct TB2Vec<float> { using type = float2; };
 // of the box has the same ghost rule (one ghost per update instead of one
 // per face; without it EM is 15 and the faces come from ef).
 template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, int EM, bool UBC>
-__device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
-                                         T *__restrict__ uo, double *__restrict__ acc,
+__device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo, double *__restrict__ acc,
                                          const T *__restrict__ ui,
                                          const T *__restrict__ rhs,
                                          const T *__restrict__ a, const BoxArgs &g,
@@ -207,6 +207,16 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
                 NP = F::NP;
   const int nx = g.nx, ny = g.ny, nz = g.nz;
   const int tid = threadIdx.x;
+  // The LDS ring, slot-interleaved: slot sl's red elements at RB + 2 sl SS,
+  // its black ones SS further, so the other colour of a slot is a constant
+  // byte offset away.  A lane's LDS accesses are a uniform slot base + one
+  // of two loop-invariant lane offsets (cbm, coy) + a constant, which the
+  // compiler folds into the ds instruction's offset field: one address add
+  // per base instead of an index computation per access.
+  constexpr unsigned ES = sizeof(T), SB = (unsigned)SS * ES;
+  char *const RBc = reinterpret_cast<char *>(RB);
+  auto slot_base = [&](int sl) { return RBc + (unsigned)sl * (2u * SB); };
+  auto ldsp = [](char *base, unsigned off) { return base + off; };
   const long sy = g.sy, sz = g.sz;
   // the tile clipped to the box: ring levels are distances from it
   const int tx1 = min(x0 + TX, nx) - 1, ty1 = min(y0 + TY, ny) - 1;
@@ -290,7 +300,11 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   }
   wthr = __builtin_amdgcn_readfirstlane(wthr);
   unsigned roff[2][NP];
-  int yzo[2][NP], rinf[2][NP], ci[NP];
+  // cbm: byte offset of the element before the pair's (pair index c - 1);
+  // coy[t]: of its y / z neighbour column minus one row (c + s - 1 - PW, s
+  // the row's shift at parity t)
+  unsigned cbm[NP], coy[2][NP];
+  int rinf[2][NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     const int c = tid + i * NT, jt = c - MAIN;
@@ -301,7 +315,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     const int m = c < MAIN ? 1 + (c & 31) : 33 + jt - (jt / (UW - 32)) * (UW - 32);
     const int gy = y0 - 3 + rr;
     const bool row_ok = c < NRP;
-    ci[i] = row_ok ? (rr + 1) * PW + m : F::PAD;
+    const int cix = row_ok ? (rr + 1) * PW + m : F::PAD;
+    cbm[i] = (unsigned)(cix - 1) * ES;
+    asm volatile("" : "+v"(cbm[i]));
     const int dy = gy < y0 ? y0 - gy : (gy > ty1 ? gy - ty1 : 0);
     const bool yok = row_ok && gy >= uylo && gy <= uyhi;
 #pragma unroll
@@ -309,7 +325,11 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
       const int sh = (gsum + gy + t) & 1;
       const int X = x0 - 6 + 2 * m + sh;
       roff[t][i] = row_ok ? boff(clampi(X, -6, nx + 3), clampi(gy, -4, ny + 3)) : 0u;
-      yzo[t][i] = sh - 1;
+      coy[t][i] = (unsigned)(cix + sh - 1 - PW) * ES;
+      // (opaque from here on: the compiler adds each use's constant in the
+      // ds instruction's offset field instead of keeping lane offset +
+      // constant combinations in registers)
+      asm volatile("" : "+v"(coy[t][i]));
       int bits = 0;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -401,7 +421,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
   };
   auto put = [&](int sl, auto bc) {  // into ring slot sl: red element -> R, black -> B
     constexpr int b = decltype(bc)::value;
-    T *Rs = R + sl * SS, *Bs = B + sl * SS;
+    T *Rs = reinterpret_cast<T *>(slot_base(sl)), *Bs = Rs + SS;
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
       if (NL * NT > CP && tid + i * NT >= CP) continue;  // whole waves past the plane
@@ -467,37 +487,43 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     // rows beyond ring W (distance > W from the tile) are never read once
     // this pass is done, so waves holding only such rows skip it
     if (NP == 1 && W < wthr) return;  // (one pair per lane only)
-    T *X = (red ? R : B) + sk * SS;  // sk = es(k)
-    T *N = (red ? B : R) + sk * SS;
-    T *Nm = (red ? B : R) + eadd(sk, -1) * SS;
-    T *Np = (red ? B : R) + eadd(sk, 1) * SS;
+    // slot bases (sk = es(k)) and the colours' offsets within a slot: X the
+    // colour updated, N the other one; y / z neighbours of pair c are pair
+    // c + o -+ PW (this plane) and c + o (planes k -+ 1), o = s - 1 (red) or
+    // s (black)
+    char *const Bk = slot_base(sk), *const Bm = slot_base(eadd(sk, -1)),
+               *const Bp = slot_base(eadd(sk, 1));
+    const unsigned XO = red ? 0u : SB, NO = red ? SB : 0u, RO = red ? 0u : ES;
+    auto at = [](char *p, unsigned o) -> T & { return *reinterpret_cast<T *>(p + o); };
+    char *a0[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) a0[i] = ldsp(Bk, cbm[i]);  // pair c - 1 of slot sk
     if constexpr (ZC == 1) {
       T v[NP];
 #pragma unroll
       for (int i = 0; i < NP; ++i) v[i] = (T)0 - cl[i] * ((T)0 - cr[i]);
 #pragma unroll
-      for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> 10) & 1 ? v[i] : (T)0;
+      for (int i = 0; i < NP; ++i) at(a0[i], XO + ES) = (rinf[t][i] >> 10) & 1 ? v[i] : (T)0;
       const bool zl = !SD && k == zfl, zh = !SD && k == zfh;
       if (zl || zh) {
-        T *Nz = zl ? Nm : Np;
+        char *const Bz = zl ? Bm : Bp;
         const int zf = zl ? 4 : 5;
 #pragma unroll
-        for (int i = 0; i < NP; ++i) Nz[ci[i] + yzo[t][i]] = ghost(gg, zf, v[i]);
+        for (int i = 0; i < NP; ++i) at(ldsp(Bz, coy[t][i]), NO + PW * ES) = ghost(gg, zf, v[i]);
       }
       return;
     }
     T uc[NP], xm[NP], xp[NP], ym[NP], yp[NP], zm[NP], zp[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      const int c = ci[i];
-      const int o = yzo[t][i] + (red ? 0 : 1);  // y / z neighbours: pair m-1+s (red), m+s (black)
-      uc[i] = ZC == 2 ? (T)0 : X[c];
-      xm[i] = N[c - (red ? 1 : 0)];
-      xp[i] = N[c + (red ? 0 : 1)];
-      ym[i] = N[c + o - PW];
-      yp[i] = N[c + o + PW];
-      zm[i] = Nm[c + o];
-      zp[i] = Np[c + o];
+      char *const a1 = ldsp(Bk, coy[t][i]);
+      uc[i] = ZC == 2 ? (T)0 : at(a0[i], XO + ES);
+      xm[i] = at(a0[i], NO + RO);       // N[c - 1] (red), N[c] (black)
+      xp[i] = at(a0[i], NO + RO + ES);  // N[c], N[c + 1]
+      ym[i] = at(a1, NO + RO);
+      yp[i] = at(a1, NO + RO + 2 * PW * ES);
+      zm[i] = at(ldsp(Bm, coy[t][i]), NO + RO + PW * ES);
+      zp[i] = at(ldsp(Bp, coy[t][i]), NO + RO + PW * ES);
     }
     if constexpr (EM != 0) {
 #pragma unroll
@@ -529,14 +555,15 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
 #pragma unroll
     for (int i = 0; i < NP; ++i) v[i] = upd(uc[i], xm[i], xp[i], ym[i], yp[i], zm[i], zp[i], cr[i], ca[i], cl[i]);
 #pragma unroll
-    for (int i = 0; i < NP; ++i) X[ci[i]] = (rinf[t][i] >> (red ? 10 : 11)) & 1 ? v[i] : uc[i];
+    for (int i = 0; i < NP; ++i)
+      at(a0[i], XO + ES) = (rinf[t][i] >> (red ? 10 : 11)) & 1 ? v[i] : uc[i];
     const bool zl = !SD && k == zfl, zh = !SD && k == zfh;
     if (zl || zh) {  // z ghosts of the face plane (every lane: an element
                      // never updated owns its ghost alone)
-      T *Nz = zl ? Nm : Np;
+      char *const Bz = zl ? Bm : Bp;
       const int zf = zl ? 4 : 5;
 #pragma unroll
-      for (int i = 0; i < NP; ++i) Nz[ci[i] + yzo[t][i] + (red ? 0 : 1)] = ghost(gg, zf, v[i]);
+      for (int i = 0; i < NP; ++i) at(ldsp(Bz, coy[t][i]), NO + RO + PW * ES) = ghost(gg, zf, v[i]);
     }
   };
   // plane k's tile cells -> u_out (or acc += them), from ring slot sl
@@ -557,8 +584,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ R, T *__restrict__ B,
     for (int i = 0; i < NP; ++i) {
       const int st = kin ? (rinf[t][i] >> 8) & 3 : 0;
       V w;
-      w.x = R[sl * SS + ci[i]];
-      w.y = B[sl * SS + ci[i]];
+      char *const a = ldsp(slot_base(sl), cbm[i]);
+      w.x = *reinterpret_cast<const T *>(a + ES);
+      w.y = *reinterpret_cast<const T *>(a + SB + ES);
       if constexpr (ACC) {  // phi += e (incr, scale 1) in the same pass
         w.x = ac0[i] + w.x;
         w.y = ac1[i] + w.y;
@@ -680,8 +708,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  const TB2Ghosts<T> gg, int kc, int ntx, int nty,
                                                  int nblocks) {
   using F = TB2<TX, TY, NT>;
-  __shared__ T R[F::NS * F::SS];  // red element of every pair, one per ring slot
-  __shared__ T B[F::NS * F::SS];  // black element
+  __shared__ T RB[F::RING];  // per ring slot: the red element of every pair, then the black
   const int L = sweep::xcd_tile(blockIdx.x, nblocks);
   const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
   const int z0 = (L / (ntx * nty)) * kc;
@@ -690,7 +717,7 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
 #define MGIC_TILE(EM)                                                                             \
-  tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, EM, UBC>(R, B, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0, \
+  tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, EM, UBC>(RB, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,   \
                                                    z1, ef)
   // (uniform) an x-face or a y-face tile runs only that direction's ghost code
   if (!ef) MGIC_TILE(0);
