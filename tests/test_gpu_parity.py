@@ -493,6 +493,51 @@ def test_fused_sweep_matches_oracle_and_passes(comm, rng, shape, lo, nsweeps):
     assert np.array_equal(outs[0], o.get(0, oracle.PHI, 0))
 
 
+@pytest.mark.parametrize("shape,lo", [((37, 9, 40), (3, -5, 7)), ((130, 47, 45), (-64, 1, 1))])
+@pytest.mark.parametrize("nsweeps", [2, 3])
+@pytest.mark.parametrize("coefs", [(1.0, -1.0, 1.0), (0.75, -1.3, 1.7)])
+@pytest.mark.parametrize("bc", [(0, 0.5), (1, 0.0), (0, 0.0)])
+def test_two_sweep_one_rule_edges_match_oracle(comm, rng, shape, lo, nsweeps, coefs, bc):
+    # every x / y domain face with the same ghost rule (the two-sweep
+    # kernel's one-rule edge bodies, split into x-face, y-face and corner
+    # tiles): inhomogeneous Dirichlet, homogeneous Neumann (ghost + -0) and
+    # the reference's Dirichlet-0, against the oracle and the per-colour
+    # passes bit for bit (z faces take the same rule)
+    mode, bcv = bc
+    alpha, beta, bval = coefs
+    nx, ny, nz = shape
+    dom = (lo[0], lo[1], lo[2], lo[0] + nx - 1, lo[1] + ny - 1, lo[2] + nz - 1)
+    dx = 0.7
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    b = np.full((nz, ny, nx), bval)
+    rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    u0 = rng.uniform(-1, 1, (nz, ny, nx))
+    bc_lo = bc_hi = (mode,) * 3
+    outs = []
+    for fused in (2, 0):
+        grid = mg.Grid(comm, dom, [dom], dx)
+        fa, fb, fr, fu = (mg.LevelData(grid) for _ in range(4))
+        fa.upload(0, a)
+        fb.upload(0, b)
+        fr.upload(0, rhs)
+        fu.upload(0, u0)
+        prm = mg.OperatorParams(alpha=alpha, beta=beta, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bcv,
+                                fused_smoother=fused)
+        op = mg.defineOperatorFactory(grid, fa, fb, prm).AMRnewOp()
+        op.relax(fu, fr, nsweeps)
+        outs.append(fu.download(0))
+    assert np.array_equal(outs[0], outs[1])
+    o = oracle.OracleMG([dom], dom, dx, alpha=alpha, beta=beta, bc_lo=bc_lo, bc_hi=bc_hi,
+                        bc_value=bcv, nlevels=1)
+    o.set(0, oracle.ACOEF, 0, a)
+    o.set(0, oracle.BCOEF, 0, b)
+    o.set(0, oracle.RHS, 0, rhs)
+    o.set(0, oracle.PHI, 0, u0)
+    o.setup()
+    o.relax(0, oracle.PHI, oracle.RHS, nsweeps)
+    assert np.array_equal(outs[0], o.get(0, oracle.PHI, 0))
+
+
 @pytest.mark.parametrize("shape,lo", [((70, 20, 13), (0, 0, 0)), ((37, 9, 40), (3, -5, 7)),
                                       ((130, 47, 45), (-64, 1, 1)), ((64, 44, 24), (0, 0, 0))])
 @pytest.mark.parametrize("nsweeps", [2, 3, 4, 5])
