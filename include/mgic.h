@@ -76,12 +76,21 @@ typedef struct {
   int n_pre, n_post, n_bottom;
   int bottom_solver;     /* 0: relax(n_bottom), 1: BiCGStab */
   int cycles;            /* 1 = V-cycle */
-  int agglomerate_below; /* gather to rank 0 once a box side < this; 0 off */
+  int agglomerate_below; /* gather to rank 0 once a box side < this; 0 off.  A
+                            gathered depth (and every depth below it) runs on
+                            rank 0 alone, its BiCGStab reductions included; the
+                            other ranks go from the gather to the scatter */
   int bicg_imax;
   double bicg_eps, bicg_reps, bicg_small;
   int bicg_restarts, bicg_norm_type;
 } mgic_mg_params;
 
+/* The layout of the parameter structs above and the entry points' argument
+ * lists: bumped whenever either changes (round 4 removed fields from the
+ * middle of mgic_op_params / mgic_mg_params).  An integrator compiled against
+ * this header checks mgic_abi_version() == MGIC_ABI_VERSION once at start-up. */
+#define MGIC_ABI_VERSION 2
+MGIC_API int mgic_abi_version(void);
 MGIC_API const char *mgic_version(void);
 MGIC_API const char *mgic_last_error(void);
 MGIC_API int mgic_set_device(int device);
@@ -156,6 +165,11 @@ MGIC_API int mgic_plan_check_transport(mgic_plan p, int transport);
  * in the message, element count.  Both sides of a message must list the same
  * (flag, first, count) rows: a get block waits for the put block of its flag */
 MGIC_API int mgic_plan_ipc_blocks(mgic_plan p, int *n, long long *rows);
+/* the same table for a block size other than the default: block_elems as
+ * MGIC_IPC_BLOCK_ELEMS sets it (a multiple of 512 in [512, 2^20]); a plan's
+ * table is built once, so one block size per plan handle */
+MGIC_API int mgic_plan_ipc_blocks_per(mgic_plan p, long long block_elems, int *n,
+                                      long long *rows);
 MGIC_API int mgic_plan_destroy(mgic_plan p);
 MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpack, int *n_peers);
 MGIC_API int mgic_plan_items(mgic_plan p, int which, long long *items);
@@ -280,8 +294,10 @@ MGIC_API int mgic_mg_fmg(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field 
  * correction equation in fp32 (GSRB / restrictResidual / prolongIncrement in
  * float, coefficients rounded from the fp64 hierarchy), the fine residual
  * rhs - L(phi) in fp64 rounded once, phi += e in fp64.  Bottom: relax
- * (n_bottom); no agglomeration.  resid (fp64) may be NULL unless a norm is
- * requested (norm_type >= 0).  Inhomogeneous BC for the fine residual. */
+ * (n_bottom).  agglomerate_below and deep_halo as for the fp64 cycle (fp32
+ * gathers / scatters and 4-deep fp32 shells).  resid (fp64) may be NULL
+ * unless a norm is requested (norm_type >= 0).  Inhomogeneous BC for the fine
+ * residual. */
 MGIC_API int mgic_mixed_create(mgic_factory f, const mgic_mg_params *p, mgic_mixed *out);
 MGIC_API int mgic_mixed_destroy(mgic_mixed m);
 MGIC_API int mgic_mixed_num_depths(mgic_mixed m, int *n);

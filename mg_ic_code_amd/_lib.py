@@ -81,6 +81,7 @@ PLL = POINTER(ctypes.c_longlong)
 # name -> argtypes (all return int status unless listed in _RESTYPE)
 SIGNATURES = {
     "mgic_version": [],
+    "mgic_abi_version": [],
     "mgic_last_error": [],
     "mgic_set_device": [c_int],
     "mgic_get_device_count": [PI],
@@ -110,6 +111,7 @@ SIGNATURES = {
     "mgic_plan_create_shell": [c_int, c_int, PI, PI, c_int, PI, PI, c_int, PH],
     "mgic_plan_check_transport": [H, c_int],
     "mgic_plan_ipc_blocks": [H, PI, PLL],
+    "mgic_plan_ipc_blocks_per": [H, ctypes.c_longlong, PI, PLL],
     "mgic_plan_destroy": [H],
     "mgic_plan_sizes": [H, PI, PI, PI, PI],
     "mgic_plan_items": [H, c_int, PLL],

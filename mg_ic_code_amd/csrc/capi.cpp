@@ -169,7 +169,11 @@ mgic_field borrowed_field(LevelData *ld) {
 
 extern "C" {
 
-MGIC_API const char *mgic_version(void) { return "mgic 0.1.0 (gfx950, fp64)"; }
+// 0.2.0 (round 5): mgic_op_params lost overlap_exchange and mgic_mg_params
+// lost fused_residual in round 4 (struct layouts changed); agglomerated
+// depths run on their owner rank only; mgic_abi_version added
+MGIC_API const char *mgic_version(void) { return "mgic 0.2.0 (gfx950, fp64 + fp32 mixed)"; }
+MGIC_API int mgic_abi_version(void) { return MGIC_ABI_VERSION; }
 MGIC_API const char *mgic_last_error(void) { return g_err.c_str(); }
 
 MGIC_API int mgic_set_device(int device) {
@@ -417,10 +421,16 @@ MGIC_API int mgic_plan_sizes(mgic_plan p, int *n_local, int *n_pack, int *n_unpa
   });
 }
 MGIC_API int mgic_plan_ipc_blocks(mgic_plan p, int *n, long long *rows) {
+  return mgic_plan_ipc_blocks_per(p, kern::kIpcBlockElemsDefault, n, rows);
+}
+MGIC_API int mgic_plan_ipc_blocks_per(mgic_plan p, long long block_elems, int *n,
+                                      long long *rows) {
   return guard([&] {
     NEED(p);
     NEED(n);
-    p->plan->finalize_ipc_host(kern::kIpcBlockElemsDefault);
+    MGIC_CHECK(block_elems >= 512 && block_elems <= (1 << 20) && block_elems % 512 == 0,
+               "block_elems must be a multiple of 512 in [512, 2^20]");
+    p->plan->finalize_ipc_host((long)block_elems);
     const auto r = p->plan->ipc_block_rows();
     *n = (int)r.size();
     if (rows)

@@ -1,6 +1,8 @@
 // level.cpp -- Comm, Grid, CopyPlan, LevelData (see level.hpp).
 #include "level.hpp"
 
+#include <cstdio>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -42,14 +44,21 @@ kern::HostPub Comm::host_pub(int slot, bool last) {
   kern::HostPub p;
   p.val = h_result_ + slot;
   if (last) {
+    // the sequence number is taken here and committed (commit_pub) once the
+    // publishing launch is queued: a launch that throws leaves the count as
+    // it was, so later waits do not wait for a number that never comes
     p.seq = h_seq_;
-    p.seqv = ++pub_count_;
+    p.seqv = pub_count_ + 1;
     if (ipc_) {
       p.err_src = sig_ + kern::kSigErr;
       p.err_dst = h_err_;
     }
   }
   return p;
+}
+
+void Comm::commit_pub(const kern::HostPub &p) {
+  if (p.seq) pub_count_ = p.seqv;
 }
 
 void Comm::wait_results(hipStream_t st, unsigned long long ticket) {
@@ -241,10 +250,24 @@ Comm::~Comm() {
   if (nccl_) ncclCommDestroy(nccl_);
   if (ipc_) {
     // no rank unmaps or frees its arena / signal page while a peer may still
-    // write into it (bounded: a peer that is gone times out the barrier)
-    try {
-      if (*h_err_ == 0) ipc_barrier();
-    } catch (...) {
+    // write into it: a collective barrier (every rank destroys its
+    // communicator), bounded -- a peer that is gone times it
+    // out after MGIC_IPC_TIMEOUT_S, which is reported on stderr.  It runs on
+    // a stream of its own after this rank's work on every stream has drained:
+    // the caller's stream (mgic_comm_set_stream) may be gone by now.
+    if (*h_err_ == 0) {
+      hipStream_t s = nullptr;
+      const hipStream_t keep = stream_;
+      try {
+        MGIC_HIP(hipDeviceSynchronize());
+        MGIC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        stream_ = s;
+        ipc_barrier();
+      } catch (const std::exception &e) {
+        fprintf(stderr, "mgic: rank %d: communicator teardown barrier: %s\n", rank_, e.what());
+      }
+      stream_ = keep;
+      if (s) (void)hipStreamDestroy(s);
     }
     (void)hipDeviceSynchronize();
     for (int r = 0; r < size_; ++r) {

@@ -72,6 +72,9 @@ class Comm {
   // result `slot` into h_result(); `last` also publishes the transport's error
   // word and the sequence number wait_results() spins on
   kern::HostPub host_pub(int slot, bool last);
+  // after the launch that publishes `p` is queued: its sequence number becomes
+  // the one wait_results() waits for
+  void commit_pub(const kern::HostPub &p);
   // until the last host_pub(…, true) result (or the one of `ticket`, a
   // last_ticket() value) has landed (host spin on pinned memory, no stream
   // synchronisation); raises a transport timeout

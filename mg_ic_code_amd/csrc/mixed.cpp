@@ -5,9 +5,11 @@
 
 namespace mgic {
 
+// the deep-halo schedule's shell depth (op.cpp kDeepDepth)
+static constexpr int kDeepShell = 4;
+
 void MixedMultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGParams &p) {
   MGParams q = p;
-  MGIC_CHECK(q.agglomerate_below == 0, "mixed V-cycle: agglomeration is not supported");
   q.bottom_solver = 0;  // relax(n_bottom) at the coarsest depth
   mg.define(factory, q);
   lf_.clear();
@@ -16,21 +18,35 @@ void MixedMultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const 
     VariableCoeffPoissonOperator &op = mg.op(d);
     const hipStream_t st = op.stream();
     LevelF &L = lf_[d];
-    L.s = op.stencil();
-    L.halo = op.grid->has_memory_faces();
+    if (mg.agglomerated(d)) {  // every rank takes part in the gather / scatter
+      L.r_stage = std::make_unique<LevelDataF>(mg.stage_grid(d));
+      L.e_stage = std::make_unique<LevelDataF>(mg.stage_grid(d));
+    }
+    // (a gathered depth on another rank: empty fields, never touched)
     L.e = std::make_unique<LevelDataF>(op.grid);
     L.r = std::make_unique<LevelDataF>(op.grid);
     L.tmp = std::make_unique<LevelDataF>(op.grid);
     L.a = std::make_unique<LevelDataF>(op.grid);
     L.b = std::make_unique<LevelDataF>(op.grid);
-    // coefficients: the fp64 hierarchy (averaged in fp64) rounded once,
-    // ghost layer 1 included (exchanged first) for the red ring on a halo
-    op.m_aCoef->exchange(st);
-    op.m_bCoef->exchange(st);
+    if (!mg.runs(d)) continue;
+    L.s = op.stencil();
+    L.halo = op.grid->has_memory_faces();
+    L.deep = L.halo && op.deepApplies();
+    // coefficients: the fp64 hierarchy (averaged in fp64) rounded once, with
+    // the ghost layers the sweeps' rings read on exchanged faces (layer 1;
+    // the 4-deep shell in deep-halo mode), exchanged first
+    const int gd = L.deep ? kDeepShell : 1;
+    if (L.deep) {
+      op.m_aCoef->exchange_shell(st, kDeepShell);
+      op.m_bCoef->exchange_shell(st, kDeepShell);
+    } else {
+      op.m_aCoef->exchange(st);
+      op.m_bCoef->exchange(st);
+    }
     for (int n = 0; n < op.grid->nlocal(); ++n) {
       const BoxArgs &g = op.boxArgs(n, true);
-      kern::to_float(L.a->p[n], op.m_aCoef->p[n], g, 1, st);
-      kern::to_float(L.b->p[n], op.m_bCoef->p[n], g, 1, st);
+      kern::to_float(L.a->p[n], op.m_aCoef->p[n], g, gd, st);
+      kern::to_float(L.b->p[n], op.m_bCoef->p[n], g, gd, st);
     }
   }
 }
@@ -86,9 +102,11 @@ void MixedMultiGrid::relax(int d, LevelDataF &e, const LevelDataF &r, int n, boo
     return;
   }
   // two sweeps per launch (the temporally blocked kernel, smoother_tb.hip)
-  // on levels without exchanged faces; a last sweep that folds phi += e
-  // into fp64 stays a single sweep
-  bool two = !L.halo && n >= 2;
+  // on levels without exchanged faces, and on exchanged layouts in deep-halo
+  // mode (a 4-deep shell before each pair: the kernel's rings run onto it);
+  // a last sweep that folds phi += e into fp64 stays a single sweep (on a
+  // 2-deep shell)
+  bool two = (!L.halo || L.deep) && n >= 2;
   for (int b = 0; two && b < op.grid->nlocal(); ++b)
     two = kern::gsrb_sweep_tb2_applies(op.boxArgs(b, true), L.s, kind);
   for (int it = 0; it < n;) {
@@ -96,7 +114,7 @@ void MixedMultiGrid::relax(int d, LevelDataF &e, const LevelDataF &r, int n, boo
     const int left = n - it;
     const int k = two && (left >= 3 || (left == 2 && !acc)) ? 2 : 1;
     const bool last = it + k == n;
-    if (L.halo && !zin) src->exchange_shell(st);
+    if (L.halo && !zin) src->exchange_shell(st, k == 2 ? kDeepShell : 2);
     for (int b = 0; b < op.grid->nlocal(); ++b) {
       const long nc = op.grid->geom[b].valid.ncells();
       prof_mark(st, nc, true, 2 * k);
@@ -120,8 +138,14 @@ void MixedMultiGrid::relax(int d, LevelDataF &e, const LevelDataF &r, int n, boo
 
 void MixedMultiGrid::prolongInto(int d) {
   VariableCoeffPoissonOperator &op = mg.op(d);
-  const Grid &cg = *mg.op(d + 1).grid;
   const hipStream_t st = op.stream();
+  LevelF &N = lf_[d + 1];
+  // a gathered coarser depth: its correction scattered back onto this
+  // layout coarsened (valid cells and face ghosts) first
+  const bool agg = mg.agglomerated(d + 1);
+  if (agg) mg.scatter_plan(d + 1).execute_f(*op.grid->comm, N.e->d_tab, N.e_stage->d_tab, st);
+  const Grid &cg = agg ? *mg.stage_grid(d + 1) : *mg.op(d + 1).grid;
+  LevelDataF &ec = agg ? *N.e_stage : *N.e;
   for (int n = 0; n < op.grid->nlocal(); ++n) {
     const Box &cb = cg.geom[n].valid;
     int alo[3], ahi[3];
@@ -129,29 +153,46 @@ void MixedMultiGrid::prolongInto(int d) {
       alo[k] = cg.periodic[k] || cb.lo[k] > cg.domain.lo[k];
       ahi[k] = cg.periodic[k] || cb.hi[k] < cg.domain.hi[k];
     }
-    kern::prolong_f(lf_[d].e->p[n], op.boxArgs(n, true), lf_[d + 1].e->p[n], cg.box_args_plain(n),
+    kern::prolong_f(lf_[d].e->p[n], op.boxArgs(n, true), ec.p[n], cg.box_args_plain(n),
                     alo, ahi, op.prm.prolong_type, st);
   }
+}
+
+void MixedMultiGrid::restrictInto(int d) {
+  VariableCoeffPoissonOperator &op = mg.op(d);
+  const hipStream_t st = op.stream();
+  LevelF &L = lf_[d], &N = lf_[d + 1];
+  const bool agg = mg.agglomerated(d + 1);
+  const Grid &cg = agg ? *mg.stage_grid(d + 1) : *mg.op(d + 1).grid;
+  LevelDataF &rc = agg ? *N.r_stage : *N.r;
+  for (int n = 0; n < op.grid->nlocal(); ++n)
+    kern::restrict_residual_f(rc.p[n], cg.box_args_plain(n), L.e->p[n], L.r->p[n], L.a->p[n],
+                              L.b->p[n], op.boxArgs(n, true), L.s, st);
+  if (agg) mg.gather_plan(d + 1).execute_f(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
 }
 
 void MixedMultiGrid::cycle(int d, bool e_zero, LevelData *phi_acc, bool halo_out) {
   VariableCoeffPoissonOperator &op = mg.op(d);
   const hipStream_t st = op.stream();
   LevelF &L = lf_[d];
-  if (L.halo) L.r->exchange(st);  // r's ghost layer once per level visit
+  // r's ghosts once per level visit (layer 1, or the 4-deep shell)
+  if (L.halo) {
+    if (L.deep) L.r->exchange_shell(st, kDeepShell);
+    else L.r->exchange(st);
+  }
   const MGParams &prm = mg.prm;
   if (d == mg.depths() - 1) {  // bottom: relax(n_bottom)
     relax(d, *L.e, *L.r, prm.n_bottom, e_zero, phi_acc, halo_out);
     return;
   }
   relax(d, *L.e, *L.r, prm.n_pre, e_zero, nullptr, true);
-  LevelF &N = lf_[d + 1];
-  const Grid &cg = *mg.op(d + 1).grid;
-  for (int n = 0; n < op.grid->nlocal(); ++n)
-    kern::restrict_residual_f(N.r->p[n], cg.box_args_plain(n), L.e->p[n], L.r->p[n], L.a->p[n],
-                              L.b->p[n], op.boxArgs(n, true), L.s, st);
-  for (int c = 0; c < prm.cycles; ++c)
-    cycle(d + 1, c == 0, nullptr, op.prm.prolong_type == 1 && c == prm.cycles - 1);
+  restrictInto(d);
+  // a gathered coarser depth runs on its owner only (the others wait for
+  // the scatter); its face ghosts come with the scatter
+  const bool agg = mg.agglomerated(d + 1);
+  if (mg.runs(d + 1))
+    for (int c = 0; c < prm.cycles; ++c)
+      cycle(d + 1, c == 0, nullptr, !agg && op.prm.prolong_type == 1 && c == prm.cycles - 1);
   prolongInto(d);
   relax(d, *L.e, *L.r, prm.n_post, false, phi_acc, halo_out);
 }
@@ -161,31 +202,36 @@ double MixedMultiGrid::fmg(LevelData &phi, const LevelData &rhs, LevelData *resi
   // the residual equation's right-hand side at every depth: r_{d+1} = R(r_d)
   // (restrictResidual of a zero correction)
   const int D = mg.depths();
-  for (int d = 0; d + 1 < D; ++d) {
+  for (int d = 0; d + 1 < D && mg.runs(d); ++d) {
     VariableCoeffPoissonOperator &op = mg.op(d);
     const hipStream_t st = op.stream();
     LevelF &L = lf_[d];
     for (int b = 0; b < op.grid->nlocal(); ++b)
       MGIC_HIP(hipMemsetAsync(L.e->base[b], 0, sizeof(float) * (size_t)op.grid->geom[b].total, st));
     if (L.halo) L.r->exchange(st);
-    const Grid &cg = *mg.op(d + 1).grid;
-    for (int n = 0; n < op.grid->nlocal(); ++n)
-      kern::restrict_residual_f(lf_[d + 1].r->p[n], cg.box_args_plain(n), L.e->p[n], L.r->p[n],
-                                L.a->p[n], L.b->p[n], op.boxArgs(n, true), L.s, st);
+    restrictInto(d);
   }
   if (D == 1) {  // a single depth: the bottom relax is the whole solve
     relax(0, *lf_[0].e, *lf_[0].r, mg.prm.n_bottom, true, &phi, false);
     return residualF(phi, rhs, resid64, normType);
   }
-  // coarsest: relax from zero; then up: e_d = P e_{d+1}, ncycles V-cycles
-  {
+  // coarsest: relax from zero (on its owner when gathered); then up: e_d =
+  // P e_{d+1}, ncycles V-cycles
+  if (mg.runs(D - 1)) {
     LevelF &B = lf_[D - 1];
-    if (B.halo) B.r->exchange(mg.op(D - 1).stream());
-    relax(D - 1, *B.e, *B.r, mg.prm.n_bottom, true, nullptr, mg.op(D - 1).prm.prolong_type == 1);
+    if (B.halo) {
+      if (B.deep) B.r->exchange_shell(mg.op(D - 1).stream(), kDeepShell);
+      else B.r->exchange(mg.op(D - 1).stream());
+    }
+    relax(D - 1, *B.e, *B.r, mg.prm.n_bottom, true, nullptr,
+          !mg.agglomerated(D - 1) && mg.op(D - 1).prm.prolong_type == 1);
   }
   for (int d = D - 2; d >= 0; --d) {
     VariableCoeffPoissonOperator &op = mg.op(d);
     const hipStream_t st = op.stream();
+    if (!mg.runs(d)) {  // a gathered depth held by another rank
+      continue;
+    }
     for (int b = 0; b < op.grid->nlocal(); ++b)
       MGIC_HIP(hipMemsetAsync(lf_[d].e->base[b], 0, sizeof(float) * (size_t)op.grid->geom[b].total, st));
     prolongInto(d);

@@ -11,7 +11,11 @@
 // fp64, folded into the last post-smoothing sweep.  Same schedule as
 // MultiGrid::cycle (pre-relax from zero, restrict, recurse, prolong,
 // post-relax; relax(n_bottom) at the coarsest depth), same halo
-// bookkeeping; no agglomeration, no BiCGStab bottom (relax only).
+// bookkeeping, same agglomeration (depths gathered onto rank 0, which alone
+// relaxes them: the restriction is gathered and the correction scattered as
+// fp32 messages) and, in deep-halo mode, the same schedule (two sweeps per
+// 4-deep shell exchange, both in one two-sweep launch); no BiCGStab bottom
+// (relax only).
 //
 // Also the full-multigrid (FMG) start the C5 config names: restrict the
 // fine residual to every depth, relax at the coarsest, then at each finer
@@ -43,14 +47,19 @@ class MixedMultiGrid {
  private:
   struct LevelF {
     std::unique_ptr<LevelDataF> e, r, tmp, a, b;
+    // the first gathered depth: the restriction before the gather and the
+    // correction after the scatter, on the finer layout coarsened
+    std::unique_ptr<LevelDataF> r_stage, e_stage;
     StencilCoefs s;
     bool halo = false;
+    bool deep = false;  // exchanged faces in deep-halo mode (4-deep shells)
   };
   std::vector<LevelF> lf_;
   void cycle(int d, bool e_zero, LevelData *phi_acc, bool halo_out);
   void relax(int d, LevelDataF &e, const LevelDataF &r, int n, bool zero_in, LevelData *acc,
              bool halo_out);
-  void prolongInto(int d);  // e[d] += P e[d+1]
+  void prolongInto(int d);  // e[d] += P e[d+1] (scattered first when d+1 is gathered)
+  void restrictInto(int d);  // r[d+1] = R(r[d] - L e[d]) (gathered when d+1 is gathered)
   double residualF(LevelData &phi, const LevelData &rhs, LevelData *resid64, int normType);
 };
 

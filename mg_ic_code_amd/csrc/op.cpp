@@ -296,6 +296,9 @@ void VariableCoeffPoissonOperator::resetLambda() {
   if (!m_lambdaNeedsResetting) return;  // .cpp:222
   m_lambdaNeedsResetting = false;
   if (!m_lambda) m_lambda = std::make_unique<LevelData>(grid);
+  // a gathered depth on a rank that does not hold it: nothing to compute
+  // (it never runs a kernel or a reduction there)
+  if (owner_local >= 0 && grid->comm->rank() != owner_local) return;
   // is bCoef one value everywhere?  (max b == min b over all ranks' boxes)
   const double bmax = reduce(4, *m_bCoef, nullptr), bmin = -reduce(5, *m_bCoef, nullptr);
   b_const_ = bmax == bmin && std::isfinite(bmax);
@@ -726,17 +729,23 @@ void VariableCoeffPoissonOperator::finish_reduce(int kind, double *parts, int to
   Comm &c = *grid->comm;
   const hipStream_t st = stream();
   double *res = c.d_result() + slot;
+  // a gathered depth reduces on its owner alone (the rank-0 bottom solve:
+  // no other rank joins its Krylov reductions)
+  if (owner_local >= 0 && c.rank() != owner_local)
+    throw Error(kState, "reduction on a gathered MG depth: it runs on its owner rank only");
   const kern::HostPub pub = c.host_pub(slot, last);
-  const bool solo = c.size() == 1;
+  const bool solo = c.size() == 1 || owner_local >= 0;
   if (total == 0) {  // no local cells: the identity of the reduction
     *c.h_stage() = kind >= 4 ? -HUGE_VAL : 0.0;
     MGIC_HIP(hipMemcpyAsync(res, c.h_stage(), sizeof(double), hipMemcpyHostToDevice, st));
     MGIC_HIP(hipStreamSynchronize(st));  // (the staging word is reused)
     c.allreduce(res, kind >= 3 ? 1 : 0, pub);
+    c.commit_pub(pub);
     return;
   }
   kern::reduce_final(kind, parts, total, res, st, solo ? pub : kern::HostPub());
   if (!solo) c.allreduce(res, kind >= 3 ? 1 : 0, pub);
+  c.commit_pub(pub);
 }
 
 double VariableCoeffPoissonOperator::reduce(int kind, const LevelData &x, const LevelData *y) {
@@ -972,6 +981,7 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
         aop->define(ag, op->prm);
         aop->m_aCoef = a;
         aop->m_bCoef = b;
+        aop->owner_local = 0;  // the bottom solve is rank 0's alone
         aop->computeLambda();
         L.r_stage = op->create();
         L.e_stage = op->create();
@@ -981,6 +991,7 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
         L.r = aop->create();
         L.op = std::move(aop);
         L.agg = true;
+        L.owner = 0;
         agg_chain = true;
       }
     } else {
@@ -1008,10 +1019,12 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
         op->m_aCoef = average_coef(*prev.m_aCoef, cg, 2, harm);
         op->m_bCoef = average_coef(*prev.m_bCoef, cg, 2, harm);
       }
+      op->owner_local = 0;
       op->computeLambda();
       L.e = op->create();
       L.r = op->create();
       L.op = std::move(op);
+      L.owner = 0;
     }
     levels_.push_back(std::move(L));
   }
@@ -1056,9 +1069,12 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
   if (N.agg) N.restrict_plan->execute(*op.grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
   // coarse correction e_c = 0 (folded into its first sweep when possible);
   // its last relax exchanges e_c's ghosts for the linear prolongation
+  // a gathered coarse depth runs on its owner only; the other ranks go on to
+  // the scatter, whose receives wait (on the device) for the owner's result
   const bool coarse_out = !N.agg && op.prm.prolong_type == 1;
-  for (int c = 0; c < prm.cycles; ++c)
-    cycle(d + 1, *N.e, *N.r, c == 0, nullptr, coarse_out && c == prm.cycles - 1);
+  if (runs(d + 1))
+    for (int c = 0; c < prm.cycles; ++c)
+      cycle(d + 1, *N.e, *N.r, c == 0, nullptr, coarse_out && c == prm.cycles - 1);
   if (!N.agg) {
     op.prolongIncrementFilled(e, *N.e);
   } else {
@@ -1073,21 +1089,24 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
 
 void MultiGrid::fmg(LevelData &e0, LevelData &r0, LevelData &phi, int ncycles) {
   const int D = depths();
-  for (int d = 1; d < D; ++d)
-    MGIC_CHECK(!levels_[d].agg, "FMG: agglomerated depths are not supported");
   auto E = [&](int d) -> LevelData & { return d == 0 ? e0 : *levels_[d].e; };
   auto Rr = [&](int d) -> LevelData & { return d == 0 ? r0 : *levels_[d].r; };
   if (D == 1) {  // one depth: the bottom solve is the whole cycle
     cycle(0, e0, r0, true, &phi);
     return;
   }
-  // right-hand sides: r_{d+1} = restrictResidual of a zero correction
-  for (int d = 0; d + 1 < D; ++d) {
+  // right-hand sides: r_{d+1} = restrictResidual of a zero correction; into
+  // a gathered depth through its stage and the gather (every rank), below it
+  // on the owner only
+  for (int d = 0; d + 1 < D && runs(d); ++d) {
+    Level &N = levels_[d + 1];
+    const hipStream_t st = levels_[d].op->stream();
     levels_[d].op->setToZero(E(d));
-    levels_[d].op->restrictResidual(Rr(d + 1), E(d), Rr(d), true);
+    levels_[d].op->restrictResidual(N.agg ? *N.r_stage : Rr(d + 1), E(d), Rr(d), true);
+    if (N.agg) N.restrict_plan->execute(*levels_[d].op->grid->comm, N.r_stage->d_tab, N.r->d_tab, st);
   }
   // coarsest depth from zero, then up with e_d = P e_{d+1} as the start
-  {
+  if (runs(D - 1)) {
     VariableCoeffPoissonOperator &op = *levels_[D - 1].op;
     if (prm.bottom_solver == 1) {
       op.setToZero(E(D - 1));
@@ -1097,9 +1116,15 @@ void MultiGrid::fmg(LevelData &e0, LevelData &r0, LevelData &phi, int ncycles) {
     }
   }
   for (int d = D - 2; d >= 0; --d) {
+    Level &N = levels_[d + 1];
     VariableCoeffPoissonOperator &op = *levels_[d].op;
+    if (N.agg) {  // scatter the gathered correction (every rank)
+      N.prolong_plan->execute(*op.grid->comm, N.e->d_tab, N.e_stage->d_tab, op.stream());
+    }
+    if (!runs(d)) continue;
     op.setToZero(E(d));
-    op.prolongIncrement(E(d), E(d + 1));
+    if (N.agg) op.prolongIncrementFilled(E(d), *N.e_stage);
+    else op.prolongIncrement(E(d), E(d + 1));
     for (int c = 0; c < ncycles; ++c)
       cycle(d, E(d), Rr(d), false, d == 0 && c == ncycles - 1 ? &phi : nullptr);
   }

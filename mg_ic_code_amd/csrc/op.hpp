@@ -133,6 +133,10 @@ class VariableCoeffPoissonOperator {
   double b_val_ = 1.0;
   bool rcp_fast_ = false;     // StencilCoefs::rcp_fast (lambda's range, all ranks)
   bool rcp_fast32_ = false;   // StencilCoefs::rcp_fast32
+  // a gathered MG depth (every box on one rank): its reductions are that
+  // rank's alone -- no allreduce, no other rank involved -- and any other rank
+  // that asks for one gets an error (MultiGrid never does); -1: collective
+  int owner_local = -1;
 
 
  private:
@@ -279,7 +283,22 @@ class MultiGrid {
   VariableCoeffPoissonOperator &op(int d) { return *levels_[d].op; }
   LevelData *corr(int d) { return levels_[d].e.get(); }
   LevelData *resid(int d) { return levels_[d].r.get(); }
+  // depth d is the first gathered depth (the restriction is gathered into it,
+  // the correction scattered out of it)
   bool agglomerated(int d) const { return levels_[d].agg; }
+  // the rank that holds every box of depth d when it is gathered (the first
+  // gathered depth and every depth below it), else -1 (distributed)
+  int owner(int d) const { return levels_[d].owner; }
+  // this rank runs depth d (distributed, or gathered onto this rank)
+  bool runs(int d) const {
+    return levels_[d].owner < 0 || levels_[d].owner == levels_[d].op->grid->comm->rank();
+  }
+  // the first gathered depth's plans: the previous layout coarsened (the
+  // restriction's target before the gather, the prolongation's source after
+  // the scatter) -> the gathered box, and back
+  std::shared_ptr<Grid> stage_grid(int d) const { return levels_[d].r_stage->grid; }
+  CopyPlan &gather_plan(int d) { return *levels_[d].restrict_plan; }
+  CopyPlan &scatter_plan(int d) { return *levels_[d].prolong_plan; }
   MGParams prm;
   BiCGStabSolver bottom;
 
@@ -287,7 +306,8 @@ class MultiGrid {
   struct Level {
     std::unique_ptr<VariableCoeffPoissonOperator> op;
     std::unique_ptr<LevelData> e, r;
-    bool agg = false;  // this level lives on rank 0 (gathered)
+    bool agg = false;  // the first gathered depth (plans below)
+    int owner = -1;    // gathered: the rank holding its box
     std::unique_ptr<LevelData> r_stage, e_stage;  // previous layout coarsened
     std::unique_ptr<CopyPlan> restrict_plan, prolong_plan;
   };

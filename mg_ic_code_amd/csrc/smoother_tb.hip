@@ -75,6 +75,12 @@ using IC = std::integral_constant<int, N>;
 constexpr bool kPF2 = true;
 constexpr bool kZinShort = true;
 constexpr bool kSkipOut = true;
+#ifndef TB2_SPREAD
+#define TB2_SPREAD 0
+#endif
+#ifndef TB2_DSTORE
+#define TB2_DSTORE 0
+#endif
 
 // Geometry.  Rows of the LDS ring are SHIFTED pairings: in row y of plane k
 // pair m holds cells (X, X+1) with X = x0 - 6 + 2m + s, s = (x0 + y + k +
@@ -429,18 +435,22 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
       Bs[tid + i * NT] = pu1[b][i];
     }
   };
-  auto fetch_c = [&](int t, int p, auto bc, auto sd) {
+  auto fetch_c = [&](int t, int p, auto bc, auto sd, int which = 3) {
     constexpr int b = decltype(bc)::value;
     constexpr bool SD = decltype(sd)::value;
     const char *pr = SD ? plane_u(rhs, p) : plane(rhs, p), *pa = SD ? plane_u(a, p) : plane(a, p);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      const V vr = at2(pr, roff[t][i]);
-      const V va = at2(pa, roff[t][i]);
-      nr0[b][i] = vr.x;
-      nr1[b][i] = vr.y;
-      na0[b][i] = va.x;
-      na1[b][i] = va.y;
+      if (which & 1) {
+        const V vr = at2(pr, roff[t][i]);
+        nr0[b][i] = vr.x;
+        nr1[b][i] = vr.y;
+      }
+      if (which & 2) {
+        const V va = at2(pa, roff[t][i]);
+        na0[b][i] = va.x;
+        na1[b][i] = va.y;
+      }
     }
   };
   auto lam = [&](T aa) {  // .cpp:234-243 (a*alpha == alpha*a)
@@ -635,28 +645,66 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     const int E0 = es(p);  // this step's slots derive from this one
     image(p + 1, ICF{}, SDC{});
     put(eadd(E0, 1), ICF{});
-    if (PF == 2) fetch_c(PT, p + 2, ICF{}, SDC{});
-    else fetch_c(PU, p + 1, ICF{}, SDC{});
-    if constexpr (ACC) {
-      const char *pl = SDC::value ? plane_u(acc, p - 3) : plane(acc, p - 3);
+    auto fc = [&](int which) {
+      if (PF == 2) fetch_c(PT, p + 2, ICF{}, SDC{}, which);
+      else fetch_c(PU, p + 1, ICF{}, SDC{}, which);
+    };
+    auto fa = [&] {
+      if constexpr (ACC) {
+        const char *pl = SDC::value ? plane_u(acc, p - 3) : plane(acc, p - 3);
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        ac0[i] = an0[i];
-        ac1[i] = an1[i];
-        const double2 v = at2(pl, roff[PU][i]);
-        an0[i] = v.x;
-        an1[i] = v.y;
+        for (int i = 0; i < NP; ++i) {
+          ac0[i] = an0[i];
+          ac1[i] = an1[i];
+          const double2 v = at2(pl, roff[PU][i]);
+          an0[i] = v.x;
+          an1[i] = v.y;
+        }
       }
-    }
-    if (PF == 2) fetch_u(PU, p + 3, ICF{}, SDC{});
-    else fetch_u(PT, p + 2, ICF{}, SDC{});
+    };
+    auto fu = [&] {
+      if (PF == 2) fetch_u(PU, p + 3, ICF{}, SDC{});
+      else fetch_u(PT, p + 2, ICF{}, SDC{});
+    };
+    constexpr int SPR = TB2_SPREAD;
+    // TB2_SPREAD (measurement): 0 every load before the first barrier; 1 u
+    // there, rhs / aCoef between the red passes, acc in the black phase; 2 u
+    // after the first barrier, the rest as 1; 3 u before, rhs between the red
+    // passes, aCoef (and acc) between the black ones
+    // TB2_DSTORE (measurement): 0 plane p-4 stored at the end of step p; 1 / 2
+    // / 3 plane p-5 stored in step p (its slot is rewritten at step p+2):
+    // after sweep-1 red, right after the first barrier, right after the second
+    // (before acc's rotation, which the stored plane still uses)
+    constexpr int DST = TB2_DSTORE;
+    static_assert(DST == 0 || SPR != 0, "a delayed store needs the spread acc load");
+    auto dstore = [&] { store(PU, p - 5, eadd(E0, -5), SDC{}); };
+    // 4: rhs / aCoef between the red passes, u (and acc) between the black
+    // ones; 5: as 4 with aCoef and acc at the start of the black phase; 6:
+    // rhs / aCoef between the red passes, u and acc at the start of the black
+    // phase; 7: rhs / aCoef before the first barrier, u between the red passes
+    if (SPR == 0) { fc(3); fa(); fu(); }
+    if (SPR == 1 || SPR == 3) fu();
+    if (SPR == 7) fc(3);
     __syncthreads();
+    if (DST == 2) dstore();
+    if (SPR == 2) fu();
     pass(IC<(ZIN && kZinShort) ? 1 : 0>{}, SDC{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], Rl[J0]);
+    if (DST == 1) dstore();
+    if (SPR == 1 || SPR == 2 || SPR == 4 || SPR == 6) fc(3);
+    if (SPR == 3 || SPR == 5) fc(1);
+    if (SPR == 7) fu();
     pass(IC<0>{}, SDC{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], Rl[J3]);
     __syncthreads();
+    if (DST == 3) dstore();
+    if (SPR == 1 || SPR == 2 || SPR == 6 || SPR == 7) fa();
+    if (SPR == 5) { fc(2); fa(); }
+    if (SPR == 6) fu();
     pass(IC<(ZIN && kZinShort) ? 2 : 0>{}, SDC{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], Bl[J0]);
+    if (SPR == 3) { fc(2); fa(); }
+    if (SPR == 4) { fu(); fa(); }
+    if (SPR == 5) fu();
     pass(IC<0>{}, SDC{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], Bl[J3]);
-    store(PT, p - 4, eadd(E0, -4), SDC{});
+    if (DST == 0) store(PT, p - 4, eadd(E0, -4), SDC{});
   };
 
   fetch_u(1, pstart - 1, IC<0>{}, IC<0>{});
@@ -694,7 +742,8 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     for (; p < pstart + 8 && p <= pend; p += 4) group(IC<0>{}, p);
     for (; p <= ssh; p += 4) group(IC<1>{}, p);
   }
-  for (; p <= pend; p += 4) group(IC<0>{}, p);
+  // (a delayed store takes one step more: plane z1 - 1 at step pend + 1)
+  for (; p <= pend + (TB2_DSTORE ? 1 : 0); p += 4) group(IC<0>{}, p);
 }
 
 

@@ -73,7 +73,8 @@ struct IpcBlock {
 constexpr long kIpcBlockElemsDefault = 2048;
 inline long ipc_item_per(long cells, long maxper) {
   long per = 512;
-  while (per < maxper && per * 32 <= cells) per *= 2;
+  // (doubling, clamped: a maxper that is not 512 * 2^k is still the cap)
+  while (per < maxper && per * 32 <= cells) per = per * 2 < maxper ? per * 2 : maxper;
   return per;
 }
 inline long ipc_blocks(long cells, long per) { return (cells + per - 1) / per; }

@@ -81,14 +81,16 @@ class HostPlan:
         most 32 peers per plan)."""
         _lib.call("mgic_plan_check_transport", self._h, {"rccl": 1, "ipc": 2}[transport])
 
-    def ipc_blocks(self) -> np.ndarray:
+    def ipc_blocks(self, block_elems: int = 2048) -> np.ndarray:
         """The peer-mapped transport's put / get blocks: rows (side 0 put /
-        1 get, peer rank, flag, first message element, element count)."""
+        1 get, peer rank, flag, first message element, element count), for
+        blocks of at most block_elems elements (MGIC_IPC_BLOCK_ELEMS; one
+        size per plan)."""
         n = ctypes.c_int()
-        _lib.call("mgic_plan_ipc_blocks", self._h, ctypes.byref(n), None)
+        _lib.call("mgic_plan_ipc_blocks_per", self._h, int(block_elems), ctypes.byref(n), None)
         out = np.zeros((n.value, 5), dtype=np.int64)
         if n.value:
-            _lib.call("mgic_plan_ipc_blocks", self._h, ctypes.byref(n),
+            _lib.call("mgic_plan_ipc_blocks_per", self._h, int(block_elems), ctypes.byref(n),
                       out.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)))
         return out
 

@@ -8,9 +8,11 @@ box has (all ranks may share device 0).
     mp_worker.py --rank R --world W --port P --n N --out DIR [--device D]
                  [--mode vcycle|mixed]
 mode vcycle (config C4): init_residual + `iters` AMRMultiGrid iterations of
-the fp64 V-cycle, deep halo.  mode mixed (config C5): init_residual, one
-FMG cycle and `iters` V-cycle iterations of the mixed fp32 smoother / fp64
-residual MultiGrid (fp32 messages).
+the fp64 V-cycle, deep halo (--bottom-solver 1: the reference's BiCGStab
+bottom, on rank 0 when the coarsest depth is gathered).  mode mixed (config
+C5): init_residual, one FMG cycle and `iters` V-cycle iterations of the mixed
+fp32 smoother / fp64 residual MultiGrid (fp32 messages), deep halo; both
+modes gather the depths --agglomerate-below names onto rank 0.
 Writes DIR/rank<R>.npz: this rank's phi boxes, the residual max norms, the
 transport used.  gloo (127.0.0.1) is the control
 plane; nothing touches the GPU before the process group exists.
@@ -35,6 +37,7 @@ def main():
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--agglomerate-below", type=int, default=0)
+    ap.add_argument("--bottom-solver", type=int, default=0)
     ap.add_argument("--mode", choices=("vcycle", "mixed"), default="vcycle")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -53,12 +56,13 @@ def main():
     from mg_ic_code_amd.commcheck import check_transport
     checked = check_transport(comm, a.world)  # bench.py's transport check
     mixed = a.mode == "mixed"
-    case = bench.build_case(mg, comm, a.world, a.n, a.levels, 4, deep_halo=0 if mixed else 1,
-                            agglomerate_below=a.agglomerate_below)
+    case = bench.build_case(mg, comm, a.world, a.n, a.levels, 4, deep_halo=1,
+                            agglomerate_below=a.agglomerate_below, bottom_solver=a.bottom_solver)
     amg, fphi, frhs, fres, grid = (case[k] for k in ("amg", "fphi", "frhs", "fres", "grid"))
     if mixed:
         amg = mg.MixedMultiGrid(case["fac"], mg.SolverParams(
-            max_depth=a.levels - 1, n_pre=4, n_post=4, n_bottom=4, bottom_solver=0))
+            max_depth=a.levels - 1, n_pre=4, n_post=4, n_bottom=4, bottom_solver=0,
+            agglomerate_below=a.agglomerate_below))
         norms = [amg.init_residual(fphi, frhs, fres, 0), amg.fmg(fphi, frhs, fres, 0)]
         norms += [amg.iteration(fphi, frhs, fres, 0) for _ in range(a.iters)]
     else:

@@ -334,12 +334,13 @@ def test_gather_plan_with_many_peers_is_rccl_executable():
     ex.check_transport("ipc")
 
 
-def _message_rows(plans, world):
+def _message_rows(plans, world, block_elems=2048):
     """{(sender, receiver): (put rows, get rows)} of every message, each as
     sorted (flag, first element, count) tuples."""
     msgs = {}
     for r, plan in enumerate(plans):
-        for side, peer, flag, first, cnt in plan.ipc_blocks().tolist():
+        for side, peer, flag, first, cnt in plan.ipc_blocks(block_elems).tolist():
+            assert 0 < cnt <= block_elems  # blocks of at most the configured size
             key = (r, peer) if side == 0 else (peer, r)
             msgs.setdefault(key, ([], []))[side].append((flag, first, cnt))
     return {k: (sorted(p), sorted(g)) for k, (p, g) in msgs.items()}
@@ -348,7 +349,8 @@ def _message_rows(plans, world):
 @pytest.mark.parametrize("world,shell,periodic", [(2, 4, (0, 0, 0)), (4, 4, (0, 0, 0)),
                                                   (8, 4, (0, 0, 0)), (8, 0, (0, 0, 0)),
                                                   (8, 4, (1, 1, 1)), (3, 1, (1, 0, 1))])
-def test_ipc_message_blocks_agree_on_both_sides(world, shell, periodic):
+@pytest.mark.parametrize("block_elems", [512, 1024, 1536, 2048, 4096])
+def test_ipc_message_blocks_agree_on_both_sides(world, shell, periodic, block_elems):
     # the peer-mapped transport's hand-off: get block f of a message waits for
     # the flag of put block f, so both sides must split every message into the
     # same blocks, numbered by message offset 0, 1, ... (bench.py's splits,
@@ -363,7 +365,7 @@ def test_ipc_message_blocks_agree_on_both_sides(world, shell, periodic):
         dom, boxes, owners = decompose((n, n, n), world)
     plans = [HostPlan(r, world, dom, list(boxes), list(owners), periodic=periodic, shell=shell)
              for r in range(world)]
-    msgs = _message_rows(plans, world)
+    msgs = _message_rows(plans, world, block_elems)
     assert msgs
     for (s, r), (put, get) in msgs.items():
         assert put == get, (s, r)

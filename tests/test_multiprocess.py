@@ -31,7 +31,8 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, mode="vcycle"):
+def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, mode="vcycle",
+                bottom_solver=0):
     port = free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONUNBUFFERED="1")
     procs = []
@@ -43,7 +44,7 @@ def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, 
             [sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), "--rank", str(r),
              "--world", str(world), "--port", str(port), "--n", str(n), "--levels", str(levels),
              "--agglomerate-below", str(agglomerate_below), "--out", str(tmp_path),
-             "--mode", mode],
+             "--mode", mode, "--bottom-solver", str(bottom_solver)],
             stdout=log, stderr=subprocess.STDOUT, env=env))
     rcs = []
     try:
@@ -63,10 +64,10 @@ def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, 
     return out
 
 
-def single_box(n, levels, iters=2, mode="vcycle"):
+def single_box(n, levels, iters=2, mode="vcycle", bottom_solver=0):
     import bench
     comm = mg.Comm()
-    case = bench.build_case(mg, comm, 1, n, levels, 4)
+    case = bench.build_case(mg, comm, 1, n, levels, 4, bottom_solver=bottom_solver)
     amg, fphi, frhs, fres = (case[k] for k in ("amg", "fphi", "frhs", "fres"))
     if mode == "mixed":
         amg = mg.MixedMultiGrid(case["fac"], mg.SolverParams(
@@ -79,8 +80,8 @@ def single_box(n, levels, iters=2, mode="vcycle"):
     return norms, fphi.download(0)
 
 
-def check(out, n, levels, iters=2, mode="vcycle"):
-    norms, phi = single_box(n, levels, iters, mode)
+def check(out, n, levels, iters=2, mode="vcycle", bottom_solver=0):
+    norms, phi = single_box(n, levels, iters, mode, bottom_solver)
     for o in out:
         assert str(o["transport"]) == "ipc"
         assert bool(o["checked"])  # commcheck.check_transport passed on every rank
@@ -122,14 +123,36 @@ def test_eight_processes_bench_split_512_bitwise(tmp_path):
                       timeout=420), n, levels)
 
 
-def test_four_processes_mixed_fmg_bitwise(tmp_path):
+@pytest.mark.parametrize("agg", [0, 9])
+def test_four_processes_mixed_fmg_bitwise(tmp_path, agg):
     # BASELINE config C5's cycle between processes: the 4-level mixed fp32
     # smoother / fp64 residual FMG and two V-cycles at 128^3 on bench.py's
-    # 4-rank split (1 x 2 x 2), fp32 messages through the peer-mapped
-    # transport -- phi and every norm bit-identical to the single box (itself
-    # bit-identical to oracle/mixed.py: test_mixed.py)
+    # 4-rank split (1 x 2 x 2), deep halo (fp32 4-deep shells before every
+    # two-sweep launch), fp32 messages through the peer-mapped transport;
+    # agg 9: the coarsest depth (16 x 8 x 8 per rank) gathered onto rank 0,
+    # which alone relaxes it (the fp32 restriction gathered, the correction
+    # scattered) -- phi and every norm bit-identical to the single box
+    # (itself bit-identical to oracle/mixed.py: test_mixed.py)
     n, levels = 128, 4
-    check(run_workers(tmp_path, 4, n, levels, mode="mixed"), n, levels, mode="mixed")
+    check(run_workers(tmp_path, 4, n, levels, agglomerate_below=agg, mode="mixed"), n, levels,
+          mode="mixed")
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_bicgstab_bottom_on_rank0_bitwise(tmp_path, world):
+    # the reference's bottom solver (BiCGStab, Main_PoissonSolver.cpp:103-117)
+    # on the gathered coarsest depth: rank 0 alone runs it -- its dot products
+    # and norms reduce on rank 0 with no allreduce; the other ranks go from
+    # the gather straight to the scatter -- on bench.py's 4- and 8-rank
+    # splits at 128^3 (coarsest depth 32^3 on rank 0, bench.py's default
+    # placement).  The gathered box is the single box's coarsest box, so its
+    # reductions add the same partials in the same order: phi and every norm
+    # bit-identical to the single box
+    import bench
+    n, levels = 128, 3
+    agg = bench.agglomerate_default(world, n, levels)
+    check(run_workers(tmp_path, world, n, levels, agglomerate_below=agg, bottom_solver=1,
+                      timeout=300), n, levels, bottom_solver=1)
 
 
 def test_transport_check_single_rank():

@@ -8,7 +8,26 @@ with the exchange routed through RCCL self send/recv (the pack -> grouped
 ncclSend/ncclRecv -> unpack path the ranks use) or the peer-mapped
 transport.  It prints V-cycles/s; xGMI latency is not modelled.
 
-usage: rank_proxy.py [--size 256] [--transport rccl|ipc] [--deep 1] [--steps 30]
+--charge (round 5; the default for the 8-GPU share, a 256^3 box at three
+levels) adds what the one-box proxy cannot run, to give the per-rank time of
+`bench.py --gpus 8` as it is configured (the coarsest depth gathered onto
+rank 0, bench.agglomerate_default):
+  * the gathered bottom: the proxy relaxes its own 64^3 coarsest box (four
+    sweeps, shell exchanges with itself); the real run gathers the eight
+    64^3 boxes into one 128^3 box on rank 0, which relaxes it while the other
+    ranks wait, and scatters the correction back.  Charged: - t(4 sweeps on
+    the proxy's 64^3 depth) + t(4 sweeps on a 128^3 box, measured here) +
+    two exchange latencies (t of one 1-deep exchange of the 64^3 depth,
+    measured here);
+  * the xGMI byte floor: every exchange's largest per-link
+    message at 153 GB/s per link and direction (2 x 2 x 2 split: a rank's
+    faces, edges and corner go to 7 different peers, one link each), the
+    gather / scatter's 7 x 64^3 (+ faces) into / out of rank 0 included --
+    added on top of the measured exchanges (whose self messages already pay
+    the latency and a local copy of the same bytes), so an upper bound.
+`charged_ms_per_vcycle` is the result.
+
+usage: rank_proxy.py [--size 256] [--transport rccl|ipc] [--deep 1] [--steps 30] [--charge]
 """
 import argparse
 import json
@@ -37,6 +56,9 @@ def main():
                     help="split the box into this many boxes (all on this rank): the N-GPU "
                          "split's exchanges and gathers on one GPU")
     ap.add_argument("--agglomerate-below", type=int, default=0)
+    ap.add_argument("--charge", type=int, default=-1,
+                    help="charge the gathered bottom and the xGMI byte floor (1 on, 0 off; "
+                         "default on for the 8-GPU share: --size 256, 3 levels, one part)")
     ap.add_argument("--norm-type", type=int, default=-1,
                     help="per-iteration residual norm (bench.py takes 0, the stop test's max "
                          "norm; -1: none, the proxy's default since round 1)")
@@ -80,12 +102,77 @@ def main():
     comm.synchronize()
     dt = time.perf_counter() - t0
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
-    print(json.dumps({"size": n, "shape": shp, "parts": parts,
-                      "agglomerate_below": args.agglomerate_below, "deep": args.deep, "periodic": per,
-                      "norm_type": args.norm_type,
-                      "transport": "local" if args.local else args.transport,
-                      "vcycles_per_s": round(args.steps / dt, 2),
-                      "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}))
+    out = {"size": n, "shape": shp, "parts": parts,
+           "agglomerate_below": args.agglomerate_below, "deep": args.deep, "periodic": per,
+           "norm_type": args.norm_type,
+           "transport": "local" if args.local else args.transport,
+           "vcycles_per_s": round(args.steps / dt, 2),
+           "ms_per_vcycle": round(dt / args.steps * 1e3, 4), "final_residual": r}
+    charge = args.charge if args.charge >= 0 else int(
+        shp == (256, 256, 256) and args.levels == 3 and parts == (1, 1, 1)
+        and args.agglomerate_below == 0)
+    if charge:
+        out.update(charges(mg, comm, amg, prm, args, shp, dt / args.steps * 1e3))
+    print(json.dumps(out))
+
+
+def timed_ms(comm, fn, reps):
+    fn()
+    comm.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    comm.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def charges(mg, comm, amg, prm, args, shp, ms):
+    """The gathered bottom and the xGMI byte floor of the 8-GPU run (module
+    docstring), from measurements in this process."""
+    D = args.levels - 1
+    reps = 50
+    # the proxy's own coarsest depth: 4 sweeps (shell exchanges with itself)
+    # and one 1-deep exchange (the latency a gather / scatter pays)
+    op_c = amg.op(D)
+    e_c, r_c = amg.level_field(D, 0), amg.level_field(D, 1)
+    t_own = timed_ms(comm, lambda: op_c.relax(e_c, r_c, 4), reps)
+    t_x = timed_ms(comm, e_c.exchange, reps)
+    # the gathered box: the 8 ranks' coarsest boxes as one box on rank 0
+    # (2 x the side), bench's coefficients coarsened the same way, Dirichlet
+    side = [2 * (s >> D) for s in shp]
+    c1 = mg.Comm()
+    dom = (0, 0, 0, side[0] - 1, side[1] - 1, side[2] - 1)
+    g = mg.Grid(c1, dom, [dom], prm.L / side[0])
+    fa, fb, fr, fe = (mg.LevelData(g) for _ in range(4))
+    bh = prm.bh()
+    bh["domain_length"] = prm.L
+    mg.set_binary_bh_coefs(fa, fr, bh)
+    fb.set_val(1.0)
+    fe.set_zero()
+    op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, coefficient_average_type=1,
+                           prolong_type=1, relax_mode=1, fused_smoother=1)
+    op_g = mg.defineOperatorFactory(g, fa, fb, op).AMRnewOp()
+    t_gath = timed_ms(c1, lambda: op_g.relax(fe, fr, 4), reps)
+    # xGMI floor: per exchange the largest per-link message (a face) over
+    # 153 GB/s; per level of the 8-GPU split (box side s): e's 4-deep shell
+    # before each of the 3 pairs that do not start from zero and r's once
+    # (deep halo), plus two 1-deep face exchanges (level 0: phi for the
+    # residual, e for the restriction; level 1: e for the restriction and the
+    # coarse e for level 0's prolongation); the gather and the scatter move
+    # 7 coarsest boxes (+ their faces) over rank 0's 7 links
+    link = 153e9
+    s0 = shp[0]
+    floor_s = 0.0
+    for lev in range(D):
+        s = s0 >> lev
+        floor_s += 4 * s * s * 4 * 8 / link + 2 * s * s * 8 / link
+    sc = s0 >> D
+    floor_s += (sc ** 3 + (sc + 2) ** 3) * 8 / link
+    floor_ms = floor_s * 1e3
+    charged = ms - t_own + t_gath + 2 * t_x + floor_ms
+    return {"bottom_own_ms": round(t_own, 4), "bottom_gathered_ms": round(t_gath, 4),
+            "gather_scatter_latency_ms": round(2 * t_x, 4), "xgmi_floor_ms": round(floor_ms, 4),
+            "charged_ms_per_vcycle": round(charged, 4)}
 
 
 if __name__ == "__main__":
