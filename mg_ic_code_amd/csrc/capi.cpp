@@ -1,4 +1,9 @@
 // capi.cpp -- extern "C" boundary (include/mgic.h) over the C++ layer.
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -7,6 +12,25 @@
 #include "amr.hpp"
 #include "mixed.hpp"
 #include "op.hpp"
+
+// MGIC_ABORT_TRACE=1 (diagnostics): on SIGABRT, write the native call stack
+// (library offsets; resolve with addr2line -e libmgic.so) to stderr first
+namespace {
+void mgic_abort_trace(int sig) {
+  void *fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "mgic: SIGABRT, native stack:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+const int kAbortTrace = [] {
+  const char *e = getenv("MGIC_ABORT_TRACE");
+  if (e && atoi(e)) signal(SIGABRT, mgic_abort_trace);
+  return 0;
+}();
+}  // namespace
 
 using namespace mgic;
 

@@ -73,14 +73,14 @@ using IC = std::integral_constant<int, N>;
 //     reads a zero input makes redundant;
 //   kSkipOut: waves whose rows all lie outside the box skip every pass.
 constexpr bool kPF2 = true;
+#ifndef TB2_ACC_PFC
+#define TB2_ACC_PFC 1
+#endif
+#ifndef TB2_ACC_SB
+#define TB2_ACC_SB 0
+#endif
 constexpr bool kZinShort = true;
 constexpr bool kSkipOut = true;
-#ifndef TB2_SPREAD
-#define TB2_SPREAD 0
-#endif
-#ifndef TB2_DSTORE
-#define TB2_DSTORE 0
-#endif
 
 // Geometry.  Rows of the LDS ring are SHIFTED pairings: in row y of plane k
 // pair m holds cells (X, X+1) with X = x0 - 6 + 2m + s, s = (x0 + y + k +
@@ -371,10 +371,14 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   // plane p+1 while step p runs; PF 2: planes p+3 / p+2, one register set
   // per step parity)
   constexpr int PF = (kPF2 && !ACC) ? 2 : 1;
+  // (ACC: TB2_ACC_PFC 2 = rhs / aCoef two steps ahead as in the other
+  // launches, with acc loaded in the step that stores it: TB2_ACC_SB)
+  constexpr int PFC = ACC ? TB2_ACC_PFC : PF;
+  constexpr bool ASB = ACC && TB2_ACC_SB;
   // (SDY: the steady-state step, kSteady above)
   constexpr bool SDY = std::is_same<T, float>::value || ZIN || ACC;
   T pu0[PF][NL], pu1[PF][NL];
-  T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
+  T nr0[PFC][NP], nr1[PFC][NP], na0[PFC][NP], na1[PFC][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
   // later), black of planes p-1 .. p-4 (made one step later from rb / ab);
@@ -435,22 +439,18 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
       Bs[tid + i * NT] = pu1[b][i];
     }
   };
-  auto fetch_c = [&](int t, int p, auto bc, auto sd, int which = 3) {
+  auto fetch_c = [&](int t, int p, auto bc, auto sd) {
     constexpr int b = decltype(bc)::value;
     constexpr bool SD = decltype(sd)::value;
     const char *pr = SD ? plane_u(rhs, p) : plane(rhs, p), *pa = SD ? plane_u(a, p) : plane(a, p);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      if (which & 1) {
-        const V vr = at2(pr, roff[t][i]);
-        nr0[b][i] = vr.x;
-        nr1[b][i] = vr.y;
-      }
-      if (which & 2) {
-        const V va = at2(pa, roff[t][i]);
-        na0[b][i] = va.x;
-        na1[b][i] = va.y;
-      }
+      const V vr = at2(pr, roff[t][i]);
+      const V va = at2(pa, roff[t][i]);
+      nr0[b][i] = vr.x;
+      nr1[b][i] = vr.y;
+      na0[b][i] = va.x;
+      na1[b][i] = va.y;
     }
   };
   auto lam = [&](T aa) {  // .cpp:234-243 (a*alpha == alpha*a)
@@ -626,7 +626,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     constexpr int J = decltype(tc)::value, PT = J & 1, PU = PT ^ 1;
     constexpr int J0 = J, J3 = (J + 1) & 3;
     constexpr int FB = PF == 2 ? (J & 1) : 0;  // in-flight register set consumed / refilled
+    constexpr int FC = PFC == 2 ? (J & 1) : 0;
     using ICF = IC<FB>;
+    using ICC = IC<FC>;
     using SDC = decltype(sd);
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
     // coefficient sets: black of plane p-1 from the raw black element, red
@@ -636,21 +638,29 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
       Br[J0][i] = rb[i];
       Ba[J0][i] = FAST ? ab[i] : s.alpha * ab[i];
       Bl[J0][i] = lam(Ba[J0][i]);
-      Rr[J0][i] = reg_copy(nr0[FB][i]);
-      Ra[J0][i] = FAST ? reg_copy(na0[FB][i]) : s.alpha * na0[FB][i];
+      Rr[J0][i] = reg_copy(nr0[FC][i]);
+      Ra[J0][i] = FAST ? reg_copy(na0[FC][i]) : s.alpha * na0[FC][i];
       Rl[J0][i] = lam(Ra[J0][i]);
-      rb[i] = reg_copy(nr1[FB][i]);
-      ab[i] = reg_copy(na1[FB][i]);
+      rb[i] = reg_copy(nr1[FC][i]);
+      ab[i] = reg_copy(na1[FC][i]);
     }
     const int E0 = es(p);  // this step's slots derive from this one
     image(p + 1, ICF{}, SDC{});
     put(eadd(E0, 1), ICF{});
-    auto fc = [&](int which) {
-      if (PF == 2) fetch_c(PT, p + 2, ICF{}, SDC{}, which);
-      else fetch_c(PU, p + 1, ICF{}, SDC{}, which);
+    auto fc = [&] {
+      if (PFC == 2) fetch_c(PT, p + 2, ICC{}, SDC{});
+      else fetch_c(PU, p + 1, ICC{}, SDC{});
     };
     auto fa = [&] {
-      if constexpr (ACC) {
+      if constexpr (ASB) {  // plane p-4, stored at the end of this step
+        const char *pl = SDC::value ? plane_u(acc, p - 4) : plane(acc, p - 4);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const double2 v = at2(pl, roff[PT][i]);
+          ac0[i] = v.x;
+          ac1[i] = v.y;
+        }
+      } else if constexpr (ACC) {
         const char *pl = SDC::value ? plane_u(acc, p - 3) : plane(acc, p - 3);
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
@@ -666,45 +676,24 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
       if (PF == 2) fetch_u(PU, p + 3, ICF{}, SDC{});
       else fetch_u(PT, p + 2, ICF{}, SDC{});
     };
-    constexpr int SPR = TB2_SPREAD;
-    // TB2_SPREAD (measurement): 0 every load before the first barrier; 1 u
-    // there, rhs / aCoef between the red passes, acc in the black phase; 2 u
-    // after the first barrier, the rest as 1; 3 u before, rhs between the red
-    // passes, aCoef (and acc) between the black ones
-    // TB2_DSTORE (measurement): 0 plane p-4 stored at the end of step p; 1 / 2
-    // / 3 plane p-5 stored in step p (its slot is rewritten at step p+2):
-    // after sweep-1 red, right after the first barrier, right after the second
-    // (before acc's rotation, which the stored plane still uses)
-    constexpr int DST = TB2_DSTORE;
-    static_assert(DST == 0 || SPR != 0, "a delayed store needs the spread acc load");
-    auto dstore = [&] { store(PU, p - 5, eadd(E0, -5), SDC{}); };
-    // 4: rhs / aCoef between the red passes, u (and acc) between the black
-    // ones; 5: as 4 with aCoef and acc at the start of the black phase; 6:
-    // rhs / aCoef between the red passes, u and acc at the start of the black
-    // phase; 7: rhs / aCoef before the first barrier, u between the red passes
-    if (SPR == 0) { fc(3); fa(); fu(); }
-    if (SPR == 1 || SPR == 3) fu();
-    if (SPR == 7) fc(3);
+    // The step's global loads are issued in three places, not in one burst
+    // (round 5): u of plane p+3 here, rhs / aCoef of plane p+2 between the
+    // two red passes, acc at the start of the black phase.  All 16 waves of
+    // all CUs issuing every load of a step at once filled the memory
+    // pipeline's queues: the waves stalled at issue for most of the step's
+    // first phase, the colour passes queued behind them (DESIGN.md 3,
+    // "Spread load issue": 512^3 plain launch -4.5%, 256^3 -6%, V-cycle
+    // +2.5%; the stores and other placements measured no better).
+    fu();
     __syncthreads();
-    if (DST == 2) dstore();
-    if (SPR == 2) fu();
     pass(IC<(ZIN && kZinShort) ? 1 : 0>{}, SDC{}, true, 3, PT, p, E0, Rr[J0], Ra[J0], Rl[J0]);
-    if (DST == 1) dstore();
-    if (SPR == 1 || SPR == 2 || SPR == 4 || SPR == 6) fc(3);
-    if (SPR == 3 || SPR == 5) fc(1);
-    if (SPR == 7) fu();
+    fc();
     pass(IC<0>{}, SDC{}, true, 1, PU, p - 3, eadd(E0, -3), Rr[J3], Ra[J3], Rl[J3]);
     __syncthreads();
-    if (DST == 3) dstore();
-    if (SPR == 1 || SPR == 2 || SPR == 6 || SPR == 7) fa();
-    if (SPR == 5) { fc(2); fa(); }
-    if (SPR == 6) fu();
+    fa();
     pass(IC<(ZIN && kZinShort) ? 2 : 0>{}, SDC{}, false, 2, PU, p - 1, eadd(E0, -1), Br[J0], Ba[J0], Bl[J0]);
-    if (SPR == 3) { fc(2); fa(); }
-    if (SPR == 4) { fu(); fa(); }
-    if (SPR == 5) fu();
     pass(IC<0>{}, SDC{}, false, 0, PT, p - 4, eadd(E0, -4), Br[J3], Ba[J3], Bl[J3]);
-    if (DST == 0) store(PT, p - 4, eadd(E0, -4), SDC{});
+    store(PT, p - 4, eadd(E0, -4), SDC{});
   };
 
   fetch_u(1, pstart - 1, IC<0>{}, IC<0>{});
@@ -715,10 +704,8 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   put(es(pstart), IC<0>{});
   fetch_u(1, pstart + 1, IC<0>{}, IC<0>{});
   fetch_c(0, pstart, IC<0>{}, IC<0>{});
-  if (PF == 2) {
-    fetch_u(0, pstart + 2, IC<PF - 1>{}, IC<0>{});
-    fetch_c(1, pstart + 1, IC<PF - 1>{}, IC<0>{});
-  }
+  if (PF == 2) fetch_u(0, pstart + 2, IC<PF - 1>{}, IC<0>{});
+  if (PFC == 2) fetch_c(1, pstart + 1, IC<PFC - 1>{}, IC<0>{});
   // (up to three steps past pend: their passes and stores fall outside every
   // range test, their loads are clamped)
   // Steady 4-step groups (SDY): steps p .. p+3 with z0 + 5 <= p and
@@ -742,8 +729,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     for (; p < pstart + 8 && p <= pend; p += 4) group(IC<0>{}, p);
     for (; p <= ssh; p += 4) group(IC<1>{}, p);
   }
-  // (a delayed store takes one step more: plane z1 - 1 at step pend + 1)
-  for (; p <= pend + (TB2_DSTORE ? 1 : 0); p += 4) group(IC<0>{}, p);
+  for (; p <= pend; p += 4) group(IC<0>{}, p);
 }
 
 

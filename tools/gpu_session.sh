@@ -40,6 +40,10 @@ for s in ${STEPS_TO_RUN:-pytest_gpu smoke bench}; do
               --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29521 bench.py \
               --gpus 8 --steps "${BSTEPS:-20}" --warmup 2 --agglomerate-below 65 ${BENCH2_ARGS:-} || exit $? ;;
     proxy) run proxy 600 python tools/rank_proxy.py ${PROXY_ARGS:-} || exit $? ;;
+    c5) run c5 600 python tools/bench_c5.py --vcycles 4 || exit $? ;;
+    c5_8) run c5_8 900 env MGIC_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 \
+              --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29522 tools/bench_c5.py \
+              --vcycles 4 || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
