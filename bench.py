@@ -376,11 +376,19 @@ def bottom_timing(mg, case, args, timed, nt, gsrb_ms):
     amg.iterations(phi, frhs, res, max(1, args.warmup), norm_type=nt)
     el, hist = timed(lambda: amg.iterations(phi, frhs, res, args.steps, norm_type=nt))
     ms = el / args.steps * 1e3
+    # the bottom solves themselves (HIP events on the rank that runs them:
+    # rank 0 when the coarsest depth is gathered), in K more iterations
+    amg.bottom_timer(True)
+    amg.iterations(phi, frhs, res, args.steps, norm_type=nt)
+    solve_ms, solves = amg.bottom_ms()
+    amg.bottom_timer(False)
     out = {"solver": "BiCGStab (imax 80, eps 1e-6, restarts 5; preCond = lambda r + 2 GSRB)",
            "depth": args.levels - 1,
            "vcycles_per_s": round(args.steps / el, 4), "ms_per_vcycle": round(ms, 4),
            "gsrb_bottom_ms_per_vcycle": round(gsrb_ms * 1e3, 4),
            "bottom_delta_ms": round(ms - gsrb_ms * 1e3, 4),
+           "bottom_solve_ms_rank0": round(solve_ms / solves, 4) if solves else None,
+           "bottom_solves_timed_rank0": solves,
            "residual_norm_history": hist[-3:] if nt >= 0 else None}
     del amg, phi, res
     return out

@@ -289,6 +289,11 @@ MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs,
  * depth e = P e_coarse and `ncycles` V-cycles; phi += e; resid = rhs - L(phi) */
 MGIC_API int mgic_mg_fmg(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                          int norm_type, int homogeneous, int ncycles, double *norm);
+/* HIP events around every BiCGStab bottom solve this rank runs (bottom_solver
+ * 1; with a gathered coarsest depth only its owner runs them): on != 0 resets
+ * and starts recording; bottom_ms returns their total time and count */
+MGIC_API int mgic_mg_bottom_timer(mgic_mg mg, int on);
+MGIC_API int mgic_mg_bottom_ms(mgic_mg mg, double *ms, int *calls);
 
 /* Mixed precision (BASELINE config C5): the same V-cycle schedule with the
  * correction equation in fp32 (GSRB / restrictResidual / prolongIncrement in

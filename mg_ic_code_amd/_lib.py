@@ -167,6 +167,8 @@ SIGNATURES = {
     "mgic_mg_iterations": [H, H, H, H, c_int, c_int, c_int, PD],
     "mgic_mg_init_residual": [H, H, H, H, c_int, c_int, PD],
     "mgic_mg_precondition": [H, H, H, c_int],
+    "mgic_mg_bottom_timer": [H, c_int],
+    "mgic_mg_bottom_ms": [H, PD, PI],
     "mgic_mg_fmg": [H, H, H, H, c_int, c_int, c_int, PD],
     "mgic_grid_create_patches": [H, PI, PI, c_double, c_int, PI, PI, PH],
     "mgic_amr_create": [c_int, POINTER(H), POINTER(H), POINTER(H), POINTER(OpParams),
@@ -237,6 +239,15 @@ def _load() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
+    # torch (when installed) before the library: torch ships its own HIP
+    # runtime, loaded under another file name, and a process that loads
+    # libmgic.so first ends up with two HIP runtimes -- which fail at exit
+    # ("double free or corruption"); loaded second, libmgic.so binds to
+    # torch's by soname
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)  # AttributeError = missing export: fail loudly

@@ -608,6 +608,16 @@ class AMRMultiGrid:
              int(norm_type), int(bool(homogeneous)), ctypes.byref(out))
         return out.value
 
+    def bottom_timer(self, on: bool = True) -> None:
+        """Time every BiCGStab bottom solve this rank runs (HIP events)."""
+        call("mgic_mg_bottom_timer", self._h, int(bool(on)))
+
+    def bottom_ms(self) -> Tuple[float, int]:
+        """(total ms, solves) of the bottom solves timed since bottom_timer(True)."""
+        ms, n = ctypes.c_double(), ctypes.c_int()
+        call("mgic_mg_bottom_ms", self._h, ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value
+
     def fmg(self, phi: LevelData, rhs: LevelData, resid: LevelData, norm_type: int = 0,
             homogeneous: bool = False, ncycles: int = 1) -> float:
         """Full multigrid on the current resid (from init_residual/iteration):

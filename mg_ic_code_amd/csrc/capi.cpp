@@ -1,8 +1,4 @@
 // capi.cpp -- extern "C" boundary (include/mgic.h) over the C++ layer.
-#include <execinfo.h>
-#include <signal.h>
-#include <unistd.h>
-
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -12,25 +8,6 @@
 #include "amr.hpp"
 #include "mixed.hpp"
 #include "op.hpp"
-
-// MGIC_ABORT_TRACE=1 (diagnostics): on SIGABRT, write the native call stack
-// (library offsets; resolve with addr2line -e libmgic.so) to stderr first
-namespace {
-void mgic_abort_trace(int sig) {
-  void *fr[64];
-  const int n = backtrace(fr, 64);
-  const char msg[] = "mgic: SIGABRT, native stack:\n";
-  (void)!write(2, msg, sizeof(msg) - 1);
-  backtrace_symbols_fd(fr, n, 2);
-  signal(sig, SIG_DFL);
-  raise(sig);
-}
-const int kAbortTrace = [] {
-  const char *e = getenv("MGIC_ABORT_TRACE");
-  if (e && atoi(e)) signal(SIGABRT, mgic_abort_trace);
-  return 0;
-}();
-}  // namespace
 
 using namespace mgic;
 
@@ -1040,6 +1017,19 @@ MGIC_API int mgic_mg_init_residual(mgic_mg mg, mgic_field phi, mgic_field rhs, m
   });
 }
 
+MGIC_API int mgic_mg_bottom_timer(mgic_mg mg, int on) {
+  return guard([&] {
+    NEED(mg);
+    mg->amg.mg.bottom_timer(on != 0);
+  });
+}
+MGIC_API int mgic_mg_bottom_ms(mgic_mg mg, double *ms, int *calls) {
+  return guard([&] {
+    NEED(mg);
+    NEED(ms);
+    *ms = mg->amg.mg.bottom_ms(calls);
+  });
+}
 MGIC_API int mgic_mg_fmg(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                          int norm_type, int h, int ncycles, double *norm) {
   return guard([&] {

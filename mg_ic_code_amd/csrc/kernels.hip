@@ -559,8 +559,6 @@ __global__ __launch_bounds__(RB) void k_reduce_partial(const double *__restrict_
 // results), and the partial sums use k_reduce_partial's row-to-wave deal and
 // accumulators, so a fused norm equals the separate one bit for bit.
 // s = r + ca*v; e = e + cb*pt; partials of the norm kind KIND of s
-// (dev != nullptr: the coefficients -a, a from the device BiCGStab state, a =
-// alpha or omega by `which`; nothing is done once the solve has ended)
 template <int KIND>
 __global__ __launch_bounds__(RB) void k_axpy2_reduce(double *__restrict__ s,
                                                      const double *__restrict__ r,
@@ -568,15 +566,7 @@ __global__ __launch_bounds__(RB) void k_axpy2_reduce(double *__restrict__ s,
                                                      double *__restrict__ e,
                                                      const double *__restrict__ pt, double cb,
                                                      const BoxArgs g,
-                                                     double *__restrict__ partials,
-                                                     const BicgDev *__restrict__ dev = nullptr,
-                                                     int which = 0) {
-  if (dev) {
-    if (dev->done) return;  // (uniform)
-    const double a = which ? dev->omega : dev->alpha;
-    ca = -a;
-    cb = a;
-  }
+                                                     double *__restrict__ partials) {
   __shared__ double sm[RB];
   constexpr int W = RB / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -652,75 +642,18 @@ __global__ __launch_bounds__(RB) void k_dot2(const double *__restrict__ t,
 }
 
 // p = ((p * beta) + c * v) + 1.0 * r  (scale(P, beta); incr(P, V, c); incr(P, R, 1))
-// (dev != nullptr: beta and c = -beta * omega from the device BiCGStab
-// state, P = R (assignLocal) on its first iteration, nothing once it has ended)
 __global__ __launch_bounds__(256) void k_bicg_p(double *__restrict__ p,
                                                 const double *__restrict__ v,
                                                 const double *__restrict__ r, double beta,
-                                                double c, const BoxArgs g,
-                                                const BicgDev *__restrict__ dev = nullptr) {
+                                                double c, const BoxArgs g) {
   const int i = blockIdx.x * TX + threadIdx.x;
   const int j = blockIdx.y * TY + threadIdx.y;
   const int k = blockIdx.z;
   if (i >= g.nx || j >= g.ny) return;
   const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
-  if (dev) {
-    if (dev->done) return;
-    if (dev->init) {
-      p[idx] = r[idx];
-      return;
-    }
-    beta = dev->beta;
-    c = -dev->beta * dev->omega;  // (the host's -beta * omega)
-  }
   double t = p[idx] * beta;
   t = t + c * v[idx];
   p[idx] = t + 1.0 * r[idx];
-}
-
-// One step of BiCGStabSolver::solve's scalar control flow (op.cpp; the same
-// expressions as the host loop there), one thread
-__global__ void k_bicg_step(BicgDev *__restrict__ d, const double *__restrict__ res,
-                            const BicgPrm p, int step) {
-  if (threadIdx.x != 0 || d->done) return;
-  const double tol = p.eps * d->init_norm;
-  switch (step) {
-    case kBicgTop:  // while (it < imax && nrm > eps * init_norm && nrm > reps) { ++it; rho2 = rho1
-      if (d->it < p.imax && d->nrm > tol && d->nrm > p.reps) {
-        d->it += 1;
-        d->rho2 = d->rho1;
-      } else {
-        d->done = 1;
-      }
-      break;
-    case kBicgRho:  // rho1 = dot(RT, R); if (rho1 == 0) break; beta = (rho1 / rho2) * (alpha / omega)
-      d->rho1 = res[0];
-      if (d->rho1 == 0.0) d->done = 1;
-      else if (!d->init) d->beta = (d->rho1 / d->rho2) * (d->alpha / d->omega);
-      break;
-    case kBicgM: {  // (P was assigned: init = false); m = dot(RT, V)
-      d->init = 0;
-      const double m = res[0];
-      if (fabs(m) > p.small * fabs(d->rho1)) d->alpha = d->rho1 / m;
-      else d->done = d->restarts >= p.num_restarts ? 1 : 2;  // break, or restart (host)
-      break;
-    }
-    case kBicgS: {  // nrm = norm(S); if (nrm <= eps * init_norm || nrm <= reps) break
-      const double x = res[0];
-      d->nrm = p.norm_kind == 2 ? sqrt(x) : x;
-      if (d->nrm <= tol || d->nrm <= p.reps) d->done = 1;
-      break;
-    }
-    case kBicgW:  // (ts, tt) = (T.S, T.T); if (tt == 0) break; omega = ts / tt
-      if (res[1] == 0.0) d->done = 1;
-      else d->omega = res[0] / res[1];
-      break;
-    default: {  // kBicgR: nrm = norm(R); if (omega == 0) break
-      const double x = res[0];
-      d->nrm = p.norm_kind == 2 ? sqrt(x) : x;
-      if (d->omega == 0.0) d->done = 1;
-    }
-  }
 }
 
 template <int KIND>
@@ -1424,33 +1357,6 @@ void bicg_p(double *p, const double *v, const double *r, double beta, double c, 
   check_launch();
 }
 
-void bicg_step(BicgDev *d, const double *res, const BicgPrm &p, BicgStep step, hipStream_t st) {
-  k_bicg_step<<<1, 64, 0, st>>>(d, res, p, (int)step);
-  check_launch();
-}
-
-void bicg_p_dev(double *p, const double *v, const double *r, const BicgDev *d, const BoxArgs &g,
-                hipStream_t st) {
-  if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  k_bicg_p<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(p, v, r, 0.0, 0.0, g, d);
-  check_launch();
-}
-
-int axpy2_reduce_dev(int kind, double *s, const double *r, const double *v, double *e,
-                     const double *pt, const BicgDev *d, int which, const BoxArgs &g,
-                     double *partials, hipStream_t st) {
-  if ((long)g.nx * g.ny * g.nz <= 0) return 0;
-  const long nb = reduce_blocks(g);
-  const dim3 grid((unsigned)nb), block(RB);
-  switch (kind) {
-    case 1: k_axpy2_reduce<1><<<grid, block, 0, st>>>(s, r, v, 0.0, e, pt, 0.0, g, partials, d, which); break;
-    case 2: k_axpy2_reduce<2><<<grid, block, 0, st>>>(s, r, v, 0.0, e, pt, 0.0, g, partials, d, which); break;
-    case 3: k_axpy2_reduce<3><<<grid, block, 0, st>>>(s, r, v, 0.0, e, pt, 0.0, g, partials, d, which); break;
-    default: throw Error(kBadArg, "axpy2_reduce: bad kind");
-  }
-  check_launch();
-  return (int)nb;
-}
 
 // Blocks per item (grid.y = item): sized for the largest item at
 // copy_ept() elements per thread, so the many small items (edges, corners of

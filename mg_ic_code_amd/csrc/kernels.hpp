@@ -139,32 +139,6 @@ int dot2_partial(const double *t, const double *s, const BoxArgs &g, double *pts
 void bicg_p(double *p, const double *v, const double *r, double beta, double c, const BoxArgs &g,
             hipStream_t st);
 
-// ---- BiCGStab with its control flow on the device (BiCGStabSolver::solve,
-// op.cpp): the scalars and the branch state live in device memory; a
-// one-thread step kernel after each reduction does the host loop's scalar
-// arithmetic and tests (same expressions, same order: the same bits), and
-// the vector updates that write persistent vectors (P, S / R and E) run only
-// while the solve is live.  done: 0 live, 1 finished (a break or the loop
-// test), 2 a restart is due (the host does it between batches).
-struct BicgDev {
-  double rho1, rho2, alpha, beta, omega, nrm, init_norm;
-  int it, restarts, init, done;
-};
-struct BicgPrm {
-  double eps, reps, small;
-  int imax, num_restarts, norm_kind;  // norm_kind: reduction kind of norm(., normType)
-};
-enum BicgStep { kBicgTop, kBicgRho, kBicgM, kBicgS, kBicgW, kBicgR };
-// res: the reductions' result slots (Comm::d_result)
-void bicg_step(BicgDev *d, const double *res, const BicgPrm &p, BicgStep step, hipStream_t st);
-// p = init ? r : ((p*beta) + (-beta*omega)*v) + r, while the solve is live
-void bicg_p_dev(double *p, const double *v, const double *r, const BicgDev *d, const BoxArgs &g,
-                hipStream_t st);
-// s = r - a*v; e = e + a*pt (a = alpha, or omega when which = 1) and the
-// partials of `kind` of s, while the solve is live (else nothing is written)
-int axpy2_reduce_dev(int kind, double *s, const double *r, const double *v, double *e,
-                     const double *pt, const BicgDev *d, int which, const BoxArgs &g,
-                     double *partials, hipStream_t st);
 // batched rectangular copies (exchange / copyTo / pack / unpack)
 void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *const *src_tab,
                 const double *src_buf, double *const *dst_tab, double *dst_buf,

@@ -804,50 +804,6 @@ void VariableCoeffPoissonOperator::dot2(const LevelData &t, const LevelData &s, 
   tt = c.h_result()[1];
 }
 
-void VariableCoeffPoissonOperator::reduceQueue(int kind, const LevelData &x, const LevelData *y,
-                                               int slot) {
-  Comm &c = *grid->comm;
-  const hipStream_t st = stream();
-  double *parts = c.d_partials(std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox);
-  int total = 0;
-  for (int n = 0; n < grid->nlocal(); ++n)
-    total += kern::reduce_partial(kind, x.p[n], y ? y->p[n] : nullptr, args_plain_[n], parts + total, st);
-  finish_reduce(kind, parts, total, slot, false);
-}
-
-void VariableCoeffPoissonOperator::dot2Queue(const LevelData &t, const LevelData &s) {
-  Comm &c = *grid->comm;
-  const hipStream_t st = stream();
-  const int cap = std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox;
-  double *parts = c.d_partials(2 * cap);
-  int total = 0;
-  for (int n = 0; n < grid->nlocal(); ++n)
-    total += kern::dot2_partial(t.p[n], s.p[n], args_plain_[n], parts + total, parts + cap + total, st);
-  finish_reduce(0, parts, total, 0, false);
-  finish_reduce(0, parts + cap, total, 1, false);
-}
-
-void VariableCoeffPoissonOperator::axpy2NormQueue(LevelData &s, const LevelData &r,
-                                                  const LevelData &v, LevelData &e,
-                                                  const LevelData &pt, const kern::BicgDev *d,
-                                                  int which, int ord) {
-  Comm &c = *grid->comm;
-  const hipStream_t st = stream();
-  const int kind = norm_kind(ord);
-  double *parts = c.d_partials(std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox);
-  int total = 0;
-  for (int n = 0; n < grid->nlocal(); ++n)
-    total += kern::axpy2_reduce_dev(kind, s.p[n], r.p[n], v.p[n], e.p[n], pt.p[n], d, which,
-                                    args_plain_[n], parts + total, st);
-  finish_reduce(kind, parts, total, 0, false);
-}
-
-void VariableCoeffPoissonOperator::bicgPDev(LevelData &p, const LevelData &v, const LevelData &r,
-                                            const kern::BicgDev *d) {
-  for (int n = 0; n < grid->nlocal(); ++n)
-    kern::bicg_p_dev(p.p[n], v.p[n], r.p[n], d, args_plain_[n], stream());
-}
-
 double VariableCoeffPoissonOperator::dotProduct(const LevelData &x, const LevelData &y) {
   return reduce(0, x, &y);
 }
@@ -915,126 +871,8 @@ std::unique_ptr<VariableCoeffPoissonOperator> VariableCoeffPoissonOperatorFactor
 }
 
 // --------------------------------------------------------------- BiCGStab
-BiCGStabSolver::~BiCGStabSolver() {
-  if (d_state_) (void)hipFree(d_state_);
-  if (h_state_) (void)hipHostFree(h_state_);
-}
-
 int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
                           bool hom) {
-  const char *e = getenv("MGIC_BICG_DEVICE");
-  return (e && atoi(e) == 0) ? solve_host(op, phi, rhs, hom) : solve_device(op, phi, rhs, hom);
-}
-
-// The loop of solve_host with its scalars and branches on the device
-// (kern::BicgDev, k_bicg_step): per iteration the same launches in the same
-// order -- reductions leave their results in the Comm's result slots, a
-// one-thread step kernel does what the host does with them -- plus the
-// preconditioner and operator applications, which also run in an iteration
-// after the solve has ended (their outputs are temporaries nothing reads
-// then).  The host reads the state back once per batch of iterations, sized
-// from the convergence rate so far; restarts (rare) are done on the host
-// between batches.  No host wait per dot product: on one GPU a bottom solve's
-// iterations otherwise each wait for five readbacks.
-int BiCGStabSolver::solve_device(VariableCoeffPoissonOperator &op, LevelData &phi,
-                                 const LevelData &rhs, bool hom) {
-  auto &tv = temps_[op.grid.get()];
-  if (tv.empty())
-    for (int i = 0; i < 9; ++i) tv.push_back(op.create());
-  LevelData &R = *tv[0], &RT = *tv[1], &E = *tv[2], &P = *tv[3], &PT = *tv[4], &S = *tv[5],
-            &ST = *tv[6], &T = *tv[7], &V = *tv[8];
-  const int nt = prm.normType;
-  const hipStream_t st = op.stream();
-  Comm &c = *op.grid->comm;
-  if (!d_state_) {
-    MGIC_HIP(hipMalloc(&d_state_, sizeof(kern::BicgDev)));
-    MGIC_HIP(hipHostMalloc(&h_state_, sizeof(kern::BicgDev), hipHostMallocDefault));
-  }
-  op.residual(R, phi, rhs, hom);
-  op.assignLocal(RT, R);
-  op.setToZero(E);
-  op.setToZero(PT);
-  op.setToZero(ST);
-  op.setToZero(P);
-  op.setToZero(V);
-  const double init_norm = op.norm(R, nt);
-  kern::BicgDev &h = *h_state_;
-  h = kern::BicgDev{};
-  h.nrm = init_norm;
-  h.init_norm = init_norm;
-  h.init = 1;
-  kern::BicgPrm bp;
-  bp.eps = prm.eps;
-  bp.reps = prm.reps;
-  bp.small = prm.small;
-  bp.imax = prm.imax;
-  bp.num_restarts = prm.numRestarts;
-  bp.norm_kind = nt == 0 ? 3 : nt == 1 ? 1 : 2;
-  auto upload = [&] {
-    MGIC_HIP(hipMemcpyAsync(d_state_, h_state_, sizeof(kern::BicgDev), hipMemcpyHostToDevice, st));
-  };
-  upload();
-  const double *res = c.d_result();
-  const double target = std::max(prm.eps * init_norm, prm.reps);
-  int batch = 2, prev_it = 0;
-  double prev_nrm = init_norm;
-  for (;;) {
-    for (int b = 0; b < batch; ++b) {
-      kern::bicg_step(d_state_, res, bp, kern::kBicgTop, st);
-      op.reduceQueue(0, RT, &R, 0);  // rho1 = dot(RT, R)
-      kern::bicg_step(d_state_, res, bp, kern::kBicgRho, st);
-      op.bicgPDev(P, V, R, d_state_);  // P = R, or P = beta P - beta omega V + R
-      if (precond) precond(PT, P);
-      else op.preCond(PT, P);
-      op.applyOp(V, PT, true);
-      op.reduceQueue(0, RT, &V, 0);  // m = dot(RT, V)
-      kern::bicg_step(d_state_, res, bp, kern::kBicgM, st);
-      op.axpy2NormQueue(S, R, V, E, PT, d_state_, 0, nt);  // S = R - alpha V; E += alpha PT
-      kern::bicg_step(d_state_, res, bp, kern::kBicgS, st);
-      if (precond) precond(ST, S);
-      else op.preCond(ST, S);
-      op.applyOp(T, ST, true);
-      op.dot2Queue(T, S);
-      kern::bicg_step(d_state_, res, bp, kern::kBicgW, st);
-      op.axpy2NormQueue(R, S, T, E, ST, d_state_, 1, nt);  // R = S - omega T; E += omega ST
-      kern::bicg_step(d_state_, res, bp, kern::kBicgR, st);
-    }
-    MGIC_HIP(hipMemcpyAsync(h_state_, d_state_, sizeof(kern::BicgDev), hipMemcpyDeviceToHost, st));
-    MGIC_HIP(hipStreamSynchronize(st));
-    if (h.done == 2) {  // restart (solve_host's else branch; its limit was checked on the device)
-      h.restarts += 1;
-      op.incr(phi, E, 1.0);
-      op.residual(R, phi, rhs, hom);
-      op.assignLocal(RT, R);
-      op.setToZero(E);
-      h.nrm = op.norm(R, nt);
-      h.init = 1;
-      h.done = 0;
-      upload();
-      prev_it = h.it;
-      prev_nrm = h.nrm;
-      batch = 2;
-      continue;
-    }
-    if (h.done) break;
-    // the next batch: the iterations the mean rate so far needs to reach
-    // the tolerance (at least one, at most 16 and imax)
-    int need = 4;
-    if (h.it > prev_it && prev_nrm > 0.0 && h.nrm > 0.0 && h.nrm < prev_nrm) {
-      const double rate = std::pow(h.nrm / prev_nrm, 1.0 / (h.it - prev_it));
-      if (rate > 0.0 && rate < 1.0) need = (int)std::ceil(std::log(target / h.nrm) / std::log(rate));
-    }
-    batch = std::max(1, std::min(std::min(need, 16), prm.imax - h.it));
-    prev_it = h.it;
-    prev_nrm = h.nrm;
-  }
-  op.incr(phi, E, 1.0);
-  last_iters = h.it;
-  return h.it;
-}
-
-int BiCGStabSolver::solve_host(VariableCoeffPoissonOperator &op, LevelData &phi,
-                               const LevelData &rhs, bool hom) {
   auto &tv = temps_[op.grid.get()];
   if (tv.empty())
     for (int i = 0; i < 9; ++i) tv.push_back(op.create());
@@ -1193,6 +1031,43 @@ void MultiGrid::define(VariableCoeffPoissonOperatorFactory &factory, const MGPar
   MGIC_HIP(hipStreamSynchronize(levels_[0].op->stream()));
 }
 
+MultiGrid::~MultiGrid() {
+  for (hipEvent_t ev : bt_ev_) (void)hipEventDestroy(ev);
+}
+
+void MultiGrid::bottom_timer(bool on) {
+  bt_on_ = on;
+  bt_used_ = 0;
+}
+
+double MultiGrid::bottom_ms(int *calls) {
+  double tot = 0.0;
+  if (bt_used_) MGIC_HIP(hipEventSynchronize(bt_ev_[bt_used_ - 1]));
+  for (size_t i = 0; i + 1 < bt_used_; i += 2) {
+    float ms = 0.f;
+    MGIC_HIP(hipEventElapsedTime(&ms, bt_ev_[i], bt_ev_[i + 1]));
+    tot += ms;
+  }
+  if (calls) *calls = (int)(bt_used_ / 2);
+  return tot;
+}
+
+// the bottom BiCGStab (Main_PoissonSolver.cpp:103-117), between events when
+// the bottom timer is on
+void MultiGrid::bottom_solve(VariableCoeffPoissonOperator &op, LevelData &e, LevelData &r) {
+  auto mark = [&] {
+    if (bt_used_ == bt_ev_.size()) {
+      hipEvent_t ev;
+      MGIC_HIP(hipEventCreate(&ev));
+      bt_ev_.push_back(ev);
+    }
+    MGIC_HIP(hipEventRecord(bt_ev_[bt_used_++], op.stream()));
+  };
+  if (bt_on_) mark();
+  bottom.solve(op, e, r, true);
+  if (bt_on_) mark();
+}
+
 void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
                       bool halo_out, const std::function<void()> *before_phi) {
   VariableCoeffPoissonOperator &op = *levels_[d].op;
@@ -1208,7 +1083,7 @@ void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData 
   if (d == (int)levels_.size() - 1) {  // bottom
     if (prm.bottom_solver == 1) {
       if (e_zero) op.setToZero(e);
-      bottom.solve(op, e, r, true);
+      bottom_solve(op, e, r);
       if (halo_out) e.exchange(st);
     } else if (e_zero) {
       op.relaxFromZero(e, r, prm.n_bottom, rf | out);
@@ -1272,7 +1147,7 @@ void MultiGrid::fmg(LevelData &e0, LevelData &r0, LevelData &phi, int ncycles) {
     VariableCoeffPoissonOperator &op = *levels_[D - 1].op;
     if (prm.bottom_solver == 1) {
       op.setToZero(E(D - 1));
-      bottom.solve(op, E(D - 1), Rr(D - 1), true);
+      bottom_solve(op, E(D - 1), Rr(D - 1));
     } else {
       op.relaxFromZero(E(D - 1), Rr(D - 1), prm.n_bottom);
     }

@@ -116,15 +116,6 @@ class VariableCoeffPoissonOperator {
   void bicgP(LevelData &p, const LevelData &v, const LevelData &r, double beta, double c);
   // dot(t, s) and dot(t, t) in one pass
   void dot2(const LevelData &t, const LevelData &s, double &ts, double &tt);
-  // the same reductions queued, results left on the device in the Comm's
-  // result slots (d_result()[slot]; dot2: slots 0 and 1) -- no host wait --
-  // and the fused updates with their coefficients from a device BiCGStab state
-  // (kern::BicgDev): BiCGStabSolver's device loop
-  void reduceQueue(int kind, const LevelData &x, const LevelData *y, int slot);
-  void dot2Queue(const LevelData &t, const LevelData &s);
-  void axpy2NormQueue(LevelData &s, const LevelData &r, const LevelData &v, LevelData &e,
-                      const LevelData &pt, const kern::BicgDev *d, int which, int ord);
-  void bicgPDev(LevelData &p, const LevelData &v, const LevelData &r, const kern::BicgDev *d);
 
   // state (public as in the reference: m_aCoef, m_bCoef, m_lambda)
   std::shared_ptr<Grid> grid;
@@ -251,18 +242,9 @@ class BiCGStabSolver {
   std::function<void(LevelData &, const LevelData &)> precond;
   int solve(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
             bool homogeneous);
-  ~BiCGStabSolver();
 
  private:
   std::map<const Grid *, std::vector<std::unique_ptr<LevelData>>> temps_;
-  // the loop on the host (a host wait per reduction) or on the device
-  // (MGIC_BICG_DEVICE, default 1): the same launches and arithmetic, the
-  // scalars and branches in device memory, read back once per batch of
-  // iterations; bit-identical (test_gpu_parity.py)
-  int solve_host(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs, bool hom);
-  int solve_device(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
-                   bool hom);
-  kern::BicgDev *d_state_ = nullptr, *h_state_ = nullptr;
 };
 
 struct MGParams {
@@ -319,6 +301,12 @@ class MultiGrid {
   CopyPlan &scatter_plan(int d) { return *levels_[d].prolong_plan; }
   MGParams prm;
   BiCGStabSolver bottom;
+  // HIP events around every BiCGStab bottom solve this rank runs (on: reset
+  // and start recording); bottom_ms: their total time and count (waits for
+  // the last one)
+  void bottom_timer(bool on);
+  double bottom_ms(int *calls);
+  ~MultiGrid();
 
  private:
   struct Level {
@@ -334,6 +322,10 @@ class MultiGrid {
   void cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,
              bool halo_out = false, const std::function<void()> *before_phi = nullptr);
   std::vector<Level> levels_;
+  bool bt_on_ = false;
+  size_t bt_used_ = 0;
+  std::vector<hipEvent_t> bt_ev_;
+  void bottom_solve(VariableCoeffPoissonOperator &op, LevelData &e, LevelData &r);
 };
 
 // [Chombo] AMRMultiGrid on a single AMR level: iterations of

@@ -73,12 +73,6 @@ using IC = std::integral_constant<int, N>;
 //     reads a zero input makes redundant;
 //   kSkipOut: waves whose rows all lie outside the box skip every pass.
 constexpr bool kPF2 = true;
-#ifndef TB2_ACC_PFC
-#define TB2_ACC_PFC 1
-#endif
-#ifndef TB2_ACC_SB
-#define TB2_ACC_SB 0
-#endif
 constexpr bool kZinShort = true;
 constexpr bool kSkipOut = true;
 
@@ -371,14 +365,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   // plane p+1 while step p runs; PF 2: planes p+3 / p+2, one register set
   // per step parity)
   constexpr int PF = (kPF2 && !ACC) ? 2 : 1;
-  // (ACC: TB2_ACC_PFC 2 = rhs / aCoef two steps ahead as in the other
-  // launches, with acc loaded in the step that stores it: TB2_ACC_SB)
-  constexpr int PFC = ACC ? TB2_ACC_PFC : PF;
-  constexpr bool ASB = ACC && TB2_ACC_SB;
   // (SDY: the steady-state step, kSteady above)
   constexpr bool SDY = std::is_same<T, float>::value || ZIN || ACC;
   T pu0[PF][NL], pu1[PF][NL];
-  T nr0[PFC][NP], nr1[PFC][NP], na0[PFC][NP], na1[PFC][NP];
+  T nr0[PF][NP], nr1[PF][NP], na0[PF][NP], na1[PF][NP];
   // coefficient sets (rhs, alpha*a, lambda): red of planes p .. p-3 (made
   // when the plane's pair arrives, last used by sweep-2 red three steps
   // later), black of planes p-1 .. p-4 (made one step later from rb / ab);
@@ -626,9 +616,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     constexpr int J = decltype(tc)::value, PT = J & 1, PU = PT ^ 1;
     constexpr int J0 = J, J3 = (J + 1) & 3;
     constexpr int FB = PF == 2 ? (J & 1) : 0;  // in-flight register set consumed / refilled
-    constexpr int FC = PFC == 2 ? (J & 1) : 0;
     using ICF = IC<FB>;
-    using ICC = IC<FC>;
     using SDC = decltype(sd);
     asm volatile("" : "+s"(p));  // opaque: plane-derived values are recomputed, not kept live
     // coefficient sets: black of plane p-1 from the raw black element, red
@@ -638,29 +626,21 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
       Br[J0][i] = rb[i];
       Ba[J0][i] = FAST ? ab[i] : s.alpha * ab[i];
       Bl[J0][i] = lam(Ba[J0][i]);
-      Rr[J0][i] = reg_copy(nr0[FC][i]);
-      Ra[J0][i] = FAST ? reg_copy(na0[FC][i]) : s.alpha * na0[FC][i];
+      Rr[J0][i] = reg_copy(nr0[FB][i]);
+      Ra[J0][i] = FAST ? reg_copy(na0[FB][i]) : s.alpha * na0[FB][i];
       Rl[J0][i] = lam(Ra[J0][i]);
-      rb[i] = reg_copy(nr1[FC][i]);
-      ab[i] = reg_copy(na1[FC][i]);
+      rb[i] = reg_copy(nr1[FB][i]);
+      ab[i] = reg_copy(na1[FB][i]);
     }
     const int E0 = es(p);  // this step's slots derive from this one
     image(p + 1, ICF{}, SDC{});
     put(eadd(E0, 1), ICF{});
     auto fc = [&] {
-      if (PFC == 2) fetch_c(PT, p + 2, ICC{}, SDC{});
-      else fetch_c(PU, p + 1, ICC{}, SDC{});
+      if (PF == 2) fetch_c(PT, p + 2, ICF{}, SDC{});
+      else fetch_c(PU, p + 1, ICF{}, SDC{});
     };
     auto fa = [&] {
-      if constexpr (ASB) {  // plane p-4, stored at the end of this step
-        const char *pl = SDC::value ? plane_u(acc, p - 4) : plane(acc, p - 4);
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-          const double2 v = at2(pl, roff[PT][i]);
-          ac0[i] = v.x;
-          ac1[i] = v.y;
-        }
-      } else if constexpr (ACC) {
+      if constexpr (ACC) {
         const char *pl = SDC::value ? plane_u(acc, p - 3) : plane(acc, p - 3);
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
@@ -704,8 +684,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   put(es(pstart), IC<0>{});
   fetch_u(1, pstart + 1, IC<0>{}, IC<0>{});
   fetch_c(0, pstart, IC<0>{}, IC<0>{});
-  if (PF == 2) fetch_u(0, pstart + 2, IC<PF - 1>{}, IC<0>{});
-  if (PFC == 2) fetch_c(1, pstart + 1, IC<PFC - 1>{}, IC<0>{});
+  if (PF == 2) {
+    fetch_u(0, pstart + 2, IC<PF - 1>{}, IC<0>{});
+    fetch_c(1, pstart + 1, IC<PF - 1>{}, IC<0>{});
+  }
   // (up to three steps past pend: their passes and stores fall outside every
   // range test, their loads are clamped)
   // Steady 4-step groups (SDY): steps p .. p+3 with z0 + 5 <= p and

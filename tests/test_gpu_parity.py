@@ -369,34 +369,6 @@ def test_bicgstab_bottom_within_tolerance(comm, rng):
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
 
 
-@pytest.mark.parametrize("parts,agg,nt", [((1, 1, 1), 0, 2), ((2, 2, 2), 16, 2), ((2, 1, 2), 0, 0)])
-def test_bicgstab_device_loop_matches_host_loop(comm, parts, agg, nt, monkeypatch):
-    # BiCGStabSolver's loop with its scalars and branches on the device
-    # (kern::BicgDev, MGIC_BICG_DEVICE=1, the default) against the host loop
-    # (a host wait per reduction): the bottom solver of three V-cycles (a
-    # distributed and a gathered coarsest depth) and the MG-preconditioned
-    # outer solve, phi, every norm and the iteration counts bit for bit
-    out = []
-    for dev in ("0", "1"):
-        monkeypatch.setenv("MGIC_BICG_DEVICE", dev)
-        S = build_pair(comm, np.random.default_rng(5), 32, parts, nlevels=4, bottom=1,
-                       agglomerate_below=agg)
-        amg = S["amg"]
-        hist = [amg.init_residual(S["fphi"], S["frhs"], S["fres"], 0)]
-        hist += [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(3)]
-        phi_v = download_global(S["fphi"], S["grid"], (32,) * 3)
-        S["fphi"].set_zero()
-        solver = mg.BiCGStabSolver(mg.MultilevelLinearOp(amg, 2), tolerance=1e-10,
-                                   max_iterations=60, norm_type=nt)
-        it = solver.solve(S["fphi"], S["frhs"])
-        out.append((hist, phi_v, it, solver.final_norm,
-                    download_global(S["fphi"], S["grid"], (32,) * 3)))
-    (h0, p0, i0, f0, q0), (h1, p1, i1, f1, q1) = out
-    assert h0 == h1 and np.array_equal(p0, p1)
-    assert i0 == i1 and f0 == f1 and np.array_equal(q0, q1)
-    assert h1[-1] < 1e-3 * h1[0]
-
-
 def test_agglomerated_hierarchy_matches_single_box(comm, rng):
     n = 32
     S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16)

@@ -81,6 +81,11 @@ def main():
     ap.add_argument("--no-fmg", action="store_true")
     ap.add_argument("--transport", default="auto", choices=("auto", "ipc", "rccl"))
     args = ap.parse_args()
+    # torch before the library: torch brings its own HIP runtime, and a
+    # process that loads libmgic.so first ends up with two runtimes, which
+    # fails at exit ("double free or corruption"); bench.py and the tests do
+    # the same
+    import torch  # noqa: F401
     import mg_ic_code_amd as mg
     from mg_ic_code_amd.params import read_params_file
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -93,7 +98,6 @@ def main():
     import bench
     if world > 1:
         import datetime
-        import torch
         import torch.distributed as dist
         dev = int(os.environ.get("MGIC_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
         torch.cuda.set_device(dev)
