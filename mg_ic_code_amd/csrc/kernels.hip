@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void k_residual_z2(RT *__restrict__ r,
   }
 }
 
-// one coarse cell of restrictResidual (k_restrict, k_restrict_t)
+// one coarse cell of restrictResidual
 template <class T, bool BC, int NT>
 __device__ __forceinline__ void restrict_cell(T *__restrict__ rc, const BoxArgs &cg,
                                               const T *__restrict__ u, const T *__restrict__ rhs,
@@ -367,35 +367,6 @@ __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxA
   const int cj = blockIdx.y * TY + threadIdx.y;
   if (ci >= cg.nx || cj >= cg.ny) return;
   restrict_cell<T, BC, NT>(rc, cg, u, rhs, a, b, fg, s, accumulate, ci, cj, blockIdx.z);
-}
-
-// The restriction on a larger tile: WX waves side by side in x (64 * WX
-// coarse columns) and 4 / WX in y, each thread visiting RY coarse rows and
-// KC coarse planes, so that the fine rows a tile shares with its neighbours
-// (its x-edge lines, y-halo rows and z-halo planes) are a smaller share of
-// what it fetches.  Per cell the same restrict_cell as k_restrict.
-template <class T, bool BC, int NT, int WX, int RY, int KC>
-__global__ __launch_bounds__(256) void k_restrict_t(T *__restrict__ rc, const BoxArgs cg,
-                                                    const T *__restrict__ u,
-                                                    const T *__restrict__ rhs,
-                                                    const T *__restrict__ a,
-                                                    const T *__restrict__ b, const BoxArgs fg,
-                                                    const StencilCoefs s64, int accumulate) {
-  constexpr int WY = 4 / WX;
-  const SC<T> s(s64);
-  const int wx = threadIdx.y % WX, wy = threadIdx.y / WX;
-  const int ci = (blockIdx.x * WX + wx) * TX + threadIdx.x;
-  if (ci >= cg.nx) return;
-#pragma unroll 1
-  for (int kk = 0; kk < KC; ++kk) {
-    const int ck = blockIdx.z * KC + kk;
-    if (ck >= cg.nz) break;
-#pragma unroll 1
-    for (int r = 0; r < RY; ++r) {
-      const int cj = (blockIdx.y * RY + r) * WY + wy;
-      if (cj < cg.ny) restrict_cell<T, BC, NT>(rc, cg, u, rhs, a, b, fg, s, accumulate, ci, cj, ck);
-    }
-  }
 }
 
 struct ProlongArgs {
@@ -1248,36 +1219,6 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
   // MGIC_RESTRICT_NT bit 0: non-temporal rhs / aCoef / bCoef loads, for
   // every bCoef kind (the same switch in restrict_residual_f)
   const int accu = accumulate ? 1 : 0;
-  static const int tile = [] {  // (measurement) MGIC_RESTRICT_TILE = WX*100 + RY*10 + KC
-    const char *e = getenv("MGIC_RESTRICT_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  if (tile > 0 && (nt & 1)) {
-#define MGIC_RT(WX, RY, KC)                                                                    \
-  case WX * 100 + RY * 10 + KC: {                                                              \
-    const dim3 gt((unsigned)((cg.nx + 64 * WX - 1) / (64 * WX)),                               \
-                  (unsigned)((cg.ny + RY * (4 / WX) - 1) / (RY * (4 / WX))),                   \
-                  (unsigned)((cg.nz + KC - 1) / KC));                                          \
-    if (s.bconst)                                                                              \
-      k_restrict_t<double, true, 1, WX, RY, KC><<<gt, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu); \
-    else                                                                                       \
-      k_restrict_t<double, false, 1, WX, RY, KC><<<gt, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu); \
-    check_launch();                                                                            \
-    return;                                                                                    \
-  }
-    switch (tile) {
-      MGIC_RT(1, 1, 1)
-      MGIC_RT(1, 4, 1)
-      MGIC_RT(1, 4, 4)
-      MGIC_RT(2, 4, 2)
-      MGIC_RT(2, 8, 1)
-      MGIC_RT(4, 2, 4)
-      MGIC_RT(4, 4, 1)
-      MGIC_RT(4, 8, 2)
-      default: throw Error(kBadArg, "MGIC_RESTRICT_TILE: no such tile");
-    }
-#undef MGIC_RT
-  }
   const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
   if (s.bconst && (nt & 1))
     k_restrict<double, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);

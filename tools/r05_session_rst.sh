@@ -2,7 +2,8 @@
 # round-5 GPU session rst: restriction tiles (MGIC_RESTRICT_TILE = WX RY KC,
 # k_restrict_t) against the per-cell grid (0): parity subset per tile, three
 # interleaved rounds of tools/bench_kernels.py at 512^3 and 256^3, FETCH_SIZE
-# of each tile's 512^3 launch, the V-cycle for the candidates.  Measurement only.
+# of each tile's 512^3 launch, the V-cycle for the candidates.  Measurement only
+# (k_restrict_t and its switch were removed after this A/B: profiles/r05g_restrict_tiles.txt).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/rst
