@@ -36,23 +36,13 @@ __device__ __forceinline__ void st_word(unsigned long long *p, unsigned long lon
 }
 
 // bounded poll of *w >= v; false on timeout (recorded in *err) or when an
-// earlier timeout of this rank is already recorded (fail fast, never hang).
-// A wait that has run for kBackoffTicks (20 us of the 100 MHz wall clock;
-// an exchange's messages land well within it) polls every ~3 us instead of
-// every 64 clocks: the ranks parked in a gathered depth's scatter while rank 0
-// runs the bottom solve (milliseconds) then stop loading the fabric with
-// system-scope polls.
-#ifndef MGIC_IPC_BACKOFF
-#define MGIC_IPC_BACKOFF 1
-#endif
-constexpr unsigned long long kBackoffTicks = 2000;
+// earlier timeout of this rank is already recorded (fail fast, never hang)
 __device__ bool ipc_wait(const unsigned long long *w, unsigned long long v,
                          unsigned long long *err, unsigned long long timeout) {
   if (ld_sys(w) >= v) return true;
   const unsigned long long t0 = wall_clock64();
   for (;;) {
-    if (MGIC_IPC_BACKOFF && wall_clock64() - t0 > kBackoffTicks) __builtin_amdgcn_s_sleep(127);
-    else __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(1);
     if (ld_sys(w) >= v) return true;
     if (ld_sys(err) != 0) return false;
     if (wall_clock64() - t0 > timeout) {
