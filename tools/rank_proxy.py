@@ -27,6 +27,14 @@ rank 0, bench.agglomerate_default):
     the latency and a local copy of the same bytes), so an upper bound.
 `charged_ms_per_vcycle` is the result.
 
+--parts 2,2,2 --size 512 --periodic 0,0,0 --agglomerate-below 65 (round 5) runs
+the whole 8-GPU split on this GPU instead -- the eight 256^3 boxes of
+bench.py's decomposition, every box-to-box message through the transport's
+put / get kernels, the coarsest depth gathered into one 128^3 box -- and
+reports one rank's share of it (split_share below): the exchanged faces,
+edges and corners of each box are exactly the real split's, not a periodic
+box's six faces.
+
 usage: rank_proxy.py [--size 256] [--transport rccl|ipc] [--deep 1] [--steps 30] [--charge]
 """
 import argparse
@@ -113,7 +121,61 @@ def main():
         and args.agglomerate_below == 0)
     if charge:
         out.update(charges(mg, comm, amg, prm, args, shp, dt / args.steps * 1e3))
+    P = parts[0] * parts[1] * parts[2]
+    if P > 1 and args.agglomerate_below > 0 and not any(per):
+        out.update(split_share(mg, prm, args, shp, parts, dt / args.steps * 1e3))
     print(json.dumps(out))
+
+
+def gathered_bottom_ms(mg, prm, side, reps=50):
+    """4 sweeps on one box of `side` cells (the gathered coarsest depth on
+    rank 0; bench's coefficients, Dirichlet)"""
+    c1 = mg.Comm()
+    dom = (0, 0, 0, side[0] - 1, side[1] - 1, side[2] - 1)
+    g = mg.Grid(c1, dom, [dom], prm.L / side[0])
+    fa, fb, fr, fe = (mg.LevelData(g) for _ in range(4))
+    bh = prm.bh()
+    bh["domain_length"] = prm.L
+    mg.set_binary_bh_coefs(fa, fr, bh)
+    fb.set_val(1.0)
+    fe.set_zero()
+    op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, coefficient_average_type=1,
+                           prolong_type=1, relax_mode=1, fused_smoother=1)
+    op_g = mg.defineOperatorFactory(g, fa, fb, op).AMRnewOp()
+    return timed_ms(c1, lambda: op_g.relax(fe, fr, 4), reps)
+
+
+def xgmi_floor_ms(s0, D, link=153e9):
+    """every exchange's largest per-link message (one face of the rank's box
+    of side s0 >> level) at `link` B/s, per V-cycle of D + 1 depths (charges()
+    below), plus the gather / scatter of 7 coarsest boxes over rank 0's links"""
+    floor_s = 0.0
+    for lev in range(D):
+        s = s0 >> lev
+        floor_s += 4 * s * s * 4 * 8 / link + 2 * s * s * 8 / link
+    sc = s0 >> D
+    floor_s += (sc ** 3 + (sc + 2) ** 3) * 8 / link
+    return floor_s * 1e3
+
+
+def split_share(mg, prm, args, shp, parts, ms):
+    """One rank's share of the N-GPU run from the whole split on this GPU
+    (round 5): the N boxes of bench.py's decomposition on one rank, every
+    box-to-box message through the transport's put / get kernels (self
+    messages), the coarsest depth gathered into one box as bench.py does.
+    Each rank's own work is 1/N of what this GPU ran, except the gathered
+    bottom, which rank 0 runs while the others wait: share = (t - t_bottom) / N
+    + t_bottom; `share_charged_ms` adds the xGMI byte floor (an upper bound:
+    the local copies of the same bytes are already in t)."""
+    P = parts[0] * parts[1] * parts[2]
+    D = args.levels - 1
+    side = [s >> D for s in shp]
+    t_b = gathered_bottom_ms(mg, prm, side)
+    share = (ms - t_b) / P + t_b
+    floor = xgmi_floor_ms(shp[0] // parts[0], D)
+    return {"split_boxes": P, "gathered_bottom_ms": round(t_b, 4),
+            "share_ms_per_vcycle": round(share, 4), "xgmi_floor_ms": round(floor, 4),
+            "share_charged_ms_per_vcycle": round(share + floor, 4)}
 
 
 def timed_ms(comm, fn, reps):
@@ -138,37 +200,16 @@ def charges(mg, comm, amg, prm, args, shp, ms):
     t_own = timed_ms(comm, lambda: op_c.relax(e_c, r_c, 4), reps)
     t_x = timed_ms(comm, e_c.exchange, reps)
     # the gathered box: the 8 ranks' coarsest boxes as one box on rank 0
-    # (2 x the side), bench's coefficients coarsened the same way, Dirichlet
-    side = [2 * (s >> D) for s in shp]
-    c1 = mg.Comm()
-    dom = (0, 0, 0, side[0] - 1, side[1] - 1, side[2] - 1)
-    g = mg.Grid(c1, dom, [dom], prm.L / side[0])
-    fa, fb, fr, fe = (mg.LevelData(g) for _ in range(4))
-    bh = prm.bh()
-    bh["domain_length"] = prm.L
-    mg.set_binary_bh_coefs(fa, fr, bh)
-    fb.set_val(1.0)
-    fe.set_zero()
-    op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, coefficient_average_type=1,
-                           prolong_type=1, relax_mode=1, fused_smoother=1)
-    op_g = mg.defineOperatorFactory(g, fa, fb, op).AMRnewOp()
-    t_gath = timed_ms(c1, lambda: op_g.relax(fe, fr, 4), reps)
-    # xGMI floor: per exchange the largest per-link message (a face) over
+    # (2 x the side), bench's coefficients coarsened the same way, Dirichlet;
+    # the xGMI floor: per exchange the largest per-link message (a face) over
     # 153 GB/s; per level of the 8-GPU split (box side s): e's 4-deep shell
     # before each of the 3 pairs that do not start from zero and r's once
     # (deep halo), plus two 1-deep face exchanges (level 0: phi for the
     # residual, e for the restriction; level 1: e for the restriction and the
     # coarse e for level 0's prolongation); the gather and the scatter move
     # 7 coarsest boxes (+ their faces) over rank 0's 7 links
-    link = 153e9
-    s0 = shp[0]
-    floor_s = 0.0
-    for lev in range(D):
-        s = s0 >> lev
-        floor_s += 4 * s * s * 4 * 8 / link + 2 * s * s * 8 / link
-    sc = s0 >> D
-    floor_s += (sc ** 3 + (sc + 2) ** 3) * 8 / link
-    floor_ms = floor_s * 1e3
+    t_gath = gathered_bottom_ms(mg, prm, [2 * (s >> D) for s in shp], reps)
+    floor_ms = xgmi_floor_ms(shp[0], D)
     charged = ms - t_own + t_gath + 2 * t_x + floor_ms
     return {"bottom_own_ms": round(t_own, 4), "bottom_gathered_ms": round(t_gath, 4),
             "gather_scatter_latency_ms": round(2 * t_x, 4), "xgmi_floor_ms": round(floor_ms, 4),
