@@ -505,6 +505,7 @@ __global__ __launch_bounds__(256) void k_blas(double *__restrict__ x, const doub
   else if constexpr (KIND == 2) x[idx] = x[idx] * s;           // scale (FArrayBox::mult(scale))
   else if constexpr (KIND == 3) x[idx] = x[idx] * y[idx];      // mult (FArrayBox::mult(src))
   else if constexpr (KIND == 4) x[idx] = s * y[idx] + t * z[idx];  // axby
+  else if constexpr (KIND == 6) x[idx] = y[idx] * z[idx];      // copy y, then mult by z (one pass)
   else x[idx] = s;                                             // setVal
 }
 
@@ -1290,6 +1291,7 @@ void blas(int kind, double *x, const double *y, const double *z, double s, doubl
     case 3: k_blas<3><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
     case 4: k_blas<4><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
     case 5: k_blas<5><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
+    case 6: k_blas<6><<<grid, kBlock, 0, st>>>(x, y, z, s, t, g); break;
     default: throw Error(kBadArg, "blas: bad kind");
   }
   check_launch();

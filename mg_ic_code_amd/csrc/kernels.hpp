@@ -89,7 +89,7 @@ void average(double *c, const BoxArgs &cg, const double *f, const BoxArgs &fg, i
 void fill_bc(double *u, const BoxArgs &g, hipStream_t st);
 
 // BLAS-1 over the valid region: kind 0 x=y, 1 x=x+s*y, 2 x=x*s, 3 x=x*y,
-// 4 x = s*y + t*z, 5 x = s (setVal)
+// 4 x = s*y + t*z, 5 x = s (setVal), 6 x = y*z (copy, then mult)
 void blas(int kind, double *x, const double *y, const double *z, double s, double t,
           const BoxArgs &g, hipStream_t st);
 // Deterministic reductions: kind 0 dot(x,y), 1 sum|x|, 2 sum x^2, 3 max|x|,

@@ -208,10 +208,10 @@ unsigned long long VariableCoeffPoissonOperator::residualNormQueue(LevelData &lh
 void VariableCoeffPoissonOperator::preCond(LevelData &cor, const LevelData &res) {
   resetLambda();  // .cpp:90
   const hipStream_t st = stream();
-  for (int n = 0; n < grid->nlocal(); ++n) {
-    kern::blas(0, cor.p[n], res.p[n], nullptr, 0.0, 0.0, args_plain_[n], st);            // :99
-    kern::blas(3, cor.p[n], m_lambda->p[n], nullptr, 0.0, 0.0, args_plain_[n], st);      // :100
-  }
+  // cor = res (:99), then cor *= lambda (:100), as one pass: res * lambda is
+  // the same product (IEEE multiplication commutes)
+  for (int n = 0; n < grid->nlocal(); ++n)
+    kern::blas(6, cor.p[n], res.p[n], m_lambda->p[n], 0.0, 0.0, args_plain_[n], st);
   relax(cor, res, 2);  // :103
 }
 
@@ -808,6 +808,48 @@ double VariableCoeffPoissonOperator::dotProduct(const LevelData &x, const LevelD
   return reduce(0, x, &y);
 }
 
+unsigned long long VariableCoeffPoissonOperator::dotProductQueue(const LevelData &x,
+                                                                 const LevelData &y, int slot) {
+  Comm &c = *grid->comm;
+  double *parts = c.d_partials(std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox);
+  int total = 0;
+  for (int n = 0; n < grid->nlocal(); ++n)
+    total += kern::reduce_partial(0, x.p[n], y.p[n], args_plain_[n], parts + total, stream());
+  finish_reduce(0, parts, total, slot);
+  return c.last_ticket();
+}
+
+unsigned long long VariableCoeffPoissonOperator::axpy2NormQueue(LevelData &s, const LevelData &r,
+                                                                const LevelData &v, double ca,
+                                                                LevelData &e, const LevelData &pt,
+                                                                double cb, int ord, int slot) {
+  Comm &c = *grid->comm;
+  double *parts = c.d_partials(std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox);
+  int total = 0;
+  for (int n = 0; n < grid->nlocal(); ++n)
+    total += kern::axpy2_reduce(norm_kind(ord), s.p[n], r.p[n], v.p[n], ca, e.p[n], pt.p[n], cb,
+                                args_plain_[n], parts + total, stream());
+  finish_reduce(norm_kind(ord), parts, total, slot);
+  return c.last_ticket();
+}
+
+unsigned long long VariableCoeffPoissonOperator::dot2Queue(const LevelData &t, const LevelData &s) {
+  Comm &c = *grid->comm;
+  const int cap = std::max(1, grid->nlocal()) * kern::kMaxPartsPerBox;
+  double *parts = c.d_partials(2 * cap);
+  int total = 0;
+  for (int n = 0; n < grid->nlocal(); ++n)
+    total += kern::dot2_partial(t.p[n], s.p[n], args_plain_[n], parts + total, parts + cap + total,
+                                stream());
+  finish_reduce(0, parts, total, 0, false);
+  finish_reduce(0, parts + cap, total, 1, true);
+  return c.last_ticket();
+}
+
+double VariableCoeffPoissonOperator::result(int slot) const {
+  return grid->comm->h_result()[slot];
+}
+
 double VariableCoeffPoissonOperator::norm(const LevelData &x, int ord) {
   if (ord == 0) return reduce(3, x, nullptr);
   if (ord == 1) return reduce(1, x, nullptr);
@@ -891,10 +933,29 @@ int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, cons
   double nrm = init_norm;
   int it = 0, restarts = 0;
   bool init = true;
+  // With op.preCond (the bottom solver) the host waits three times per
+  // iteration instead of five: the second half-step's preconditioner,
+  // applyOp and dot2 are queued behind the first half-step's norm, and the
+  // next iteration's <RT, R> behind the second's, each pair read back at
+  // once.  The queued work only writes temporaries (ST, T) or nothing, so an
+  // iteration that stops on the norm discards it and every value is the
+  // unpipelined loop's.  Slots: 2 = the norms, 0 / 1 = the dots.
+  // (MGIC_BICG_PIPE=0: the unpipelined loop, read per solve; the parity test
+  // compares the two bit for bit)
+  const char *pe = getenv("MGIC_BICG_PIPE");
+  const bool pipe = !precond && !(pe && atoi(pe) == 0);
+  auto norm_of = [&](int slot) {
+    const double x = op.result(slot);
+    return nt == 1 || nt == 0 ? x : std::sqrt(x);
+  };
+  auto wait = [&](unsigned long long ticket) { op.grid->comm->wait_results(op.stream(), ticket); };
+  bool have_rho = false;  // the next rho1, read back with the last norm (pipelined)
+  double rho_next = 0.0;
   while (it < prm.imax && nrm > prm.eps * init_norm && nrm > prm.reps) {
     ++it;
     rho2 = rho1;
-    rho1 = op.dotProduct(RT, R);
+    rho1 = have_rho ? rho_next : op.dotProduct(RT, R);
+    have_rho = false;
     if (rho1 == 0.0) break;
     if (init) {
       op.assignLocal(P, R);
@@ -909,17 +970,37 @@ int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, cons
     const double m = op.dotProduct(RT, V);
     if (std::fabs(m) > prm.small * std::fabs(rho1)) {
       alpha = rho1 / m;
-      nrm = op.axpy2Norm(S, R, V, -alpha, E, PT, alpha, nt);  // S = R - alpha V; E += alpha PT
-      if (nrm <= prm.eps * init_norm || nrm <= prm.reps) break;
-      if (precond) precond(ST, S);
-      else op.preCond(ST, S);
-      op.applyOp(T, ST, true);
       double ts = 0.0, tt = 0.0;
-      op.dot2(T, S, ts, tt);
+      if (pipe) {
+        op.axpy2NormQueue(S, R, V, -alpha, E, PT, alpha, nt, 2);  // S = R - alpha V; E += alpha PT
+        op.preCond(ST, S);
+        op.applyOp(T, ST, true);
+        wait(op.dot2Queue(T, S));
+        nrm = norm_of(2);
+        if (nrm <= prm.eps * init_norm || nrm <= prm.reps) break;
+        ts = op.result(0);
+        tt = op.result(1);
+      } else {
+        nrm = op.axpy2Norm(S, R, V, -alpha, E, PT, alpha, nt);  // S = R - alpha V; E += alpha PT
+        if (nrm <= prm.eps * init_norm || nrm <= prm.reps) break;
+        if (precond) precond(ST, S);
+        else op.preCond(ST, S);
+        op.applyOp(T, ST, true);
+        op.dot2(T, S, ts, tt);
+      }
       if (tt == 0.0) break;
       omega = ts / tt;
-      nrm = op.axpy2Norm(R, S, T, -omega, E, ST, omega, nt);  // R = S - omega T; E += omega ST
-      if (omega == 0.0) break;
+      if (pipe) {
+        op.axpy2NormQueue(R, S, T, -omega, E, ST, omega, nt, 2);  // R = S - omega T; E += omega ST
+        wait(op.dotProductQueue(RT, R, 0));  // <RT, R> of the next iteration
+        nrm = norm_of(2);
+        rho_next = op.result(0);
+        have_rho = true;
+        if (omega == 0.0) break;
+      } else {
+        nrm = op.axpy2Norm(R, S, T, -omega, E, ST, omega, nt);  // R = S - omega T; E += omega ST
+        if (omega == 0.0) break;
+      }
     } else {
       if (restarts >= prm.numRestarts) break;
       ++restarts;

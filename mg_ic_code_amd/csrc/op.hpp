@@ -116,6 +116,15 @@ class VariableCoeffPoissonOperator {
   void bicgP(LevelData &p, const LevelData &v, const LevelData &r, double beta, double c);
   // dot(t, s) and dot(t, t) in one pass
   void dot2(const LevelData &t, const LevelData &s, double &ts, double &tt);
+  // the same reductions queued: each publishes into result slot `slot` (dot2:
+  // slots 0 and 1) and returns the ticket of its readback; result(slot) reads
+  // it once Comm::wait_results has seen that ticket (the BiCGStab loop waits
+  // once for several queued reductions)
+  unsigned long long dotProductQueue(const LevelData &x, const LevelData &y, int slot);
+  unsigned long long axpy2NormQueue(LevelData &s, const LevelData &r, const LevelData &v, double ca,
+                                    LevelData &e, const LevelData &pt, double cb, int ord, int slot);
+  unsigned long long dot2Queue(const LevelData &t, const LevelData &s);
+  double result(int slot) const;
 
   // state (public as in the reference: m_aCoef, m_bCoef, m_lambda)
   std::shared_ptr<Grid> grid;

@@ -369,6 +369,24 @@ def test_bicgstab_bottom_within_tolerance(comm, rng):
     assert np.linalg.norm(g - c) <= 1e-10 * np.linalg.norm(c)
 
 
+def test_bicgstab_bottom_pipelined_readbacks_bitwise(comm, rng, monkeypatch):
+    """The bottom BiCGStab reads back three times per iteration (the second
+    half-step and the next <RT, R> queued behind the norms, op.cpp
+    BiCGStabSolver::solve): phi and every residual norm equal the loop with
+    five readbacks (MGIC_BICG_PIPE=0) bit for bit."""
+    n = 32
+    runs = []
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("MGIC_BICG_PIPE", pipe)
+        S = build_pair(comm, np.random.default_rng(7), n, (1, 1, 1), nlevels=3, bottom=1)  # BiCGStab at 8^3
+        amg = S["amg"]
+        amg.init_residual(S["fphi"], S["frhs"], S["fres"])
+        norms = [amg.iteration(S["fphi"], S["frhs"], S["fres"], 0) for _ in range(3)]
+        runs.append((norms, download_global(S["fphi"], S["grid"], (n,) * 3)))
+    assert runs[0][0] == runs[1][0]
+    assert np.array_equal(runs[0][1], runs[1][1])
+
+
 def test_agglomerated_hierarchy_matches_single_box(comm, rng):
     n = 32
     S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16)
