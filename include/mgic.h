@@ -122,6 +122,9 @@ MGIC_API int mgic_comm_destroy(mgic_comm c);
 MGIC_API int mgic_comm_set_stream(mgic_comm c, void *hip_stream); /* NULL: own stream */
 MGIC_API int mgic_comm_get_stream(mgic_comm c, void **hip_stream);
 MGIC_API int mgic_comm_set_self_messages(mgic_comm c, int on);
+/* exchanges with messages (peer-mapped or RCCL) issued on this communicator so far:
+   a measurement counter (tools/rank_proxy.py charges per-exchange latency with it) */
+MGIC_API int mgic_comm_exchanges(mgic_comm c, unsigned long long *count);
 MGIC_API int mgic_comm_synchronize(mgic_comm c); /* + raises a transport timeout */
 MGIC_API int mgic_comm_rank(mgic_comm c, int *rank, int *size, int *uses_rccl);
 

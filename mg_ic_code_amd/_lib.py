@@ -96,6 +96,7 @@ SIGNATURES = {
     "mgic_comm_set_stream": [H, c_void_p],
     "mgic_comm_get_stream": [H, PH],
     "mgic_comm_set_self_messages": [H, c_int],
+    "mgic_comm_exchanges": [H, ctypes.POINTER(ctypes.c_ulonglong)],
     "mgic_comm_synchronize": [H],
     "mgic_comm_rank": [H, PI, PI, PI],
     "mgic_grid_create": [H, PI, PI, c_double, c_int, PI, PI, PH],

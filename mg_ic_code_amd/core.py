@@ -160,6 +160,14 @@ class Comm:
         call("mgic_comm_set_self_messages", self._h, int(bool(on)))
 
     @property
+    def exchanges(self) -> int:
+        """Exchanges with messages issued on this communicator so far (a
+        measurement counter)."""
+        n = ctypes.c_ulonglong()
+        call("mgic_comm_exchanges", self._h, ctypes.byref(n))
+        return n.value
+
+    @property
     def uses_rccl(self) -> bool:
         u = ctypes.c_int()
         call("mgic_comm_rank", self._h, None, None, ctypes.byref(u))

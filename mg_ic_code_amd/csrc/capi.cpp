@@ -299,6 +299,13 @@ MGIC_API int mgic_comm_set_self_messages(mgic_comm c, int on) {
     c->c->set_self_messages(on != 0);
   });
 }
+MGIC_API int mgic_comm_exchanges(mgic_comm c, unsigned long long *count) {
+  return guard([&] {
+    NEED(c);
+    NEED(count);
+    *count = c->c->exchanges();
+  });
+}
 MGIC_API int mgic_comm_synchronize(mgic_comm c) {
   return guard([&] {
     NEED(c);

@@ -714,6 +714,7 @@ void CopyPlan::execute_ipc(Comm &comm, T *const *src_tab, T *const *dst_tab, hip
 void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_tab,
                        hipStream_t st) {
   const bool remote = send_total_ || recv_total_;
+  if (remote) comm.count_exchange();
   if (remote && comm.uses_ipc()) {  // local copies included: one launch
     execute_ipc<double>(comm, src_tab, dst_tab, st);
     return;
@@ -741,6 +742,7 @@ void CopyPlan::execute(Comm &comm, double *const *src_tab, double *const *dst_ta
 void CopyPlan::execute_f(Comm &comm, float *const *src_tab, float *const *dst_tab,
                          hipStream_t st) {
   const bool remote = send_total_ || recv_total_;
+  if (remote) comm.count_exchange();
   if (remote && comm.uses_ipc()) {  // local copies included: one launch
     execute_ipc<float>(comm, src_tab, dst_tab, st);
     return;

@@ -55,6 +55,9 @@ class Comm {
   // path on one GPU)
   bool self_messages() const { return self_messages_; }
   void set_self_messages(bool v) { self_messages_ = v; }
+  // exchanges with messages issued so far (CopyPlan::execute*, a measurement counter)
+  unsigned long long exchanges() const { return exchanges_; }
+  void count_exchange() { ++exchanges_; }
   ncclComm_t nccl() const { return nccl_; }
   hipStream_t stream() const { return stream_; }
   void set_stream(hipStream_t s) { stream_ = s; }
@@ -129,6 +132,7 @@ class Comm {
   unsigned long long *h_seq_ = nullptr;
   unsigned long long pub_count_ = 0;
   void alloc_host_block();
+  unsigned long long exchanges_ = 0;
   bool ipc_ = false;
   int grid_cap_ = 0;
   long block_elems_ = kern::kIpcBlockElemsDefault;

@@ -105,10 +105,12 @@ def main():
     amg.init_residual(fphi, frhs, fres, norm_type=0)
     amg.iterations(fphi, frhs, fres, args.warmup, norm_type=args.norm_type)
     comm.synchronize()
+    x0 = comm.exchanges
     t0 = time.perf_counter()
     amg.iterations(fphi, frhs, fres, args.steps, norm_type=args.norm_type)
     comm.synchronize()
     dt = time.perf_counter() - t0
+    n_x = (comm.exchanges - x0) / args.steps  # exchanges with messages per V-cycle
     r = amg.init_residual(fphi, frhs, fres, norm_type=0)
     out = {"size": n, "shape": shp, "parts": parts,
            "agglomerate_below": args.agglomerate_below, "deep": args.deep, "periodic": per,
@@ -123,7 +125,7 @@ def main():
         out.update(charges(mg, comm, amg, prm, args, shp, dt / args.steps * 1e3))
     P = parts[0] * parts[1] * parts[2]
     if P > 1 and args.agglomerate_below > 0 and not any(per):
-        out.update(split_share(mg, prm, args, shp, parts, dt / args.steps * 1e3))
+        out.update(split_share(mg, comm, amg, prm, args, shp, parts, dt / args.steps * 1e3, n_x))
     print(json.dumps(out))
 
 
@@ -158,22 +160,33 @@ def xgmi_floor_ms(s0, D, link=153e9):
     return floor_s * 1e3
 
 
-def split_share(mg, prm, args, shp, parts, ms):
+def split_share(mg, comm, amg, prm, args, shp, parts, ms, n_x):
     """One rank's share of the N-GPU run from the whole split on this GPU
     (round 5): the N boxes of bench.py's decomposition on one rank, every
     box-to-box message through the transport's put / get kernels (self
     messages), the coarsest depth gathered into one box as bench.py does.
-    Each rank's own work is 1/N of what this GPU ran, except the gathered
-    bottom, which rank 0 runs while the others wait: share = (t - t_bottom) / N
-    + t_bottom; `share_charged_ms` adds the xGMI byte floor (an upper bound:
-    the local copies of the same bytes are already in t)."""
+    Each rank's own work is 1/N of what this GPU ran, except
+      * the gathered bottom, which rank 0 runs while the others wait;
+      * the exchanges' fixed cost: one launch here moves all N boxes'
+        messages, where every rank pays its own launch and hand-off, so each
+        of the n_x exchanges per V-cycle is charged (1 - 1/N) x t_x more,
+        t_x = one 1-deep exchange of the split's coarsest distributed depth
+        (small messages: mostly that fixed cost);
+    share = (t - t_bottom) / N + t_bottom + n_x (1 - 1/N) t_x, and
+    `share_charged_ms` adds the xGMI byte floor (an upper bound: the local
+    copies of the same bytes are already in t)."""
     P = parts[0] * parts[1] * parts[2]
     D = args.levels - 1
     side = [s >> D for s in shp]
     t_b = gathered_bottom_ms(mg, prm, side)
-    share = (ms - t_b) / P + t_b
+    e_d = amg.level_field(D - 1, 0)
+    t_x = timed_ms(comm, e_d.exchange, 50)
+    lat = n_x * (1.0 - 1.0 / P) * t_x
+    share = (ms - t_b) / P + t_b + lat
     floor = xgmi_floor_ms(shp[0] // parts[0], D)
     return {"split_boxes": P, "gathered_bottom_ms": round(t_b, 4),
+            "exchanges_per_vcycle": round(n_x, 2), "exchange_fixed_ms": round(t_x, 4),
+            "exchange_latency_charge_ms": round(lat, 4),
             "share_ms_per_vcycle": round(share, 4), "xgmi_floor_ms": round(floor, 4),
             "share_charged_ms_per_vcycle": round(share + floor, 4)}
 
