@@ -727,33 +727,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   using F = TB2<TX, TY, NT>;
   __shared__ T RB[F::RING];  // per ring slot: the red element of every pair, then the black
   const int L = sweep::xcd_tile(blockIdx.x, nblocks);
-#ifndef TB2_MAP
-#define TB2_MAP 0
-#endif
-  int tx_, ty_, tz_;
-  if (TB2_MAP == 1) {
-    // band order: the tile rows split into 8 bands (one per XCD's range of
-    // L), each band walked chunk by chunk, rows, then x: an XCD's
-    // consecutive rounds continue the same rows into the next chunk, and
-    // the 8 XCDs work on adjacent bands of the same planes at once
-    const int nch = nblocks / (ntx * nty);
-    int k = 0;
-#pragma unroll 1
-    for (int b = 1; b < 8; ++b)
-      if (((b * nty) / 8) * ntx * nch <= L) k = b;
-    const int r0 = (k * nty) / 8, rows = ((k + 1) * nty) / 8 - r0;
-    const int r = L - r0 * ntx * nch;
-    tz_ = r / (rows * ntx);
-    const int rem = r - tz_ * rows * ntx;
-    ty_ = r0 + rem / ntx;
-    tx_ = rem % ntx;
-  } else {
-    tx_ = L % ntx;
-    ty_ = (L / ntx) % nty;
-    tz_ = L / (ntx * nty);
-  }
-  const int x0 = tx_ * TX, y0 = ty_ * TY;
-  const int z0 = tz_ * kc;
+  const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
+  const int z0 = (L / (ntx * nty)) * kc;
   const int z1 = min(z0 + kc, g.nz);
   // uniform: the x / y domain faces the tile's rings (3 cells) reach
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
