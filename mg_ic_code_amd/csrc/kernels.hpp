@@ -54,9 +54,11 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
                     hipStream_t st);
-// the same two-sweep launch on fp32 fields (no phi += e)
+// the same two-sweep launch on fp32 fields; acc (the fp64 phi, or null):
+// the second sweep's values are added to it as (double)e instead of stored
 void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
-                      const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st);
+                      const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
+                      hipStream_t st);
 long gsrb_block_max_cells();
 // VCCOMPUTEOP3D (.ChF:181-237)
 void apply_op(double *lu, const double *u, const double *a, const double *b,

@@ -104,15 +104,15 @@ void MixedMultiGrid::relax(int d, LevelDataF &e, const LevelDataF &r, int n, boo
   // two sweeps per launch (the temporally blocked kernel, smoother_tb.hip)
   // on levels without exchanged faces, and on exchanged layouts in deep-halo
   // mode (a 4-deep shell before each pair: the kernel's rings run onto it);
-  // a last sweep that folds phi += e into fp64 stays a single sweep (on a
-  // 2-deep shell)
+  // the last pair folds phi += e into fp64 (round 5; a pair cannot start
+  // from zero and accumulate, so that one case takes two single sweeps)
   bool two = (!L.halo || L.deep) && n >= 2;
   for (int b = 0; two && b < op.grid->nlocal(); ++b)
     two = kern::gsrb_sweep_tb2_applies(op.boxArgs(b, true), L.s, kind);
   for (int it = 0; it < n;) {
     const bool zin = zero_in && it == 0;
     const int left = n - it;
-    const int k = two && (left >= 3 || (left == 2 && !acc)) ? 2 : 1;
+    const int k = two && left >= 2 && !(zin && left == 2 && acc) ? 2 : 1;
     const bool last = it + k == n;
     if (L.halo && !zin) src->exchange_shell(st, k == 2 ? kDeepShell : 2);
     for (int b = 0; b < op.grid->nlocal(); ++b) {
@@ -120,7 +120,7 @@ void MixedMultiGrid::relax(int d, LevelDataF &e, const LevelDataF &r, int n, boo
       prof_mark(st, nc, true, 2 * k);
       if (k == 2)
         kern::gsrb_sweep_tb2_f(dst->p[b], src->p[b], r.p[b], L.a->p[b], op.boxArgs(b, true), L.s,
-                               zin, st);
+                               zin, last && acc ? acc->p[b] : nullptr, st);
       else
         kern::gsrb_sweep_fused_f(dst->p[b], src->p[b], r.p[b], L.a->p[b], L.b->p[b],
                                  op.boxArgs(b, true), L.s, zin, last && acc ? acc->p[b] : nullptr,

@@ -199,7 +199,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
                                          const T *__restrict__ a, const BoxArgs &g,
                                          const StencilCoefs &s64, const TB2Ghosts<T> &gg, int x0,
                                          int y0, int z0, int z1, int ef) {
-  static_assert(!ACC || std::is_same<T, double>::value, "phi += e is folded into fp64 sweeps only");
+  // (ACC: acc is the fp64 sum field whatever T; a float sweep adds (double)e)
   using F = TB2<TX, TY, NT>;
   using V = typename TB2Vec<T>::type;
   const TB2Coefs<T> s(s64);
@@ -234,10 +234,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   const long corner = -16 - 4 * sy;
   auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
   // (steady steps: every plane they touch lies inside [-4, nz + 3], no clamp)
-  auto plane_u = [&](const T *f, int p) {
+  auto plane_u = [&](const auto *f, int p) {
     return reinterpret_cast<const char *>(f + corner + (long)p * sz);
   };
-  auto plane = [&](const T *f, int p) {  // corner of (clamped) plane p
+  auto plane = [&](const auto *f, int p) {  // corner of (clamped) plane p
     return reinterpret_cast<const char *>(f + corner + (long)clampi(p, -4, nz + 3) * sz);
   };
   // the lane offset is laundered per access: otherwise the compiler hoists
@@ -247,6 +247,13 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   auto at2 = [](const char *base, unsigned off) {
     asm volatile("" : "+v"(off));
     return *reinterpret_cast<const V *>(base + off);
+  };
+  // the fp64 sum field (ACC) at the byte offset of the same cell: offsets
+  // scale by sizeof(double) / sizeof(T)
+  constexpr unsigned kAccScale = (unsigned)(sizeof(double) / sizeof(T));
+  auto at2d = [](const char *base, unsigned off) {
+    asm volatile("" : "+v"(off));
+    return *reinterpret_cast<const double2 *>(base + off);
   };
   auto boff = [&](int x, int y) {  // byte offset of cell (x, y) from the corner
     return (unsigned)(sizeof(T) * (16 + x + (long)(y + 4) * sy));
@@ -587,6 +594,20 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
       char *const a = ldsp(slot_base(sl), cbm[i]);
       w.x = *reinterpret_cast<const T *>(a + ES);
       w.y = *reinterpret_cast<const T *>(a + SB + ES);
+      if constexpr (ACC && !std::is_same<T, double>::value) {
+        // phi += (double)e into the fp64 field (the fp32 sweeps of the mixed
+        // V-cycle; smoother.hip's single sweep does the same)
+        double2 d;
+        d.x = ac0[i] + (double)w.x;
+        d.y = ac1[i] + (double)w.y;
+        const unsigned off = kAccScale * roff[t][i];
+        const unsigned o4 = st == 3 ? off : kDrop;
+        const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(double) : kDrop);
+        const double e = st == 1 ? d.x : d.y;
+        sweep::bstore(rs, d, o4);
+        sweep::bstore(rs, e, o2);
+        continue;
+      }
       if constexpr (ACC) {  // phi += e (incr, scale 1) in the same pass
         w.x = ac0[i] + w.x;
         w.y = ac1[i] + w.y;
@@ -646,7 +667,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
         for (int i = 0; i < NP; ++i) {
           ac0[i] = an0[i];
           ac1[i] = an1[i];
-          const double2 v = at2(pl, roff[PU][i]);
+          const double2 v = at2d(pl, kAccScale * roff[PU][i]);
           an0[i] = v.x;
           an1[i] = v.y;
         }
@@ -835,13 +856,9 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
           u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks);                              \
   } while (0)
   if (acc) {
-    if constexpr (std::is_same<T, double>::value) {
-      if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
-      if (fast) MGIC_TB2(false, true, true);
-      else MGIC_TB2(false, true, false);
-    } else {
-      throw Error(kBadArg, "two-sweep launch: phi += e is folded into fp64 sweeps only");
-    }
+    if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
+    if (fast) MGIC_TB2(false, true, true);
+    else MGIC_TB2(false, true, false);
   } else if (zero_in) {
     if (fast) MGIC_TB2(true, false, true);
     else MGIC_TB2(true, false, false);
@@ -884,8 +901,9 @@ void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const 
 // single-sweep fp32 kernel and oracle/mixed.py compute them (phi += e stays a
 // separate fp64 sweep there)
 void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
-                      const BoxArgs &g, const StencilCoefs &s, bool zero_in, hipStream_t st) {
-  launch_tb2<float, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, nullptr, st);
+                      const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
+                      hipStream_t st) {
+  launch_tb2<float, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
 }
 
 }  // namespace kern
