@@ -452,6 +452,84 @@ __global__ __launch_bounds__(256) void k_restrict_f2(float *__restrict__ rc, con
   }
 }
 
+// (measurement) the fp64 restriction with two coarse cells per thread: two
+// 16-B loads per fine row and array; per coarse cell restrict_cell's
+// expressions in its order (MGIC_RESTRICT_D2=1 selects it)
+template <bool BC, int NT = 0>
+__global__ __launch_bounds__(256) void k_restrict_d2(double *__restrict__ rc, const BoxArgs cg,
+                                                     const double *__restrict__ u,
+                                                     const double *__restrict__ rhs,
+                                                     const double *__restrict__ a,
+                                                     const double *__restrict__ b, const BoxArgs fg,
+                                                     const StencilCoefs s64, int accumulate) {
+  const SC<double> s(s64);
+  const int ci = 2 * (blockIdx.x * TX + threadIdx.x);
+  const int cj = blockIdx.y * TY + threadIdx.y;
+  const int ck = blockIdx.z;
+  if (ci >= cg.nx || cj >= cg.ny) return;
+  const bool two = ci + 1 < cg.nx;
+  const double denom = (double)(2 * 2 * 2);  // .ChF:402
+  const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
+  double sum[2];
+  sum[0] = accumulate ? rc[cidx] : 0.0;
+  sum[1] = accumulate && two ? rc[cidx + 1] : 0.0;
+  const int i0 = 2 * ci;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = 2 * cj + jj, k = 2 * ck + kk;
+      const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
+      double c[4], ym[4], yp[4], zm[4], zp[4], rv[4], av[4], bv[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const V2<double> c2 = ld2(u + row + 2 * h);
+        const V2<double> ym2 = ld2(u + row + 2 * h - fg.sy), yp2 = ld2(u + row + 2 * h + fg.sy);
+        const V2<double> zm2 = ld2(u + row + 2 * h - fg.sz), zp2 = ld2(u + row + 2 * h + fg.sz);
+        const V2<double> rv2 = ld2n<NT & 1>(rhs + row + 2 * h), av2 = ld2n<NT & 1>(a + row + 2 * h);
+        c[2 * h] = c2.x; c[2 * h + 1] = c2.y;
+        ym[2 * h] = ym2.x; ym[2 * h + 1] = ym2.y;
+        yp[2 * h] = yp2.x; yp[2 * h + 1] = yp2.y;
+        zm[2 * h] = zm2.x; zm[2 * h + 1] = zm2.y;
+        zp[2 * h] = zp2.x; zp[2 * h + 1] = zp2.y;
+        rv[2 * h] = rv2.x; rv[2 * h + 1] = rv2.y;
+        av[2 * h] = av2.x; av[2 * h + 1] = av2.y;
+        if (BC) {
+          bv[2 * h] = bv[2 * h + 1] = s.bval;
+        } else {
+          const V2<double> bv2 = ld2n<NT & 1>(b + row + 2 * h);
+          bv[2 * h] = bv2.x; bv[2 * h + 1] = bv2.y;
+        }
+      }
+      const double xl = u[row - 1], xr = u[row + 4];
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const int e = 2 * q + ii, i = i0 + e;
+          const double uc = c[e];
+          double vxm = e == 0 ? xl : c[e - 1], vxp = e == 3 ? xr : c[e + 1];
+          double vym = ym[e], vyp = yp[e], vzm = zm[e], vzp = zp[e];
+          if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], fg.bcc[0], uc);
+          if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], fg.bcc[1], uc);
+          if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], fg.bcc[2], uc);
+          if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], fg.bcc[3], uc);
+          if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], fg.bcc[4], uc);
+          if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], fg.bcc[5], uc);
+          const double tx = (vxp + vxm) - 2.0 * uc;
+          const double ty = (vyp + vym) - 2.0 * uc;
+          const double tz = (vzp + vzm) - 2.0 * uc;
+          double ldpsi = (tx + ty) + tz;                       // .ChF:416-425
+          double lofdpsi = s.alpha * av[e] * uc;               // .ChF:411-412
+          ldpsi = ldpsi * s.dxinv * s.beta * bv[e];            // .ChF:427
+          lofdpsi = lofdpsi - ldpsi;                           // .ChF:429
+          sum[q] = sum[q] + (rv[e] - lofdpsi) / denom;         // .ChF:431-432
+        }
+    }
+  rc[cidx] = sum[0];
+  if (two) rc[cidx + 1] = sum[1];
+}
+
 struct ProlongArgs {
   int avail_lo[3], avail_hi[3];
 };
@@ -1390,6 +1468,17 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
   // every bCoef kind (the same switch in restrict_residual_f)
   const int accu = accumulate ? 1 : 0;
   const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
+  static const bool d2 = [] {
+    const char *e = getenv("MGIC_RESTRICT_D2");
+    return e && atoi(e) > 0;
+  }();
+  if (d2 && (nt & 1)) {
+    const dim3 g2 = grid_cells((cg.nx + 1) / 2, cg.ny, cg.nz);
+    if (s.bconst) k_restrict_d2<true, 1><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
+    else k_restrict_d2<false, 1><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
+    check_launch();
+    return;
+  }
   if (s.bconst && (nt & 1))
     k_restrict<double, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
   else if (s.bconst)

@@ -22,4 +22,29 @@ for l in open(sys.argv[1]):
     v, j = l.split(" ", 1); d = json.loads(j); m = d["mixed"]
     print(v, "fmg", m["ms_per_fmg"], "vcycle", m["ms_per_vcycle"], "oracle", d.get("oracle_check", {}).get("bit_identical"), "res", m["residual_max_norm"]["after_fmg_plus_4_vcycles"])
 PY
+# the fp64 restriction with two coarse cells per thread (MGIC_RESTRICT_D2=1,
+# a measurement switch): parity subset, three interleaved rounds of
+# bench_kernels at 512^3 / 256^3 and the V-cycle
+MGIC_RESTRICT_D2=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -q -x \
+  -k "restrict or operator_methods or vcycle_iterations or full_size_512_vcycle or multibox or agglomerat" \
+  --timeout 200 --timeout-method thread > gpurun_out/rf2/pytest_d2.log 2>&1; rc=$?
+echo "d2: $(tail -1 gpurun_out/rf2/pytest_d2.log)"; [ $rc -ne 0 ] && { tail -30 gpurun_out/rf2/pytest_d2.log; exit $rc; }
+o2=gpurun_out/rf2/d2.txt; : > $o2
+for r in 1 2 3; do
+  for v in 0 1; do
+    MGIC_RESTRICT_D2=$v timeout -k 10 120 python tools/bench_kernels.py --size 512 --reps 30 --tag d2=$v >> $o2 || exit 1
+    MGIC_RESTRICT_D2=$v timeout -k 10 120 python tools/bench_kernels.py --size 256 --reps 50 --tag d2=$v >> $o2 || exit 1
+    MGIC_RESTRICT_D2=$v timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-bottom > gpurun_out/rf2/b.tmp 2> gpurun_out/rf2/err.log || { tail gpurun_out/rf2/err.log; exit 1; }
+    python3 -c "import json; d=json.loads(open('gpurun_out/rf2/b.tmp').read().strip().splitlines()[-1]); print(json.dumps({'tag':'d2=$v','vcycles':d['value']}))" >> $o2
+  done
+done
+python3 - $o2 <<'PY'
+import json, sys, collections
+d = collections.defaultdict(list)
+for l in open(sys.argv[1]):
+    j = json.loads(l)
+    if "restrict" in j: d[(j["tag"], j["size"])].append(j["restrict"]["ms"])
+    else: d[(j["tag"], "vcycles")].append(j["vcycles"])
+for k in sorted(d): print(k, d[k])
+PY
 echo "session done"
