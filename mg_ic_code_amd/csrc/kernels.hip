@@ -369,167 +369,6 @@ __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxA
   restrict_cell<T, BC, NT>(rc, cg, u, rhs, a, b, fg, s, accumulate, ci, cj, blockIdx.z);
 }
 
-// The fp32 restriction with two coarse cells per thread (the mixed V-cycle):
-// a fine row's four floats are one 16-B load per array, as the fp64 form's two
-// doubles are, instead of the 8-B pairs of restrict_cell<float>.  Per coarse
-// cell the same expressions in the same (k, j, i) order, so the same bits.
-template <bool NT>
-__device__ __forceinline__ float4 ld4n(const float *__restrict__ p) {
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  f4 v;
-  if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(p));
-  else v = *reinterpret_cast<const f4 *>(p);
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float f4at(const float4 &v, int e) {
-  return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
-}
-template <bool BC, int NT = 0>
-__global__ __launch_bounds__(256) void k_restrict_f2(float *__restrict__ rc, const BoxArgs cg,
-                                                     const float *__restrict__ u,
-                                                     const float *__restrict__ rhs,
-                                                     const float *__restrict__ a,
-                                                     const float *__restrict__ b, const BoxArgs fg,
-                                                     const StencilCoefs s64, int accumulate) {
-  const SC<float> s(s64);
-  const int ci = 2 * (blockIdx.x * TX + threadIdx.x);
-  const int cj = blockIdx.y * TY + threadIdx.y;
-  const int ck = blockIdx.z;
-  if (ci >= cg.nx || cj >= cg.ny) return;
-  const bool two = ci + 1 < cg.nx;
-  const float denom = (float)(2 * 2 * 2);  // .ChF:402
-  const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
-  float sum[2];
-  sum[0] = accumulate ? rc[cidx] : 0.0f;
-  sum[1] = accumulate && two ? rc[cidx + 1] : 0.0f;
-  const int i0 = 2 * ci;
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = 2 * cj + jj, k = 2 * ck + kk;
-      const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
-      const float4 c = ld4n<false>(u + row);
-      const float4 ym = ld4n<false>(u + row - fg.sy), yp = ld4n<false>(u + row + fg.sy);
-      const float4 zm = ld4n<false>(u + row - fg.sz), zp = ld4n<false>(u + row + fg.sz);
-      const float xl = u[row - 1], xr = u[row + 4];
-      const float4 rv = ld4n<(NT & 1) != 0>(rhs + row), av = ld4n<(NT & 1) != 0>(a + row);
-      float4 bv;
-      if (BC) bv = make_float4(s.bval, s.bval, s.bval, s.bval);
-      else bv = ld4n<(NT & 1) != 0>(b + row);
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii) {
-          const int e = 2 * q + ii, i = i0 + e;
-          const float uc = f4at(c, e);
-          float vxm = e == 0 ? xl : f4at(c, e - 1), vxp = e == 3 ? xr : f4at(c, e + 1);
-          float vym = f4at(ym, e), vyp = f4at(yp, e);
-          float vzm = f4at(zm, e), vzp = f4at(zp, e);
-          if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], (float)fg.bcc[0], uc);
-          if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], (float)fg.bcc[1], uc);
-          if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], (float)fg.bcc[2], uc);
-          if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], (float)fg.bcc[3], uc);
-          if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], (float)fg.bcc[4], uc);
-          if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], (float)fg.bcc[5], uc);
-          const float tx = (vxp + vxm) - 2.0f * uc;
-          const float ty = (vyp + vym) - 2.0f * uc;
-          const float tz = (vzp + vzm) - 2.0f * uc;
-          float ldpsi = (tx + ty) + tz;                                  // .ChF:416-425
-          float lofdpsi = s.alpha * f4at(av, e) * uc;                    // .ChF:411-412
-          ldpsi = ldpsi * s.dxinv * s.beta * f4at(bv, e);                // .ChF:427
-          lofdpsi = lofdpsi - ldpsi;                                     // .ChF:429
-          sum[q] = sum[q] + (f4at(rv, e) - lofdpsi) / denom;            // .ChF:431-432
-        }
-    }
-  if (two) {
-    V2<float> w;
-    w.x = sum[0];
-    w.y = sum[1];
-    *reinterpret_cast<V2<float> *>(rc + cidx) = w;
-  } else {
-    rc[cidx] = sum[0];
-  }
-}
-
-// (measurement) the fp64 restriction with two coarse cells per thread: two
-// 16-B loads per fine row and array; per coarse cell restrict_cell's
-// expressions in its order (MGIC_RESTRICT_D2=1 selects it)
-template <bool BC, int NT = 0>
-__global__ __launch_bounds__(256) void k_restrict_d2(double *__restrict__ rc, const BoxArgs cg,
-                                                     const double *__restrict__ u,
-                                                     const double *__restrict__ rhs,
-                                                     const double *__restrict__ a,
-                                                     const double *__restrict__ b, const BoxArgs fg,
-                                                     const StencilCoefs s64, int accumulate) {
-  const SC<double> s(s64);
-  const int ci = 2 * (blockIdx.x * TX + threadIdx.x);
-  const int cj = blockIdx.y * TY + threadIdx.y;
-  const int ck = blockIdx.z;
-  if (ci >= cg.nx || cj >= cg.ny) return;
-  const bool two = ci + 1 < cg.nx;
-  const double denom = (double)(2 * 2 * 2);  // .ChF:402
-  const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
-  double sum[2];
-  sum[0] = accumulate ? rc[cidx] : 0.0;
-  sum[1] = accumulate && two ? rc[cidx + 1] : 0.0;
-  const int i0 = 2 * ci;
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = 2 * cj + jj, k = 2 * ck + kk;
-      const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
-      double c[4], ym[4], yp[4], zm[4], zp[4], rv[4], av[4], bv[4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const V2<double> c2 = ld2(u + row + 2 * h);
-        const V2<double> ym2 = ld2(u + row + 2 * h - fg.sy), yp2 = ld2(u + row + 2 * h + fg.sy);
-        const V2<double> zm2 = ld2(u + row + 2 * h - fg.sz), zp2 = ld2(u + row + 2 * h + fg.sz);
-        const V2<double> rv2 = ld2n<NT & 1>(rhs + row + 2 * h), av2 = ld2n<NT & 1>(a + row + 2 * h);
-        c[2 * h] = c2.x; c[2 * h + 1] = c2.y;
-        ym[2 * h] = ym2.x; ym[2 * h + 1] = ym2.y;
-        yp[2 * h] = yp2.x; yp[2 * h + 1] = yp2.y;
-        zm[2 * h] = zm2.x; zm[2 * h + 1] = zm2.y;
-        zp[2 * h] = zp2.x; zp[2 * h + 1] = zp2.y;
-        rv[2 * h] = rv2.x; rv[2 * h + 1] = rv2.y;
-        av[2 * h] = av2.x; av[2 * h + 1] = av2.y;
-        if (BC) {
-          bv[2 * h] = bv[2 * h + 1] = s.bval;
-        } else {
-          const V2<double> bv2 = ld2n<NT & 1>(b + row + 2 * h);
-          bv[2 * h] = bv2.x; bv[2 * h + 1] = bv2.y;
-        }
-      }
-      const double xl = u[row - 1], xr = u[row + 4];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii) {
-          const int e = 2 * q + ii, i = i0 + e;
-          const double uc = c[e];
-          double vxm = e == 0 ? xl : c[e - 1], vxp = e == 3 ? xr : c[e + 1];
-          double vym = ym[e], vyp = yp[e], vzm = zm[e], vzp = zp[e];
-          if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], fg.bcc[0], uc);
-          if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], fg.bcc[1], uc);
-          if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], fg.bcc[2], uc);
-          if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], fg.bcc[3], uc);
-          if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], fg.bcc[4], uc);
-          if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], fg.bcc[5], uc);
-          const double tx = (vxp + vxm) - 2.0 * uc;
-          const double ty = (vyp + vym) - 2.0 * uc;
-          const double tz = (vzp + vzm) - 2.0 * uc;
-          double ldpsi = (tx + ty) + tz;                       // .ChF:416-425
-          double lofdpsi = s.alpha * av[e] * uc;               // .ChF:411-412
-          ldpsi = ldpsi * s.dxinv * s.beta * bv[e];            // .ChF:427
-          lofdpsi = lofdpsi - ldpsi;                           // .ChF:429
-          sum[q] = sum[q] + (rv[e] - lofdpsi) / denom;         // .ChF:431-432
-        }
-    }
-  rc[cidx] = sum[0];
-  if (two) rc[cidx + 1] = sum[1];
-}
-
 struct ProlongArgs {
   int avail_lo[3], avail_hi[3];
 };
@@ -593,92 +432,6 @@ __global__ __launch_bounds__(256) void k_prolong(T *__restrict__ uf, const BoxAr
       v.x = v.x + e0;
       v.y = v.y + e1;
       *reinterpret_cast<V2<T> *>(uf + row) = v;
-    }
-}
-
-// The fp32 prolongation with two coarse cells per thread (the mixed
-// V-cycle): a fine row's four floats are one 16-B read-modify-write, the
-// coarse pair and its y / z neighbour pairs 8-B loads.  Per fine cell the
-// same terms in the same order as k_prolong<float>.
-template <int TYPE>
-__global__ __launch_bounds__(256) void k_prolong_f2(float *__restrict__ uf, const BoxArgs fg,
-                                                    const float *__restrict__ ec, const BoxArgs cg,
-                                                    const ProlongArgs pa) {
-  const int ci = 2 * (blockIdx.x * TX + threadIdx.x);
-  const int cj = blockIdx.y * TY + threadIdx.y;
-  const int ck = blockIdx.z;
-  if (ci >= cg.nx || cj >= cg.ny) return;
-  const bool two = ci + 1 < cg.nx;
-  const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
-  const V2<float> cc = ld2(ec + cidx);  // (ci + 1 is allocated: a ghost or padding when !two)
-  const float c0[2] = {cc.x, cc.y};
-  float dlo[2][3], dhi[2][3];
-  bool ok[2][3];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      dlo[q][d] = dhi[q][d] = 0.0f;
-      ok[q][d] = false;
-    }
-  if (TYPE == 1) {
-    const float xl = ec[cidx - 1], xr = ec[cidx + 2];
-    const V2<float> ym = ld2(ec + cidx - cg.sy), yp = ld2(ec + cidx + cg.sy);
-    const V2<float> zm = ld2(ec + cidx - cg.sz), zp = ld2(ec + cidx + cg.sz);
-    const int cn[3] = {cg.nx, cg.ny, cg.nz};
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int ic[3] = {ci + q, cj, ck};
-      const float lo[3] = {q ? c0[0] : xl, q ? ym.y : ym.x, q ? zm.y : zm.x};
-      const float hi[3] = {q ? xr : c0[1], q ? yp.y : yp.x, q ? zp.y : zp.x};
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const bool has_lo = (ic[d] > 0) || pa.avail_lo[d];
-        const bool has_hi = (ic[d] < cn[d] - 1) || pa.avail_hi[d];
-        ok[q][d] = has_lo || has_hi;
-        const float sl_hi = hi[d] - c0[q], sl_lo = c0[q] - lo[d];
-        dhi[q][d] = (has_hi ? sl_hi : sl_lo) * 0.25f;    // upper child: +0.25 * slope
-        dlo[q][d] = (!has_lo ? sl_hi : sl_lo) * -0.25f;  // lower child: -0.25 * slope
-      }
-    }
-  }
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const long row = (long)(2 * ci) + (long)(2 * cj + jj) * fg.sy + (long)(2 * ck + kk) * fg.sz;
-      float4 v = *reinterpret_cast<const float4 *>(uf + row);
-      float out[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        float e0 = c0[q], e1 = c0[q];
-        if (TYPE == 1) {
-          if (ok[q][0]) {
-            e0 = e0 + dlo[q][0];
-            e1 = e1 + dhi[q][0];
-          }
-          if (ok[q][1]) {
-            const float tt = jj ? dhi[q][1] : dlo[q][1];
-            e0 = e0 + tt;
-            e1 = e1 + tt;
-          }
-          if (ok[q][2]) {
-            const float tt = kk ? dhi[q][2] : dlo[q][2];
-            e0 = e0 + tt;
-            e1 = e1 + tt;
-          }
-        }
-        out[2 * q] = out[2 * q] + e0;
-        out[2 * q + 1] = out[2 * q + 1] + e1;
-      }
-      if (two) {
-        *reinterpret_cast<float4 *>(uf + row) = make_float4(out[0], out[1], out[2], out[3]);
-      } else {
-        V2<float> w;
-        w.x = out[0];
-        w.y = out[1];
-        *reinterpret_cast<V2<float> *>(uf + row) = w;
-      }
     }
 }
 
@@ -1468,17 +1221,6 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
   // every bCoef kind (the same switch in restrict_residual_f)
   const int accu = accumulate ? 1 : 0;
   const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
-  static const bool d2 = [] {
-    const char *e = getenv("MGIC_RESTRICT_D2");
-    return e && atoi(e) > 0;
-  }();
-  if (d2 && (nt & 1)) {
-    const dim3 g2 = grid_cells((cg.nx + 1) / 2, cg.ny, cg.nz);
-    if (s.bconst) k_restrict_d2<true, 1><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
-    else k_restrict_d2<false, 1><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
-    check_launch();
-    return;
-  }
   if (s.bconst && (nt & 1))
     k_restrict<double, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
   else if (s.bconst)
@@ -1744,28 +1486,6 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
     const char *e = getenv("MGIC_RESTRICT_NT");
     return e ? atoi(e) : 1;
   }();
-  // two coarse cells per thread (16-B fine-row loads) when the fine field's
-  // rows are 16-B aligned, as FabGeom lays them out (MGIC_RESTRICT_F2=0: one)
-  static const bool f2 = [] {
-    const char *e = getenv("MGIC_RESTRICT_F2");
-    return !(e && atoi(e) == 0);
-  }();
-  const bool al = ((reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(rhs) |
-                    reinterpret_cast<uintptr_t>(a) | (s.bconst ? 0 : reinterpret_cast<uintptr_t>(b))) &
-                   15) == 0 && (fg.sy & 3) == 0 && (fg.sz & 3) == 0;
-  if (f2 && al) {
-    const dim3 g2 = grid_cells((cg.nx + 1) / 2, cg.ny, cg.nz);
-    if (s.bconst && (nt & 1))
-      k_restrict_f2<true, 1><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
-    else if (s.bconst)
-      k_restrict_f2<true><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
-    else if (nt & 1)
-      k_restrict_f2<false, 1><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
-    else
-      k_restrict_f2<false><<<g2, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
-    check_launch();
-    return;
-  }
   const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
   if (s.bconst && (nt & 1))
     k_restrict<float, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
@@ -1788,22 +1508,6 @@ void prolong_f(float *uf, const BoxArgs &fg, const float *ec, const BoxArgs &cg,
   }
   MGIC_CHECK(fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz,
              "prolong: fine box must be the coarse box refined by 2");
-  // two coarse cells per thread (16-B fine-row read-modify-writes) when the
-  // rows are 16-B aligned (FabGeom's layout; MGIC_PROLONG_F2=0: one)
-  static const bool f2 = [] {
-    const char *e = getenv("MGIC_PROLONG_F2");
-    return !(e && atoi(e) == 0);
-  }();
-  const bool al = ((reinterpret_cast<uintptr_t>(uf) & 15) == 0) &&
-                  ((reinterpret_cast<uintptr_t>(ec) & 7) == 0) && (fg.sy & 3) == 0 &&
-                  (fg.sz & 3) == 0 && (cg.sy & 1) == 0 && (cg.sz & 1) == 0;
-  if (f2 && al) {
-    const dim3 g2 = grid_cells((cg.nx + 1) / 2, cg.ny, cg.nz);
-    if (type == 1) k_prolong_f2<1><<<g2, kBlock, 0, st>>>(uf, fg, ec, cg, pa);
-    else k_prolong_f2<0><<<g2, kBlock, 0, st>>>(uf, fg, ec, cg, pa);
-    check_launch();
-    return;
-  }
   if (type == 1)
     k_prolong<float, 1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
   else
