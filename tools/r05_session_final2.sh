@@ -15,8 +15,8 @@ cat gpurun_out/f2/smoke.log
 timeout -k 10 900 python bench.py --steps 20 --warmup 5 > gpurun_out/f2/bench.log 2>&1 || { tail gpurun_out/f2/bench.log; exit 1; }
 tail -n 1 gpurun_out/f2/bench.log > gpurun_out/f2/bench_line.json
 python3 -c "import json; d=json.load(open('gpurun_out/f2/bench_line.json')); print(d['value'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['roofline']['traffic'], d['cpu_baseline']['value'], d['bottom'])"
-TAG=r05k BSTEPS=10 bash tools/trace_bench.sh > /dev/null || exit 1
-grep -E "k_gsrb_tb2" gpurun_out/trace_r05k.txt | head -8
+TAG=${FTAG:-r05k} BSTEPS=10 bash tools/trace_bench.sh > /dev/null || exit 1
+grep -E "k_gsrb_tb2" gpurun_out/trace_${FTAG:-r05k}.txt | head -8
 : > gpurun_out/f2/proxy.txt
 for r in 1 2 3; do
   timeout -k 10 200 python3 tools/rank_proxy.py --transport ipc --deep 1 --steps 30 --charge 1 >> gpurun_out/f2/proxy.txt 2> gpurun_out/f2/proxy_err.log || { tail gpurun_out/f2/proxy_err.log; exit 1; }
