@@ -1,7 +1,8 @@
 """Per-kernel means of SQ / GRBM counters from rocprofv3 --pmc passes
 (tools/r04_session_pmc_sq.sh): every *_counter_collection.csv under the
 given directory, grouped by (kernel, grid size), one mean per counter per
-dispatch, plus the shares of SQ_WAVE_CYCLES (wait / issue-stall / active).
+dispatch, plus the shares of SQ_WAVE_CYCLES (wait / issue-stall / active);
+PMC_KERNELS: a regex of the kernels shown (default tb2).
 Measurement tooling only."""
 import csv
 import glob
@@ -20,7 +21,7 @@ def main(d):
             key = (os.path.dirname(f), r.get("Dispatch_Id", ""))
             per[k][r["Counter_Name"]][key] = per[k][r["Counter_Name"]].get(key, 0.0) + float(r["Counter_Value"])
     for k, cs in sorted(per.items(), key=lambda kv: -len(next(iter(kv[1].values())))):
-        if "tb2" not in k[0]:
+        if not re.search(os.environ.get("PMC_KERNELS", "tb2"), k[0]):
             continue
         print(f"{k[0]} grid={k[1]}")
         mean = {c: sum(v.values()) / len(v) for c, v in cs.items()}
