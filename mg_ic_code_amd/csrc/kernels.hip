@@ -369,6 +369,133 @@ __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxA
   restrict_cell<T, BC, NT>(rc, cg, u, rhs, a, b, fg, s, accumulate, ci, cj, blockIdx.z);
 }
 
+// The restriction streaming in z with the fine u planes staged in LDS: a
+// workgroup owns 64 x 4 coarse columns over a chunk of coarse planes; the
+// four fine planes a coarse plane reads (2k-1 .. 2k+2) sit in a 4-slot LDS
+// ring of 10 x 132 doubles (the tile's 8 fine rows and 128 fine columns with
+// their halo), each loaded from global memory once with 16-B loads and the
+// next two prefetched into registers while the current plane is summed.  rhs
+// and aCoef stream from global memory as in k_restrict.  Per coarse cell the
+// expressions and order of restrict_cell, so the same bits.
+constexpr int kRzCols = 132, kRzRows = 10, kRzPairs = kRzRows * kRzCols / 2;  // 660
+template <bool BC, int NT>
+__global__ __launch_bounds__(256) void k_restrict_zl(double *__restrict__ rc, const BoxArgs cg,
+                                                     const double *__restrict__ u,
+                                                     const double *__restrict__ rhs,
+                                                     const double *__restrict__ a,
+                                                     const double *__restrict__ b, const BoxArgs fg,
+                                                     const StencilCoefs s64, int accumulate, int kc,
+                                                     int ntx, int nty) {
+  __shared__ double Ls[4][kRzRows][kRzCols];
+  const SC<double> s(s64);
+  const int ntile = ntx * nty;
+  const int tile = blockIdx.x % ntile, chunk = blockIdx.x / ntile;
+  const int cx0 = (tile % ntx) * TX, cy0 = (tile / ntx) * 4;
+  const int k0 = chunk * kc, k1 = min(k0 + kc, cg.nz);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ci = cx0 + lane, cj = cy0 + w;
+  const bool act = ci < cg.nx && cj < cg.ny;
+  // the staged plane: fine rows 2 cy0 - 1 .. 2 cy0 + 8, columns 2 cx0 - 2 ..
+  // 2 cx0 + 129, as 660 16-B pairs; pair q of lane tid + 256 i (clamped into
+  // the allocated ghosts: what a clamped pair holds is never read)
+  const int fx0 = 2 * cx0 - 2, fy0 = 2 * cy0 - 1;
+  long poff[3];
+  int pl[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int q = tid + 256 * i;
+    const int r = q / (kRzCols / 2), m = q - r * (kRzCols / 2);
+    const int y = min(fy0 + r, fg.ny + 1), x = min(fx0 + 2 * m, fg.nx);
+    poff[i] = (long)x + (long)y * fg.sy;
+    pl[i] = q < kRzPairs ? r * kRzCols + 2 * m : -1;
+  }
+  auto plane_ptr = [&](int k) { return u + (long)min(k, fg.nz + 1) * fg.sz; };
+  V2<double> pre[2][3];
+  auto fetch = [&](int k, int h) {
+    const double *p = plane_ptr(k);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (pl[i] >= 0) pre[h][i] = ld2(p + poff[i]);
+  };
+  auto put = [&](int k, int h) {
+    double *dst = &Ls[k & 3][0][0];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (pl[i] >= 0) *reinterpret_cast<V2<double> *>(dst + pl[i]) = pre[h][i];
+  };
+  fetch(2 * k0 - 1, 0);
+  fetch(2 * k0, 1);
+  put(2 * k0 - 1, 0);
+  put(2 * k0, 1);
+  fetch(2 * k0 + 1, 0);
+  fetch(2 * k0 + 2, 1);
+  put(2 * k0 + 1, 0);
+  put(2 * k0 + 2, 1);
+  __syncthreads();
+  const double denom = (double)(2 * 2 * 2);  // .ChF:402
+  for (int ck = k0; ck < k1; ++ck) {
+    const bool more = ck + 1 < k1;
+    if (more) {
+      fetch(2 * ck + 3, 0);
+      fetch(2 * ck + 4, 1);
+    }
+    if (act) {
+      const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
+      double sum = accumulate ? rc[cidx] : 0.0;
+      const int i0 = 2 * ci;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int j = 2 * cj + jj, k = 2 * ck + kk;
+          const int r = 2 * w + jj + 1, cx = 2 * lane + 2;
+          const double *Lk = &Ls[k & 3][0][0], *Lm = &Ls[(k - 1) & 3][0][0],
+                       *Lp = &Ls[(k + 1) & 3][0][0];
+          const V2<double> c = *reinterpret_cast<const V2<double> *>(Lk + r * kRzCols + cx);
+          const V2<double> ym = *reinterpret_cast<const V2<double> *>(Lk + (r - 1) * kRzCols + cx);
+          const V2<double> yp = *reinterpret_cast<const V2<double> *>(Lk + (r + 1) * kRzCols + cx);
+          const V2<double> zm = *reinterpret_cast<const V2<double> *>(Lm + r * kRzCols + cx);
+          const V2<double> zp = *reinterpret_cast<const V2<double> *>(Lp + r * kRzCols + cx);
+          const double xl = Lk[r * kRzCols + cx - 1], xr = Lk[r * kRzCols + cx + 2];
+          const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
+          const V2<double> rv = ld2n<NT & 1>(rhs + row), av = ld2n<NT & 1>(a + row);
+          V2<double> bv;
+          if (BC) bv.x = bv.y = s.bval;
+          else bv = ld2n<NT & 1>(b + row);
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii) {
+            const int i = i0 + ii;
+            const double uc = ii ? c.y : c.x;
+            double vxm = ii ? c.x : xl, vxp = ii ? xr : c.y;
+            double vym = ii ? ym.y : ym.x, vyp = ii ? yp.y : yp.x;
+            double vzm = ii ? zm.y : zm.x, vzp = ii ? zp.y : zp.x;
+            if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], fg.bcc[0], uc);
+            if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], fg.bcc[1], uc);
+            if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], fg.bcc[2], uc);
+            if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], fg.bcc[3], uc);
+            if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], fg.bcc[4], uc);
+            if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], fg.bcc[5], uc);
+            const double tx = (vxp + vxm) - 2.0 * uc;
+            const double ty = (vyp + vym) - 2.0 * uc;
+            const double tz = (vzp + vzm) - 2.0 * uc;
+            double ldpsi = (tx + ty) + tz;                                  // .ChF:416-425
+            double lofdpsi = s.alpha * (ii ? av.y : av.x) * uc;            // .ChF:411-412
+            ldpsi = ldpsi * s.dxinv * s.beta * (ii ? bv.y : bv.x);         // .ChF:427
+            lofdpsi = lofdpsi - ldpsi;                                      // .ChF:429
+            sum = sum + ((ii ? rv.y : rv.x) - lofdpsi) / denom;             // .ChF:431-432
+          }
+        }
+      rc[cidx] = sum;
+    }
+    if (more) {
+      __syncthreads();  // every lane is done with planes 2ck-1, 2ck
+      put(2 * ck + 3, 0);
+      put(2 * ck + 4, 1);
+      __syncthreads();
+    }
+  }
+}
+
 struct ProlongArgs {
   int avail_lo[3], avail_hi[3];
 };
@@ -1220,6 +1347,21 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
   // MGIC_RESTRICT_NT bit 0: non-temporal rhs / aCoef / bCoef loads, for
   // every bCoef kind (the same switch in restrict_residual_f)
   const int accu = accumulate ? 1 : 0;
+  static const int zl = [] {  // (measurement) MGIC_RESTRICT_ZL = the z chunk in coarse planes
+    const char *e = getenv("MGIC_RESTRICT_ZL");
+    return e ? atoi(e) : 0;
+  }();
+  if (zl > 0 && (nt & 1) && fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz) {
+    const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
+    const int kc = zl < cg.nz ? zl : cg.nz;
+    const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
+    if (s.bconst)
+      k_restrict_zl<true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
+    else
+      k_restrict_zl<false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
+    check_launch();
+    return;
+  }
   const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
   if (s.bconst && (nt & 1))
     k_restrict<double, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu);
