@@ -369,14 +369,19 @@ __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxA
   restrict_cell<T, BC, NT>(rc, cg, u, rhs, a, b, fg, s, accumulate, ci, cj, blockIdx.z);
 }
 
-// The restriction streaming in z with the fine u planes staged in LDS: a
+// The restriction with the fine u planes staged in LDS (the default): a
 // workgroup owns 64 x 4 coarse columns over a chunk of coarse planes; the
 // four fine planes a coarse plane reads (2k-1 .. 2k+2) sit in a 4-slot LDS
 // ring of 10 x 132 doubles (the tile's 8 fine rows and 128 fine columns with
 // their halo), each loaded from global memory once with 16-B loads and the
 // next two prefetched into registers while the current plane is summed.  rhs
 // and aCoef stream from global memory as in k_restrict.  Per coarse cell the
-// expressions and order of restrict_cell, so the same bits.
+// expressions and order of restrict_cell, so the same bits.  Loading every
+// fine row once into LDS instead of five times per lane through the L1 (c,
+// y -+ 1, z -+ 1) is what pays: k_restrict's L1 sent the L2 twice its
+// compulsory bytes and stalled on pending requests two thirds of the time
+// (profiles/r05q_stream_pmc.txt); short chunks (2 coarse planes) keep the
+// grid large, longer ones re-read fewer halo planes but ran slower.
 constexpr int kRzCols = 132, kRzRows = 10, kRzPairs = kRzRows * kRzCols / 2;  // 660
 template <bool BC, int NT>
 __global__ __launch_bounds__(256) void k_restrict_zl(double *__restrict__ rc, const BoxArgs cg,
@@ -1347,9 +1352,12 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
   // MGIC_RESTRICT_NT bit 0: non-temporal rhs / aCoef / bCoef loads, for
   // every bCoef kind (the same switch in restrict_residual_f)
   const int accu = accumulate ? 1 : 0;
-  static const int zl = [] {  // (measurement) MGIC_RESTRICT_ZL = the z chunk in coarse planes
+  // k_restrict_zl, two coarse planes per workgroup (MGIC_RESTRICT_ZL: the
+  // chunk; 0 = k_restrict).  512^3: 0.706 -> 0.641 ms, 256^3 equal, V-cycle
+  // +1.4% (chunks 1 .. 32 measured, profiles/r05r_restrict_lds_ab.txt)
+  static const int zl = [] {
     const char *e = getenv("MGIC_RESTRICT_ZL");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   if (zl > 0 && (nt & 1) && fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz) {
     const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
