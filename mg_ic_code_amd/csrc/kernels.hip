@@ -355,6 +355,128 @@ __device__ __forceinline__ void restrict_cell(T *__restrict__ rc, const BoxArgs 
   rc[cidx] = sum;
 }
 
+// k_residual_z2 with the u planes staged in LDS: the workgroup's 128 x 4
+// cells of a plane plus their one-cell halo (6 rows x 132 columns) go to a
+// 4-slot LDS ring, each row loaded once with 16-B loads (the next plane
+// prefetched into registers), one barrier per plane; rhs / aCoef / bCoef
+// and r stream as in k_residual_z2.  Same grid, same cells per thread, same
+// expressions, so the same bits and the same norm partials.
+constexpr int kRlCols = 132, kRlRows = 6, kRlPairs = kRlRows * kRlCols / 2;  // 396
+template <bool BC, class RT, int NT = 0, bool NRM = false>
+__global__ __launch_bounds__(256) void k_residual_zl(RT *__restrict__ r,
+                                                     const double *__restrict__ u,
+                                                     const double *__restrict__ rhs,
+                                                     const double *__restrict__ a,
+                                                     const double *__restrict__ b, const BoxArgs g,
+                                                     const StencilCoefs s, int kc,
+                                                     double *__restrict__ partials = nullptr) {
+  __shared__ double Ls[4][kRlRows][kRlCols];
+  const int tid = threadIdx.x + TX * threadIdx.y;
+  const int x0 = 2 * blockIdx.x * TX, y0 = blockIdx.y * TY;
+  const int i = x0 + 2 * threadIdx.x, j = y0 + threadIdx.y;
+  const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, g.nz);
+  // pair q of the staged plane: row q / 66 (cell y0 - 1 + row), pair q % 66
+  // (cells x0 - 2 + 2 m, +1); clamped into the allocated ghosts (a clamped
+  // pair is never read)
+  long poff[2];
+  int pl[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int q = tid + 256 * h;
+    const int rr = q / (kRlCols / 2), m = q - rr * (kRlCols / 2);
+    const int y = min(y0 - 1 + rr, g.ny + 1), x = min(x0 - 2 + 2 * m, g.nx);
+    poff[h] = (long)x + (long)y * g.sy;
+    pl[h] = q < kRlPairs ? rr * kRlCols + 2 * m : -1;
+  }
+  V2<double> pre[2];
+  auto fetch = [&](int k) {
+    const double *p = u + (long)min(k, g.nz + 1) * g.sz;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (pl[h] >= 0) pre[h] = ld2(p + poff[h]);
+  };
+  auto put = [&](int k) {
+    double *dst = &Ls[k & 3][0][0];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (pl[h] >= 0) *reinterpret_cast<V2<double> *>(dst + pl[h]) = pre[h];
+  };
+  fetch(k0 - 1);
+  put(k0 - 1);
+  fetch(k0);
+  put(k0);
+  fetch(k0 + 1);
+  put(k0 + 1);
+  fetch(k0 + 2);
+  __syncthreads();
+  double nmax = 0.0;  // the identity of max |x|
+  const bool act = i < g.nx && j < g.ny;
+  const long col = (long)i + (long)j * g.sy;
+  const bool two = i + 1 < g.nx;
+  const bool fx0 = i == 0 && g.bcm[0];
+  const bool fx1a = i == g.nx - 1 && g.bcm[1], fx1b = i + 1 == g.nx - 1 && g.bcm[1];
+  const bool fy0 = j == 0 && g.bcm[2], fy1 = j == g.ny - 1 && g.bcm[3];
+  const int lr = threadIdx.y + 1, lc = 2 * threadIdx.x + 2;
+  for (int k = k0; k < k1; ++k) {
+    put(k + 2);  // (slot of plane k - 2, last read in the previous step)
+    if (k + 3 < k1 + 2) fetch(k + 3);
+    if (act) {
+      const double *Lk = &Ls[k & 3][0][0], *Lm = &Ls[(k - 1) & 3][0][0], *Lp = &Ls[(k + 1) & 3][0][0];
+      const long idx = col + (long)k * g.sz;
+      const double2 uc = *reinterpret_cast<const double2 *>(Lk + lr * kRlCols + lc);
+      const double2 um = *reinterpret_cast<const double2 *>(Lm + lr * kRlCols + lc);
+      const double2 up = *reinterpret_cast<const double2 *>(Lp + lr * kRlCols + lc);
+      const double xl = Lk[lr * kRlCols + lc - 1], xr = Lk[lr * kRlCols + lc + 2];
+      const double2 ym = *reinterpret_cast<const double2 *>(Lk + (lr - 1) * kRlCols + lc);
+      const double2 yp = *reinterpret_cast<const double2 *>(Lk + (lr + 1) * kRlCols + lc);
+      const double2 rv = ld2n<NT & 1>(rhs + idx), av = ld2n<NT & 1>(a + idx);
+      const double2 bv = BC ? make_double2(s.bval, s.bval) : ld2n<NT & 1>(b + idx);
+      auto cell = [&](double c, double xm, double xp, double ymv, double ypv, double zm, double zp,
+                      double rr, double aa, double bb, bool bxm, bool bxp) {
+        if (bxm) xm = ghost_of(g.bcm[0], g.bcc[0], c);
+        if (bxp) xp = ghost_of(g.bcm[1], g.bcc[1], c);
+        if (fy0) ymv = ghost_of(g.bcm[2], g.bcc[2], c);
+        if (fy1) ypv = ghost_of(g.bcm[3], g.bcc[3], c);
+        if (k == 0 && g.bcm[4]) zm = ghost_of(g.bcm[4], g.bcc[4], c);
+        if (k == g.nz - 1 && g.bcm[5]) zp = ghost_of(g.bcm[5], g.bcc[5], c);
+        const double res = rr - s.alpha * aa * c;            // .ChF:314-316
+        const double tx = (xp + xm) - 2.0 * c;
+        const double ty = (ypv + ymv) - 2.0 * c;
+        const double tz = (zp + zm) - 2.0 * c;
+        double ldpsi = (tx + ty) + tz;                       // .ChF:320-329
+        ldpsi = ldpsi * s.dxinv * s.beta * bb;               // .ChF:331
+        return (RT)(res + ldpsi);                            // .ChF:333
+      };
+      const RT r0 = cell(uc.x, xl, uc.y, ym.x, yp.x, um.x, up.x, rv.x, av.x, bv.x, fx0, fx1a);
+      const RT r1 = cell(uc.y, uc.x, xr, ym.y, yp.y, um.y, up.y, rv.y, av.y, bv.y, false, fx1b);
+      if (two) {
+        V2<RT> w;
+        w.x = r0;
+        w.y = r1;
+        st2n<(NT & 2) != 0>(r + idx, w);
+      } else {
+        r[idx] = r0;
+      }
+      if constexpr (NRM) {
+        nmax = red_op<3>(nmax, fabs((double)r0));
+        if (two) nmax = red_op<3>(nmax, fabs((double)r1));
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (NRM) {
+    __shared__ double sm[TY];
+    for (int o = 32; o > 0; o >>= 1) nmax = red_op<3>(nmax, __shfl_xor(nmax, o, 64));
+    if (threadIdx.x == 0) sm[threadIdx.y] = nmax;
+    __syncthreads();
+    if (threadIdx.x == 0 && threadIdx.y == 0) {
+      double m = sm[0];
+      for (int w = 1; w < TY; ++w) m = red_op<3>(m, sm[w]);
+      partials[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] = m;
+    }
+  }
+}
+
 template <class T, bool BC, int NT = 0>
 __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxArgs cg,
                                                   const T *__restrict__ u,
@@ -1263,6 +1385,14 @@ void apply_op(double *lu, const double *u, const double *a, const double *b, con
   check_launch();
 }
 
+static bool residual_lds() {  // (measurement) MGIC_RESIDUAL_ZL=1: k_residual_zl
+  static const bool v = [] {
+    const char *e = getenv("MGIC_RESIDUAL_ZL");
+    return e && atoi(e) > 0;
+  }();
+  return v;
+}
+
 void residual(double *r, const double *u, const double *rhs, const double *a, const double *b,
               const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
@@ -1284,7 +1414,10 @@ void residual(double *r, const double *u, const double *rhs, const double *a, co
     }();
 #define MGIC_RZ2(N)                                                                        \
   do {                                                                                     \
-    if (s.bconst) k_residual_z2<true, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+    if (residual_lds()) {                                                                  \
+      if (s.bconst) k_residual_zl<true, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+      else k_residual_zl<false, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
+    } else if (s.bconst) k_residual_z2<true, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
     else k_residual_z2<false, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
   } while (0)
     switch (nt & 3) {
@@ -1334,7 +1467,12 @@ void residual_norm(double *r, const double *u, const double *rhs, const double *
   grid.z = (unsigned)((g.nz + kc - 1) / kc);
   // the default streams of residual() (MGIC_RESIDUAL_NT = 3: rhs / aCoef
   // loads and r stores non-temporal)
-  if (s.bconst)
+  if (residual_lds()) {
+    if (s.bconst)
+      k_residual_zl<true, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
+    else
+      k_residual_zl<false, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
+  } else if (s.bconst)
     k_residual_z2<true, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
   else
     k_residual_z2<false, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
@@ -1615,7 +1753,10 @@ void residual_to_f(float *r, const double *u, const double *rhs, const double *a
   // every value of MGIC_RESIDUAL_NT & 3, for both bCoef kinds, as residual()
 #define MGIC_RZ2F(N)                                                                        \
   do {                                                                                      \
-    if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+    if (residual_lds()) {                                                                   \
+      if (s.bconst) k_residual_zl<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+      else k_residual_zl<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
+    } else if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
     else k_residual_z2<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
   } while (0)
   switch (nt & 3) {
