@@ -1385,21 +1385,23 @@ void apply_op(double *lu, const double *u, const double *a, const double *b, con
   check_launch();
 }
 
-static bool residual_lds() {  // (measurement) MGIC_RESIDUAL_ZL=1: k_residual_zl
+// the fp64 residual on LDS-staged u planes (k_residual_zl) in 32-plane
+// chunks: 512^3 0.800 -> 0.775 ms, 256^3 0.100 -> 0.092, V-cycle +0.4%
+// (profiles/r05s_residual_lds_ab.txt); MGIC_RESIDUAL_ZL=0: k_residual_z2
+static bool residual_lds() {
   static const bool v = [] {
     const char *e = getenv("MGIC_RESIDUAL_ZL");
-    return e && atoi(e) > 0;
+    return !(e && atoi(e) == 0);
   }();
   return v;
 }
 
+static int residual_kc_env();
+
 void residual(double *r, const double *u, const double *rhs, const double *a, const double *b,
               const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  static const int mode = [] {
-    const char *e = getenv("MGIC_RESIDUAL_KC");
-    return e ? atoi(e) : 16;
-  }();
+  const int mode = residual_kc_env();
   static const int pairs = [] {
     const char *e = getenv("MGIC_RESIDUAL_PAIRS");
     return e ? atoi(e) : 1;
@@ -1444,7 +1446,7 @@ void residual(double *r, const double *u, const double *rhs, const double *a, co
 static int residual_kc_env() {
   static const int mode = [] {
     const char *e = getenv("MGIC_RESIDUAL_KC");
-    return e ? atoi(e) : 16;
+    return e ? atoi(e) : (residual_lds() ? 32 : 16);
   }();
   return mode;
 }
@@ -1753,10 +1755,7 @@ void residual_to_f(float *r, const double *u, const double *rhs, const double *a
   // every value of MGIC_RESIDUAL_NT & 3, for both bCoef kinds, as residual()
 #define MGIC_RZ2F(N)                                                                        \
   do {                                                                                      \
-    if (residual_lds()) {                                                                   \
-      if (s.bconst) k_residual_zl<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
-      else k_residual_zl<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
-    } else if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+    if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
     else k_residual_z2<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
   } while (0)
   switch (nt & 3) {
