@@ -689,102 +689,6 @@ __global__ __launch_bounds__(256) void k_prolong(T *__restrict__ uf, const BoxAr
     }
 }
 
-// The linear prolongation with the coarse planes staged in LDS: a workgroup
-// owns 64 x 4 coarse columns over a chunk of coarse planes; each coarse plane
-// (with its one-cell halo: 6 rows x 68 columns) is loaded once with 16-B
-// loads into a 4-slot ring (the next one prefetched into registers), so a
-// coarse value is no longer fetched through the L1 by the seven threads that
-// read it.  The fine read-modify-writes and every expression are
-// k_prolong<double, 1>'s, so the same bits.
-constexpr int kPzCols = 68, kPzRows = 6, kPzPairs = kPzRows * kPzCols / 2;  // 204
-__global__ __launch_bounds__(256) void k_prolong_zl(double *__restrict__ uf, const BoxArgs fg,
-                                                    const double *__restrict__ ec,
-                                                    const BoxArgs cg, const ProlongArgs pa,
-                                                    int kc) {
-  __shared__ double Ls[4][kPzRows][kPzCols];
-  const int tid = threadIdx.x + TX * threadIdx.y;
-  const int cx0 = blockIdx.x * TX, cy0 = blockIdx.y * TY;
-  const int ci = cx0 + threadIdx.x, cj = cy0 + threadIdx.y;
-  const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, cg.nz);
-  long poff = 0;
-  int pl = -1;
-  {
-    const int q = tid;
-    const int rr = q / (kPzCols / 2), m = q - rr * (kPzCols / 2);
-    const int y = min(cy0 - 1 + rr, cg.ny + 1), x = min(cx0 - 2 + 2 * m, cg.nx & ~1);
-    poff = (long)x + (long)y * cg.sy;
-    pl = q < kPzPairs ? rr * kPzCols + 2 * m : -1;
-  }
-  V2<double> pre;
-  auto fetch = [&](int k) {
-    if (pl >= 0) pre = ld2(ec + (long)min(k, cg.nz + 1) * cg.sz + poff);
-  };
-  auto put = [&](int k) {
-    if (pl >= 0) *reinterpret_cast<V2<double> *>(&Ls[k & 3][0][0] + pl) = pre;
-  };
-  fetch(k0 - 1);
-  put(k0 - 1);
-  fetch(k0);
-  put(k0);
-  fetch(k0 + 1);
-  put(k0 + 1);
-  fetch(k0 + 2);
-  __syncthreads();
-  const bool act = ci < cg.nx && cj < cg.ny;
-  const int lr = threadIdx.y + 1, lc = threadIdx.x + 2;
-  for (int ck = k0; ck < k1; ++ck) {
-    put(ck + 2);  // (slot of plane ck - 2, last read in the previous step)
-    if (ck + 3 < k1 + 2) fetch(ck + 3);
-    if (act) {
-      const double *Lk = &Ls[ck & 3][0][0];
-      const double c0 = Lk[lr * kPzCols + lc];
-      const double lo[3] = {Lk[lr * kPzCols + lc - 1], Lk[(lr - 1) * kPzCols + lc],
-                            Ls[(ck - 1) & 3][lr][lc]};
-      const double hi[3] = {Lk[lr * kPzCols + lc + 1], Lk[(lr + 1) * kPzCols + lc],
-                            Ls[(ck + 1) & 3][lr][lc]};
-      double dlo[3], dhi[3];
-      bool ok[3];
-      const int ic[3] = {ci, cj, ck};
-      const int cn[3] = {cg.nx, cg.ny, cg.nz};
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const bool has_lo = (ic[d] > 0) || pa.avail_lo[d];
-        const bool has_hi = (ic[d] < cn[d] - 1) || pa.avail_hi[d];
-        ok[d] = has_lo || has_hi;
-        const double sl_hi = hi[d] - c0, sl_lo = c0 - lo[d];
-        dhi[d] = (has_hi ? sl_hi : sl_lo) * 0.25;    // upper child: +0.25 * slope
-        dlo[d] = (!has_lo ? sl_hi : sl_lo) * -0.25;  // lower child: -0.25 * slope
-      }
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const long row = (long)(2 * ci) + (long)(2 * cj + jj) * fg.sy + (long)(2 * ck + kk) * fg.sz;
-          V2<double> v = ld2(uf + row);
-          double e0 = c0, e1 = c0;
-          if (ok[0]) {
-            e0 = e0 + dlo[0];
-            e1 = e1 + dhi[0];
-          }
-          if (ok[1]) {
-            const double tt = jj ? dhi[1] : dlo[1];
-            e0 = e0 + tt;
-            e1 = e1 + tt;
-          }
-          if (ok[2]) {
-            const double tt = kk ? dhi[2] : dlo[2];
-            e0 = e0 + tt;
-            e1 = e1 + tt;
-          }
-          v.x = v.x + e0;
-          v.y = v.y + e1;
-          *reinterpret_cast<V2<double> *>(uf + row) = v;
-        }
-    }
-    __syncthreads();
-  }
-}
-
 __global__ __launch_bounds__(256) void k_lambda(double *__restrict__ lam,
                                                 const double *__restrict__ a, const BoxArgs g,
                                                 const StencilCoefs s) {
@@ -1628,18 +1532,6 @@ void prolong(double *uf, const BoxArgs &fg, const double *ec, const BoxArgs &cg,
   }
   MGIC_CHECK(fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz,
              "prolong: fine box must be the coarse box refined by 2");
-  static const int zl = [] {  // (measurement) MGIC_PROLONG_ZL = the z chunk (0: k_prolong)
-    const char *e = getenv("MGIC_PROLONG_ZL");
-    return e ? atoi(e) : 0;
-  }();
-  if (type == 1 && zl > 0) {
-    const int kc = zl < cg.nz ? zl : cg.nz;
-    dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
-    grid.z = (unsigned)((cg.nz + kc - 1) / kc);
-    k_prolong_zl<<<grid, kBlock, 0, st>>>(uf, fg, ec, cg, pa, kc);
-    check_launch();
-    return;
-  }
   if (type == 1)
     k_prolong<double, 1><<<grid_cells(cg.nx, cg.ny, cg.nz), kBlock, 0, st>>>(uf, fg, ec, cg, pa);
   else
