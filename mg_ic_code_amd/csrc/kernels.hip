@@ -1745,7 +1745,12 @@ void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStrea
 void residual_to_f(float *r, const double *u, const double *rhs, const double *a, const double *b,
                    const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  const int kc = 16 < g.nz ? 16 : g.nz;
+  static const int fzl = [] {  // (measurement) MGIC_RESIDUAL_F_ZL = chunk of k_residual_zl<float>
+    const char *e = getenv("MGIC_RESIDUAL_F_ZL");
+    return e ? atoi(e) : 0;
+  }();
+  const int kc0 = fzl > 0 ? fzl : 16;
+  const int kc = kc0 < g.nz ? kc0 : g.nz;
   dim3 grid = grid_cells((g.nx + 1) / 2, g.ny, g.nz);
   grid.z = (unsigned)((g.nz + kc - 1) / kc);
   static const int nt = [] {  // as residual(): MGIC_RESIDUAL_NT, default 3
@@ -1755,7 +1760,10 @@ void residual_to_f(float *r, const double *u, const double *rhs, const double *a
   // every value of MGIC_RESIDUAL_NT & 3, for both bCoef kinds, as residual()
 #define MGIC_RZ2F(N)                                                                        \
   do {                                                                                      \
-    if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+    if (fzl > 0) {                                                                          \
+      if (s.bconst) k_residual_zl<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
+      else k_residual_zl<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
+    } else if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
     else k_residual_z2<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
   } while (0)
   switch (nt & 3) {
