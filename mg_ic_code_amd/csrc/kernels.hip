@@ -1745,9 +1745,12 @@ void incr_grown(double *x, const double *y, const BoxArgs &g, int grow, hipStrea
 void residual_to_f(float *r, const double *u, const double *rhs, const double *a, const double *b,
                    const BoxArgs &g, const StencilCoefs &s, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
-  static const int fzl = [] {  // (measurement) MGIC_RESIDUAL_F_ZL = chunk of k_residual_zl<float>
+  // k_residual_zl<float> in 16-plane chunks by default (MGIC_RESIDUAL_F_ZL;
+  // 0: k_residual_z2): 1024^3 mixed V-cycle 33.4 -> 32.8 ms
+  // (profiles/r05u_residual_f_lds_ab.txt)
+  static const int fzl = [] {
     const char *e = getenv("MGIC_RESIDUAL_F_ZL");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 16;
   }();
   const int kc0 = fzl > 0 ? fzl : 16;
   const int kc = kc0 < g.nz ? kc0 : g.nz;
