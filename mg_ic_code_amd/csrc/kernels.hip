@@ -505,16 +505,16 @@ __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxA
 // (profiles/r05q_stream_pmc.txt); short chunks (2 coarse planes) keep the
 // grid large, longer ones re-read fewer halo planes but ran slower.
 constexpr int kRzCols = 132, kRzRows = 10, kRzPairs = kRzRows * kRzCols / 2;  // 660
-template <bool BC, int NT>
-__global__ __launch_bounds__(256) void k_restrict_zl(double *__restrict__ rc, const BoxArgs cg,
-                                                     const double *__restrict__ u,
-                                                     const double *__restrict__ rhs,
-                                                     const double *__restrict__ a,
-                                                     const double *__restrict__ b, const BoxArgs fg,
+template <class T, bool BC, int NT>
+__global__ __launch_bounds__(256) void k_restrict_zl(T *__restrict__ rc, const BoxArgs cg,
+                                                     const T *__restrict__ u,
+                                                     const T *__restrict__ rhs,
+                                                     const T *__restrict__ a,
+                                                     const T *__restrict__ b, const BoxArgs fg,
                                                      const StencilCoefs s64, int accumulate, int kc,
                                                      int ntx, int nty) {
-  __shared__ double Ls[4][kRzRows][kRzCols];
-  const SC<double> s(s64);
+  __shared__ T Ls[4][kRzRows][kRzCols];
+  const SC<T> s(s64);
   const int ntile = ntx * nty;
   const int tile = blockIdx.x % ntile, chunk = blockIdx.x / ntile;
   const int cx0 = (tile % ntx) * TX, cy0 = (tile / ntx) * 4;
@@ -537,18 +537,18 @@ __global__ __launch_bounds__(256) void k_restrict_zl(double *__restrict__ rc, co
     pl[i] = q < kRzPairs ? r * kRzCols + 2 * m : -1;
   }
   auto plane_ptr = [&](int k) { return u + (long)min(k, fg.nz + 1) * fg.sz; };
-  V2<double> pre[2][3];
+  V2<T> pre[2][3];
   auto fetch = [&](int k, int h) {
-    const double *p = plane_ptr(k);
+    const T *p = plane_ptr(k);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       if (pl[i] >= 0) pre[h][i] = ld2(p + poff[i]);
   };
   auto put = [&](int k, int h) {
-    double *dst = &Ls[k & 3][0][0];
+    T *dst = &Ls[k & 3][0][0];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
-      if (pl[i] >= 0) *reinterpret_cast<V2<double> *>(dst + pl[i]) = pre[h][i];
+      if (pl[i] >= 0) *reinterpret_cast<V2<T> *>(dst + pl[i]) = pre[h][i];
   };
   fetch(2 * k0 - 1, 0);
   fetch(2 * k0, 1);
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(256) void k_restrict_zl(double *__restrict__ rc, co
   put(2 * k0 + 1, 0);
   put(2 * k0 + 2, 1);
   __syncthreads();
-  const double denom = (double)(2 * 2 * 2);  // .ChF:402
+  const T denom = (T)(2 * 2 * 2);  // .ChF:402
   for (int ck = k0; ck < k1; ++ck) {
     const bool more = ck + 1 < k1;
     if (more) {
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) void k_restrict_zl(double *__restrict__ rc, co
     }
     if (act) {
       const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
-      double sum = accumulate ? rc[cidx] : 0.0;
+      T sum = accumulate ? rc[cidx] : (T)0;
       const int i0 = 2 * ci;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -576,37 +576,37 @@ __global__ __launch_bounds__(256) void k_restrict_zl(double *__restrict__ rc, co
         for (int jj = 0; jj < 2; ++jj) {
           const int j = 2 * cj + jj, k = 2 * ck + kk;
           const int r = 2 * w + jj + 1, cx = 2 * lane + 2;
-          const double *Lk = &Ls[k & 3][0][0], *Lm = &Ls[(k - 1) & 3][0][0],
+          const T *Lk = &Ls[k & 3][0][0], *Lm = &Ls[(k - 1) & 3][0][0],
                        *Lp = &Ls[(k + 1) & 3][0][0];
-          const V2<double> c = *reinterpret_cast<const V2<double> *>(Lk + r * kRzCols + cx);
-          const V2<double> ym = *reinterpret_cast<const V2<double> *>(Lk + (r - 1) * kRzCols + cx);
-          const V2<double> yp = *reinterpret_cast<const V2<double> *>(Lk + (r + 1) * kRzCols + cx);
-          const V2<double> zm = *reinterpret_cast<const V2<double> *>(Lm + r * kRzCols + cx);
-          const V2<double> zp = *reinterpret_cast<const V2<double> *>(Lp + r * kRzCols + cx);
-          const double xl = Lk[r * kRzCols + cx - 1], xr = Lk[r * kRzCols + cx + 2];
+          const V2<T> c = *reinterpret_cast<const V2<T> *>(Lk + r * kRzCols + cx);
+          const V2<T> ym = *reinterpret_cast<const V2<T> *>(Lk + (r - 1) * kRzCols + cx);
+          const V2<T> yp = *reinterpret_cast<const V2<T> *>(Lk + (r + 1) * kRzCols + cx);
+          const V2<T> zm = *reinterpret_cast<const V2<T> *>(Lm + r * kRzCols + cx);
+          const V2<T> zp = *reinterpret_cast<const V2<T> *>(Lp + r * kRzCols + cx);
+          const T xl = Lk[r * kRzCols + cx - 1], xr = Lk[r * kRzCols + cx + 2];
           const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
-          const V2<double> rv = ld2n<NT & 1>(rhs + row), av = ld2n<NT & 1>(a + row);
-          V2<double> bv;
+          const V2<T> rv = ld2n<NT & 1>(rhs + row), av = ld2n<NT & 1>(a + row);
+          V2<T> bv;
           if (BC) bv.x = bv.y = s.bval;
           else bv = ld2n<NT & 1>(b + row);
 #pragma unroll
           for (int ii = 0; ii < 2; ++ii) {
             const int i = i0 + ii;
-            const double uc = ii ? c.y : c.x;
-            double vxm = ii ? c.x : xl, vxp = ii ? xr : c.y;
-            double vym = ii ? ym.y : ym.x, vyp = ii ? yp.y : yp.x;
-            double vzm = ii ? zm.y : zm.x, vzp = ii ? zp.y : zp.x;
-            if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], fg.bcc[0], uc);
-            if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], fg.bcc[1], uc);
-            if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], fg.bcc[2], uc);
-            if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], fg.bcc[3], uc);
-            if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], fg.bcc[4], uc);
-            if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], fg.bcc[5], uc);
-            const double tx = (vxp + vxm) - 2.0 * uc;
-            const double ty = (vyp + vym) - 2.0 * uc;
-            const double tz = (vzp + vzm) - 2.0 * uc;
-            double ldpsi = (tx + ty) + tz;                                  // .ChF:416-425
-            double lofdpsi = s.alpha * (ii ? av.y : av.x) * uc;            // .ChF:411-412
+            const T uc = ii ? c.y : c.x;
+            T vxm = ii ? c.x : xl, vxp = ii ? xr : c.y;
+            T vym = ii ? ym.y : ym.x, vyp = ii ? yp.y : yp.x;
+            T vzm = ii ? zm.y : zm.x, vzp = ii ? zp.y : zp.x;
+            if (i == 0 && fg.bcm[0]) vxm = ghost_of(fg.bcm[0], (T)fg.bcc[0], uc);
+            if (i == fg.nx - 1 && fg.bcm[1]) vxp = ghost_of(fg.bcm[1], (T)fg.bcc[1], uc);
+            if (j == 0 && fg.bcm[2]) vym = ghost_of(fg.bcm[2], (T)fg.bcc[2], uc);
+            if (j == fg.ny - 1 && fg.bcm[3]) vyp = ghost_of(fg.bcm[3], (T)fg.bcc[3], uc);
+            if (k == 0 && fg.bcm[4]) vzm = ghost_of(fg.bcm[4], (T)fg.bcc[4], uc);
+            if (k == fg.nz - 1 && fg.bcm[5]) vzp = ghost_of(fg.bcm[5], (T)fg.bcc[5], uc);
+            const T tx = (vxp + vxm) - (T)2 * uc;
+            const T ty = (vyp + vym) - (T)2 * uc;
+            const T tz = (vzp + vzm) - (T)2 * uc;
+            T ldpsi = (tx + ty) + tz;                                  // .ChF:416-425
+            T lofdpsi = s.alpha * (ii ? av.y : av.x) * uc;            // .ChF:411-412
             ldpsi = ldpsi * s.dxinv * s.beta * (ii ? bv.y : bv.x);         // .ChF:427
             lofdpsi = lofdpsi - ldpsi;                                      // .ChF:429
             sum = sum + ((ii ? rv.y : rv.x) - lofdpsi) / denom;             // .ChF:431-432
@@ -1504,9 +1504,9 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
     const int kc = zl < cg.nz ? zl : cg.nz;
     const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
     if (s.bconst)
-      k_restrict_zl<true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
+      k_restrict_zl<double, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
     else
-      k_restrict_zl<false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
+      k_restrict_zl<double, false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
     check_launch();
     return;
   }
@@ -1787,6 +1787,21 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
     const char *e = getenv("MGIC_RESTRICT_NT");
     return e ? atoi(e) : 1;
   }();
+  static const int fzl = [] {  // (measurement) MGIC_RESTRICT_F_ZL = chunk of k_restrict_zl<float>
+    const char *e = getenv("MGIC_RESTRICT_F_ZL");
+    return e ? atoi(e) : 0;
+  }();
+  if (fzl > 0 && (nt & 1) && fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz) {
+    const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
+    const int kc = fzl < cg.nz ? fzl : cg.nz;
+    const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
+    if (s.bconst)
+      k_restrict_zl<float, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty);
+    else
+      k_restrict_zl<float, false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty);
+    check_launch();
+    return;
+  }
   const dim3 grid = grid_cells(cg.nx, cg.ny, cg.nz);
   if (s.bconst && (nt & 1))
     k_restrict<float, true, 1><<<grid, kBlock, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0);
