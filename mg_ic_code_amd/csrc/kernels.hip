@@ -1787,9 +1787,12 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
     const char *e = getenv("MGIC_RESTRICT_NT");
     return e ? atoi(e) : 1;
   }();
-  static const int fzl = [] {  // (measurement) MGIC_RESTRICT_F_ZL = chunk of k_restrict_zl<float>
+  // k_restrict_zl<float>, two coarse planes per workgroup (MGIC_RESTRICT_F_ZL;
+  // 0: k_restrict): 1024^3 mixed V-cycle 32.6 -> 32.0 ms, FMG 45.4 -> 44.1
+  // (profiles/r05v_restrict_f_lds_ab.txt)
+  static const int fzl = [] {
     const char *e = getenv("MGIC_RESTRICT_F_ZL");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   if (fzl > 0 && (nt & 1) && fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz) {
     const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
