@@ -293,6 +293,44 @@ def test_pipelined_iterations_match_iteration_calls(comm, rng, parts, deep, bott
     assert np.array_equal(download_global(fres2, grid, shp), download_global(S["fres"], grid, shp))
 
 
+@pytest.mark.parametrize("bvar", [False, True])
+def test_lds_staged_residual_restriction_odd_shapes_bitwise(rng, comm, bvar):
+    """The LDS-staged residual and restriction (k_residual_zl, k_restrict_zl:
+    64 x 4 coarse / 128 x 4 fine tiles, 2- and 32-plane chunks) on a box none
+    of whose sides fills a tile or a chunk, with odd coarse sides: a 2-level
+    V-cycle at an odd offset with Dirichlet / Neumann faces, bit for bit
+    against the oracle, norms included."""
+    shape = (70, 38, 46)  # coarse 35 x 19 x 23
+    lo = (3, -5, 7)
+    dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
+    dx = 0.29
+    bc_lo, bc_hi, bcv = (0, 1, 0), (1, 0, 0), 0.0
+    nz, ny, nx = shape[2], shape[1], shape[0]
+    a = rng.uniform(-2.0, -0.5, (nz, ny, nx))
+    b = rng.uniform(0.5, 2.0, (nz, ny, nx)) if bvar else np.ones((nz, ny, nx))
+    rhs = rng.uniform(-1, 1, (nz, ny, nx))
+    grid = mg.Grid(comm, dom, [dom], dx)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    fa.upload(0, a)
+    fb.upload(0, b)
+    frhs.upload(0, rhs)
+    fphi.set_zero()
+    prm = mg.OperatorParams(alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi, bc_value=bcv,
+                            coefficient_average_type=1, prolong_type=1)
+    amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, prm),
+                          mg.SolverParams(max_depth=1, bottom_solver=0))
+    o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi,
+                        bc_value=bcv, nlevels=2, avg_type=1, prolong_type=1, bottom_solver=0)
+    for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs)):
+        o.set(0, f, 0, arr)
+    o.setup()
+    amg.init_residual(fphi, frhs, fres)
+    o.init_residual(0)
+    for _ in range(3):
+        assert amg.iteration(fphi, frhs, fres, 0) == o.iteration(0)
+    assert np.array_equal(fphi.download(0), o.get(0, oracle.PHI, 0))
+
+
 @pytest.mark.parametrize("fused", [2, 3])
 @pytest.mark.parametrize("bvar", [False, True])
 def test_vcycle_ragged_mixed_bc_bitwise(rng, comm, fused, bvar):
