@@ -297,11 +297,11 @@ def test_pipelined_iterations_match_iteration_calls(comm, rng, parts, deep, bott
 def test_lds_staged_residual_restriction_odd_shapes_bitwise(rng, comm, bvar):
     """The LDS-staged residual and restriction (k_residual_zl, k_restrict_zl:
     64 x 4 coarse / 128 x 4 fine tiles, 2- and 32-plane chunks) on a box none
-    of whose sides fills a tile or a chunk, with odd coarse sides: a 2-level
-    V-cycle at an odd offset with Dirichlet / Neumann faces, bit for bit
-    against the oracle, norms included."""
-    shape = (70, 38, 46)  # coarse 35 x 19 x 23
-    lo = (3, -5, 7)
+    of whose sides fills a tile, a row group or a chunk: a 2-level V-cycle off
+    the origin with Dirichlet / Neumann faces, bit for bit against the oracle,
+    norms included."""
+    shape = (76, 44, 52)  # coarse 38 x 22 x 26 (MGnewOp needs the box coarsenable by 4)
+    lo = (8, -12, 16)
     dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
     dx = 0.29
     bc_lo, bc_hi, bcv = (0, 1, 0), (1, 0, 0), 0.0
@@ -319,6 +319,7 @@ def test_lds_staged_residual_restriction_odd_shapes_bitwise(rng, comm, bvar):
                             coefficient_average_type=1, prolong_type=1)
     amg = mg.AMRMultiGrid(mg.defineOperatorFactory(grid, fa, fb, prm),
                           mg.SolverParams(max_depth=1, bottom_solver=0))
+    assert amg.num_depths == 2
     o = oracle.OracleMG([dom], dom, dx, alpha=1.0, beta=-1.0, bc_lo=bc_lo, bc_hi=bc_hi,
                         bc_value=bcv, nlevels=2, avg_type=1, prolong_type=1, bottom_solver=0)
     for f, arr in ((oracle.ACOEF, a), (oracle.BCOEF, b), (oracle.RHS, rhs)):
