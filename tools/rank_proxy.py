@@ -184,11 +184,35 @@ def split_share(mg, comm, amg, prm, args, shp, parts, ms, n_x):
     lat = n_x * (1.0 - 1.0 / P) * t_x
     share = (ms - t_b) / P + t_b + lat
     floor = xgmi_floor_ms(shp[0] // parts[0], D)
-    return {"split_boxes": P, "gathered_bottom_ms": round(t_b, 4),
-            "exchanges_per_vcycle": round(n_x, 2), "exchange_fixed_ms": round(t_x, 4),
-            "exchange_latency_charge_ms": round(lat, 4),
-            "share_ms_per_vcycle": round(share, 4), "xgmi_floor_ms": round(floor, 4),
-            "share_charged_ms_per_vcycle": round(share + floor, 4)}
+    out = {"split_boxes": P, "gathered_bottom_ms": round(t_b, 4),
+           "exchanges_per_vcycle": round(n_x, 2), "exchange_fixed_ms": round(t_x, 4),
+           "exchange_latency_charge_ms": round(lat, 4),
+           "share_ms_per_vcycle": round(share, 4), "xgmi_floor_ms": round(floor, 4),
+           "share_charged_ms_per_vcycle": round(share + floor, 4)}
+    # the same charge with t_x as the device sees it (t_x above is the host
+    # loop's rate, Python and ctypes included): HIP events around 50
+    # exchanges queued behind 16 sweeps of depth 1, so the device runs them
+    # back to back
+    e1, r1 = amg.level_field(1, 0), amg.level_field(1, 1)
+    t_xg = gpu_timed_ms(comm, lambda: amg.op(1).relax(e1, r1, 16), e_d.exchange, 50)
+    if t_xg is not None:
+        lat_g = n_x * (1.0 - 1.0 / P) * t_xg
+        out.update({"exchange_fixed_gpu_ms": round(t_xg, 4),
+                    "share_gpu_charge_ms_per_vcycle": round((ms - t_b) / P + t_b + lat_g, 4)})
+    # t_x above still moves all N boxes' messages of depth D - 1 (128^3
+    # boxes: ~3 MB), whose bytes t / N already holds; the fixed cost alone is
+    # the same split's exchange on 16^3 boxes (messages of a few KB)
+    from mg_ic_code_amd.decomposition import split_domain
+    dom = tuple([0, 0, 0] + [16 * q - 1 for q in parts])
+    g0 = mg.Grid(comm, dom, split_domain(dom, parts), 1.0 / (16 * parts[0]), periodic=(0, 0, 0))
+    f0 = mg.LevelData(g0)
+    f0.set_zero()
+    t_x0 = gpu_timed_ms(comm, lambda: amg.op(1).relax(e1, r1, 16), f0.exchange, 50)
+    if t_x0 is not None:
+        lat0 = n_x * (1.0 - 1.0 / P) * t_x0
+        out.update({"exchange_fixed_small_gpu_ms": round(t_x0, 4),
+                    "share_small_charge_ms_per_vcycle": round((ms - t_b) / P + t_b + lat0, 4)})
+    return out
 
 
 def timed_ms(comm, fn, reps):
@@ -199,6 +223,26 @@ def timed_ms(comm, fn, reps):
         fn()
     comm.synchronize()
     return (time.perf_counter() - t0) / reps * 1e3
+
+
+def gpu_timed_ms(comm, blocker, fn, reps):
+    """device time per call of fn, from HIP events on the library's stream
+    around reps calls queued while `blocker` still runs (None if the host
+    did not get ahead of the device, i.e. the events would time the host)"""
+    import torch
+    fn()
+    comm.synchronize()
+    s = torch.cuda.ExternalStream(comm.stream)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    blocker()
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    ahead = not a.query()  # the blocker was still running when the last call was queued
+    b.synchronize()
+    comm.synchronize()
+    return a.elapsed_time(b) / reps if ahead else None
 
 
 def charges(mg, comm, amg, prm, args, shp, ms):
