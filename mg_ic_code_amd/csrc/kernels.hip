@@ -355,6 +355,30 @@ __device__ __forceinline__ void restrict_cell(T *__restrict__ rc, const BoxArgs 
   rc[cidx] = sum;
 }
 
+// XCD-aware tile order for the LDS-staged streaming kernels: consecutive
+// workgroup ids go round-robin to the 8 XCDs, so in the dispatch order a
+// tile's x / y neighbours run on other XCDs and share none of their halo
+// rows through an L2.  In bands of S tiles: every group of 8 S ids takes 8
+// consecutive bands of the logical x-fastest order, one per XCD, so an XCD
+// streams runs of S neighbouring tiles (its L2 shares their halo rows) while
+// the 8 XCDs stay on neighbouring bands (the concurrent streams stay close
+// in memory, as in the dispatch order); ids past the last whole group keep
+// their place.  S = 0: the dispatch order.
+__device__ __forceinline__ unsigned xcd_order(unsigned bid, unsigned nb, unsigned S) {
+  if (S == 0) return bid;
+  const unsigned G = 8 * S, full = nb / G * G;
+  if (bid >= full) return bid;
+  const unsigned g = bid / G, j = bid - g * G;
+  return g * G + (j % 8) * S + j / 8;
+}
+// (x, y, z) tile of this workgroup: lg.w == 0, the 3D grid as launched;
+// else a 1D grid of lg.x * lg.y * lg.z ids in bands of lg.w tiles
+__device__ __forceinline__ uint3 tile_of(const uint4 lg) {
+  if (lg.w == 0) return make_uint3(blockIdx.x, blockIdx.y, blockIdx.z);
+  const unsigned L = xcd_order(blockIdx.x, gridDim.x, lg.w);
+  return make_uint3(L % lg.x, (L / lg.x) % lg.y, L / (lg.x * lg.y));
+}
+
 // k_residual_z2 with the u planes staged in LDS: the workgroup's 128 x 4
 // cells of a plane plus their one-cell halo (6 rows x 132 columns) go to a
 // 4-slot LDS ring, each row loaded once with 16-B loads (the next plane
@@ -369,12 +393,14 @@ __global__ __launch_bounds__(256) void k_residual_zl(RT *__restrict__ r,
                                                      const double *__restrict__ a,
                                                      const double *__restrict__ b, const BoxArgs g,
                                                      const StencilCoefs s, int kc,
-                                                     double *__restrict__ partials = nullptr) {
+                                                     double *__restrict__ partials = nullptr,
+                                                     const uint4 lg = uint4{0, 0, 0, 0}) {
   __shared__ double Ls[4][kRlRows][kRlCols];
+  const uint3 bt = tile_of(lg);
   const int tid = threadIdx.x + TX * threadIdx.y;
-  const int x0 = 2 * blockIdx.x * TX, y0 = blockIdx.y * TY;
+  const int x0 = 2 * (int)bt.x * TX, y0 = (int)bt.y * TY;
   const int i = x0 + 2 * threadIdx.x, j = y0 + threadIdx.y;
-  const int k0 = blockIdx.z * kc, k1 = min(k0 + kc, g.nz);
+  const int k0 = (int)bt.z * kc, k1 = min(k0 + kc, g.nz);
   // pair q of the staged plane: row q / 66 (cell y0 - 1 + row), pair q % 66
   // (cells x0 - 2 + 2 m, +1); clamped into the allocated ghosts (a clamped
   // pair is never read)
@@ -472,7 +498,8 @@ __global__ __launch_bounds__(256) void k_residual_zl(RT *__restrict__ r,
     if (threadIdx.x == 0 && threadIdx.y == 0) {
       double m = sm[0];
       for (int w = 1; w < TY; ++w) m = red_op<3>(m, sm[w]);
-      partials[blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)] = m;
+      const unsigned gx = lg.w ? lg.x : gridDim.x, gy = lg.w ? lg.y : gridDim.y;
+      partials[bt.x + gx * (bt.y + gy * bt.z)] = m;
     }
   }
 }
@@ -512,11 +539,15 @@ __global__ __launch_bounds__(256) void k_restrict_zl(T *__restrict__ rc, const B
                                                      const T *__restrict__ a,
                                                      const T *__restrict__ b, const BoxArgs fg,
                                                      const StencilCoefs s64, int accumulate, int kc,
-                                                     int ntx, int nty) {
+                                                     int ntx, int nty, int xcd = 0) {
   __shared__ T Ls[4][kRzRows][kRzCols];
   const SC<T> s(s64);
   const int ntile = ntx * nty;
-  const int tile = blockIdx.x % ntile, chunk = blockIdx.x / ntile;
+  // xcd > 0: bands of xcd tiles in the x-fastest, chunk-slowest order; < 0:
+  // bands of -xcd in the chunk-fastest order (a tile's z chunks together)
+  const int bid = (int)xcd_order(blockIdx.x, gridDim.x, (unsigned)(xcd < 0 ? -xcd : xcd));
+  const int nch = (int)gridDim.x / ntile;
+  const int tile = xcd < 0 ? bid / nch : bid % ntile, chunk = xcd < 0 ? bid % nch : bid / ntile;
   const int cx0 = (tile % ntx) * TX, cy0 = (tile / ntx) * 4;
   const int k0 = chunk * kc, k1 = min(k0 + kc, cg.nz);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1215,6 +1246,37 @@ inline void check_launch() {
   if (e != hipSuccess) throw Error(kHipErr, std::string("kernel launch: ") + hipGetErrorString(e));
 }
 
+// the LDS-staged residual (MGIC_RESIDUAL_XCD) and restriction
+// (MGIC_RESTRICT_XCD) in XCD bands of S tiles (xcd_order above; 0: the
+// dispatch order; the restriction's S < 0: chunk-fastest bands of -S).
+// The residual takes bands of 16 tiles (4 y rows of the 512^3 plane): its
+// HBM fetch 4.34 -> 3.41 GB per 512^3 launch, 0.782 -> 0.732 ms, 256^3
+// 0.093 -> 0.081 ms, V-cycle +1.3% (profiles/r05ad_xcd_bands_ab.txt); the
+// restriction measured neutral to slower in every band order: dispatch order
+static int residual_xcd() {
+  static const int v = [] {
+    const char *e = getenv("MGIC_RESIDUAL_XCD");
+    return e ? atoi(e) : 16;
+  }();
+  return v;
+}
+static int restrict_xcd() {
+  static const int v = [] {
+    const char *e = getenv("MGIC_RESTRICT_XCD");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+// a 3D tile grid as launched: itself, or 1D with its logical shape in lg
+inline dim3 xcd_grid(const dim3 &g, uint4 &lg) {
+  if (residual_xcd() <= 0) {
+    lg = uint4{0, 0, 0, 0};
+    return g;
+  }
+  lg = uint4{g.x, g.y, g.z, (unsigned)residual_xcd()};
+  return dim3(g.x * g.y * g.z);
+}
+
 // fp64 -> fp32 over the valid region grown by `grow` (coefficients of the
 // mixed-precision V-cycle); and a float box copy
 __global__ __launch_bounds__(256) void k_to_float(float *__restrict__ d, const double *__restrict__ s,
@@ -1417,8 +1479,10 @@ void residual(double *r, const double *u, const double *rhs, const double *a, co
 #define MGIC_RZ2(N)                                                                        \
   do {                                                                                     \
     if (residual_lds()) {                                                                  \
-      if (s.bconst) k_residual_zl<true, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
-      else k_residual_zl<false, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
+      uint4 lg;                                                                            \
+      const dim3 xg = xcd_grid(grid, lg);                                                  \
+      if (s.bconst) k_residual_zl<true, double, N><<<xg, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, nullptr, lg); \
+      else k_residual_zl<false, double, N><<<xg, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, nullptr, lg);         \
     } else if (s.bconst) k_residual_z2<true, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
     else k_residual_z2<false, double, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
   } while (0)
@@ -1470,10 +1534,12 @@ void residual_norm(double *r, const double *u, const double *rhs, const double *
   // the default streams of residual() (MGIC_RESIDUAL_NT = 3: rhs / aCoef
   // loads and r stores non-temporal)
   if (residual_lds()) {
+    uint4 lg;
+    const dim3 xg = xcd_grid(grid, lg);
     if (s.bconst)
-      k_residual_zl<true, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
+      k_residual_zl<true, double, 3, true><<<xg, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials, lg);
     else
-      k_residual_zl<false, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
+      k_residual_zl<false, double, 3, true><<<xg, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials, lg);
   } else if (s.bconst)
     k_residual_z2<true, double, 3, true><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, partials);
   else
@@ -1504,9 +1570,11 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
     const int kc = zl < cg.nz ? zl : cg.nz;
     const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
     if (s.bconst)
-      k_restrict_zl<double, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
+      k_restrict_zl<double, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty,
+                                                         restrict_xcd());
     else
-      k_restrict_zl<double, false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty);
+      k_restrict_zl<double, false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty,
+                                                          restrict_xcd());
     check_launch();
     return;
   }
@@ -1764,8 +1832,10 @@ void residual_to_f(float *r, const double *u, const double *rhs, const double *a
 #define MGIC_RZ2F(N)                                                                        \
   do {                                                                                      \
     if (fzl > 0) {                                                                          \
-      if (s.bconst) k_residual_zl<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
-      else k_residual_zl<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
+      uint4 lg;                                                                             \
+      const dim3 xg = xcd_grid(grid, lg);                                                   \
+      if (s.bconst) k_residual_zl<true, float, N><<<xg, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, nullptr, lg); \
+      else k_residual_zl<false, float, N><<<xg, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc, nullptr, lg);         \
     } else if (s.bconst) k_residual_z2<true, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc); \
     else k_residual_z2<false, float, N><<<grid, kBlock, 0, st>>>(r, u, rhs, a, b, g, s, kc);         \
   } while (0)
@@ -1799,9 +1869,11 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
     const int kc = fzl < cg.nz ? fzl : cg.nz;
     const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
     if (s.bconst)
-      k_restrict_zl<float, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty);
+      k_restrict_zl<float, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty,
+                                                        restrict_xcd());
     else
-      k_restrict_zl<float, false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty);
+      k_restrict_zl<float, false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty,
+                                                         restrict_xcd());
     check_launch();
     return;
   }
