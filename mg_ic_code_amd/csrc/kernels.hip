@@ -1251,7 +1251,7 @@ inline void check_launch() {
 // dispatch order; the restriction's S < 0: chunk-fastest bands of -S).
 // The residual takes bands of 16 tiles (4 y rows of the 512^3 plane): its
 // HBM fetch 4.34 -> 3.41 GB per 512^3 launch, 0.782 -> 0.732 ms, 256^3
-// 0.093 -> 0.081 ms, V-cycle +1.3% (profiles/r05ad_xcd_bands_ab.txt); the
+// 0.093 -> 0.081 ms, V-cycle +0.3..0.7% (profiles/r05ad_xcd_bands_ab.txt); the
 // restriction measured neutral to slower in every band order: dispatch order
 static int residual_xcd() {
   static const int v = [] {
