@@ -1251,8 +1251,11 @@ inline void check_launch() {
 // dispatch order; the restriction's S < 0: chunk-fastest bands of -S).
 // The residual takes bands of 16 tiles (4 y rows of the 512^3 plane): its
 // HBM fetch 4.34 -> 3.41 GB per 512^3 launch, 0.782 -> 0.732 ms, 256^3
-// 0.093 -> 0.081 ms, V-cycle +0.3..0.7% (profiles/r05ad_xcd_bands_ab.txt); the
-// restriction measured neutral to slower in every band order: dispatch order
+// 0.093 -> 0.081 ms, V-cycle +0.3..0.7% (profiles/r05ad_xcd_bands_ab.txt).  The
+// fp64 restriction takes bands of 16 with 4-plane chunks: HBM fetch 3.84 ->
+// 3.41 GB per 512^3 launch (1.19x -> 1.06x the compulsory reads) at the
+// same time (profiles/r05ah_restrict_chunk_band.txt: it is not bound by its
+// HBM bytes); the fp32 one keeps the dispatch order (MGIC_RESTRICT_F_XCD)
 static int residual_xcd() {
   static const int v = [] {
     const char *e = getenv("MGIC_RESIDUAL_XCD");
@@ -1263,6 +1266,13 @@ static int residual_xcd() {
 static int restrict_xcd() {
   static const int v = [] {
     const char *e = getenv("MGIC_RESTRICT_XCD");
+    return e ? atoi(e) : 16;
+  }();
+  return v;
+}
+static int restrict_f_xcd() {
+  static const int v = [] {
+    const char *e = getenv("MGIC_RESTRICT_F_XCD");
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -1560,10 +1570,11 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
   const int accu = accumulate ? 1 : 0;
   // k_restrict_zl, two coarse planes per workgroup (MGIC_RESTRICT_ZL: the
   // chunk; 0 = k_restrict).  512^3: 0.706 -> 0.641 ms, 256^3 equal, V-cycle
-  // +1.4% (chunks 1 .. 32 measured, profiles/r05r_restrict_lds_ab.txt)
+  // +1.4% (chunks 1 .. 32 measured, profiles/r05r_restrict_lds_ab.txt); 4
+  // planes in XCD bands since (restrict_xcd above)
   static const int zl = [] {
     const char *e = getenv("MGIC_RESTRICT_ZL");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 4;
   }();
   if (zl > 0 && (nt & 1) && fg.nx == 2 * cg.nx && fg.ny == 2 * cg.ny && fg.nz == 2 * cg.nz) {
     const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
@@ -1870,10 +1881,10 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
     const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
     if (s.bconst)
       k_restrict_zl<float, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty,
-                                                        restrict_xcd());
+                                                        restrict_f_xcd());
     else
       k_restrict_zl<float, false, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty,
-                                                         restrict_xcd());
+                                                         restrict_f_xcd());
     check_launch();
     return;
   }
