@@ -293,14 +293,18 @@ def test_pipelined_iterations_match_iteration_calls(comm, rng, parts, deep, bott
     assert np.array_equal(download_global(fres2, grid, shp), download_global(S["fres"], grid, shp))
 
 
+@pytest.mark.parametrize("shape", [(76, 44, 52), (256, 132, 64)])
 @pytest.mark.parametrize("bvar", [False, True])
-def test_lds_staged_residual_restriction_odd_shapes_bitwise(rng, comm, bvar):
+def test_lds_staged_residual_restriction_odd_shapes_bitwise(rng, comm, bvar, shape):
     """The LDS-staged residual and restriction (k_residual_zl, k_restrict_zl:
-    64 x 4 coarse / 128 x 4 fine tiles, 2- and 32-plane chunks) on a box none
-    of whose sides fills a tile, a row group or a chunk: a 2-level V-cycle off
-    the origin with Dirichlet / Neumann faces, bit for bit against the oracle,
-    norms included."""
-    shape = (76, 44, 52)  # coarse 38 x 22 x 26 (MGnewOp needs the box coarsenable by 4)
+    64 x 4 coarse / 128 x 4 fine tiles, 4- and 32-plane chunks, XCD bands of
+    16 tiles) on boxes none of whose sides fills a tile, a row group or a
+    chunk: a 2-level V-cycle off the origin with Dirichlet / Neumann faces,
+    bit for bit against the oracle, norms included.  (76, 44, 52): fewer
+    tiles than one band group (the dispatch order); (256, 132, 64): 132
+    residual and 272 restriction tiles, i.e. whole groups of 8 x 16 bands
+    plus a tail."""
+    # (MGnewOp needs the box coarsenable by 4)
     lo = (8, -12, 16)
     dom = tuple(lo) + tuple(lo[d] + shape[d] - 1 for d in range(3))
     dx = 0.29
