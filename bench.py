@@ -62,6 +62,11 @@ def parse():
                     help="skip the second, event-instrumented timed region (roofline fields null)")
     ap.add_argument("--no-bottom", action="store_true",
                     help="skip the separately reported BiCGStab-bottom V-cycle timing")
+    ap.add_argument("--bottom-vcycles", type=int, default=8,
+                    help="V-cycles timed from phi = 0 with the BiCGStab bottom (fixed, so the "
+                         "bottom's work does not depend on --steps / --warmup)")
+    ap.add_argument("--bottom-replays", type=int, default=10,
+                    help="replays of the last bottom solve from e = 0 on the same coarse residual")
     ap.add_argument("--norm-type", type=int, default=0,
                     help="per-iteration residual norm of AMRMultiGrid's stop test (params.txt:37-38, "
                          "m_normType 0 = max norm; -1 skips it)")
@@ -361,41 +366,63 @@ def build_case(mg, comm, world, n, levels, nsmooth, boxes_per_rank=(1, 1, 1), fu
 
 
 def bottom_timing(mg, case, args, timed, nt, gsrb_ms):
-    """K V-cycle iterations with the BiCGStab bottom (bottom_solver = 1, the
-    reference's, Main_PoissonSolver.cpp:103-117: MultilevelLinearOp's
-    BiCGStab at the coarsest MG depth) on a second hierarchy over the same
-    operator factory, from phi = 0: ms per V-cycle beside the GSRB-bottom
-    headline, and the difference (the bottom's own cost)."""
+    """The V-cycle with the reference's bottom solver (bottom_solver = 1,
+    Main_PoissonSolver.cpp:103-117: MultilevelLinearOp's BiCGStab at the
+    coarsest MG depth, preconditioned by preCond,
+    Source/VariableCoeffPoissonOperator.cpp:72-104) on a second hierarchy
+    over the same operator factory.  Every timed solve starts from work: the
+    K_b = --bottom-vcycles V-cycles are timed from phi = 0 (a fixed count,
+    independent of --steps / --warmup, short of the roundoff floor where
+    BiCGStab would stop on its absolute tolerance at once), and the solves
+    are then replayed from e = 0 on one coarse residual (a fixed amount of
+    work per solve).  Reported: ms per V-cycle, the bottom's share, the
+    iterations per solve and the coarse residual norms the solves started
+    from."""
     amg = mg.AMRMultiGrid(case["fac"], mg.SolverParams(
         max_depth=args.levels - 1, n_pre=args.nsmooth, n_post=args.nsmooth,
         n_bottom=args.nsmooth, bottom_solver=1, agglomerate_below=case["agglomerate_below"]))
     phi, res = mg.LevelData(case["grid"]), mg.LevelData(case["grid"])
-    phi.set_zero()
     frhs = case["frhs"]
-    amg.init_residual(phi, frhs, res, norm_type=0)
-    amg.iterations(phi, frhs, res, max(1, args.warmup), norm_type=nt)
-    el, hist = timed(lambda: amg.iterations(phi, frhs, res, args.steps, norm_type=nt))
-    ms = el / args.steps * 1e3
-    # the bottom solves themselves (HIP events on the rank that runs them:
-    # rank 0 when the coarsest depth is gathered), over the same iterations
-    # replayed from phi = 0: BiCGStab's iteration count follows the residual,
-    # so solves timed after the timed region (a converged residual) would
-    # exit at once and say nothing about the bottom_delta above
-    phi.set_zero()
-    amg.init_residual(phi, frhs, res, norm_type=0)
-    amg.iterations(phi, frhs, res, max(1, args.warmup), norm_type=nt)
+    kb = args.bottom_vcycles
+
+    def fresh():
+        phi.set_zero()
+        amg.init_residual(phi, frhs, res, norm_type=0)
+
+    # one untimed iteration allocates the solver's temporaries
+    fresh()
+    amg.iterations(phi, frhs, res, 1, norm_type=nt)
+    fresh()
+    el, hist = timed(lambda: amg.iterations(phi, frhs, res, kb, norm_type=nt))
+    ms = el / kb * 1e3
+    # the same K_b iterations again with HIP events around each solve on the
+    # rank that runs it (rank 0 when the coarsest depth is gathered)
+    fresh()
     amg.bottom_timer(True)
-    amg.iterations(phi, frhs, res, args.steps, norm_type=nt)
+    amg.iterations(phi, frhs, res, kb, norm_type=nt)
     solve_ms, solves = amg.bottom_ms()
+    iters, r0_lo, r0_hi = amg.bottom_iters()
     amg.bottom_timer(False)
-    out = {"solver": "BiCGStab (imax 80, eps 1e-6, restarts 5; preCond = lambda r + 2 GSRB)",
+    # the last solve replayed from e = 0 on its own coarse residual
+    rep_ms, rep_iters, rep_r0, rep_n = amg.bottom_replay(args.bottom_replays)
+    out = {"solver": "BiCGStab (imax 80, eps 1e-6, reps 1e-12, restarts 5; preCond = lambda r + "
+                     "2 GSRB)",
            "depth": args.levels - 1,
-           "vcycles_per_s": round(args.steps / el, 4), "ms_per_vcycle": round(ms, 4),
+           "vcycles_timed": kb,
+           "vcycles_per_s": round(kb / el, 4), "ms_per_vcycle": round(ms, 4),
            "gsrb_bottom_ms_per_vcycle": round(gsrb_ms * 1e3, 4),
            "bottom_delta_ms": round(ms - gsrb_ms * 1e3, 4),
            "bottom_solve_ms_rank0": round(solve_ms / solves, 4) if solves else None,
            "bottom_solves_timed_rank0": solves,
-           "residual_norm_history": hist[-3:] if nt >= 0 else None}
+           "iterations_per_solve": round(iters / solves, 3) if solves else None,
+           "coarse_residual_norm_range": [r0_lo, r0_hi] if solves else None,
+           "replay": ({"solves": rep_n, "ms_per_solve": round(rep_ms / rep_n, 4),
+                       "iterations_per_solve": rep_iters,
+                       "ms_per_iteration": round(rep_ms / rep_n / max(1, rep_iters), 5),
+                       "coarse_residual_norm": rep_r0} if rep_n else None),
+           "residual_norm_history": hist[-3:] if nt >= 0 else None,
+           "note": "every timed solve starts from an unconverged coarse residual (the range "
+                   "above): K_b V-cycles from phi = 0, then the last solve replayed from e = 0"}
     del amg, phi, res
     return out
 

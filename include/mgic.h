@@ -297,6 +297,19 @@ MGIC_API int mgic_mg_fmg(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field 
  * and starts recording; bottom_ms returns their total time and count */
 MGIC_API int mgic_mg_bottom_timer(mgic_mg mg, int on);
 MGIC_API int mgic_mg_bottom_ms(mgic_mg mg, double *ms, int *calls);
+/* BiCGStab iterations summed over the solves timed since mgic_mg_bottom_timer
+ * (1), and the smallest / largest norm of the coarse residual they started
+ * from (the bench's proof that each timed solve did work) */
+MGIC_API int mgic_mg_bottom_iters(mgic_mg mg, long long *iters, double *r0_min, double *r0_max);
+/* the last BiCGStab bottom solve this rank ran: on the device (1) or by the
+ * host loop (0), its iterations and the norm of the residual it started from */
+MGIC_API int mgic_mg_bottom_info(mgic_mg mg, int *device, int *iters, double *r0);
+/* the last bottom solve again, n times, each from e = 0 on the same coarse
+ * residual: total ms (HIP events), iterations per solve, the residual's norm;
+ * *solves = n, or 0 on a rank that does not run the coarsest depth or before
+ * a V-cycle has run a bottom solve */
+MGIC_API int mgic_mg_bottom_replay(mgic_mg mg, int n, double *ms, int *iters, double *r0,
+                                   int *solves);
 
 /* Mixed precision (BASELINE config C5): the same V-cycle schedule with the
  * correction equation in fp32 (GSRB / restrictResidual / prolongIncrement in

@@ -170,6 +170,9 @@ SIGNATURES = {
     "mgic_mg_precondition": [H, H, H, c_int],
     "mgic_mg_bottom_timer": [H, c_int],
     "mgic_mg_bottom_ms": [H, PD, PI],
+    "mgic_mg_bottom_iters": [H, PLL, PD, PD],
+    "mgic_mg_bottom_replay": [H, c_int, PD, PI, PD, PI],
+    "mgic_mg_bottom_info": [H, PI, PI, PD],
     "mgic_mg_fmg": [H, H, H, H, c_int, c_int, c_int, PD],
     "mgic_grid_create_patches": [H, PI, PI, c_double, c_int, PI, PI, PH],
     "mgic_amr_create": [c_int, POINTER(H), POINTER(H), POINTER(H), POINTER(OpParams),
@@ -235,21 +238,60 @@ _RESTYPE = {
 }
 
 
+def hip_runtime_images() -> list:
+    """The distinct HIP runtime files (libamdhip64*) mapped into this process,
+    from /proc/self/maps ([] where that file does not exist)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6:
+                    p = parts[5].strip()
+                    if os.path.basename(p).startswith("libamdhip64"):
+                        paths.add(os.path.realpath(p))
+    except OSError:
+        return []
+    return sorted(paths)
+
+
+def check_single_hip_runtime() -> None:
+    """Fail loudly when this process maps more than one HIP runtime: torch
+    bundles its own libamdhip64 under another path, and a process that loads
+    libmgic.so (which binds /opt/rocm's by soname) before torch holds both --
+    they corrupt each other's heap at exit ("double free or corruption",
+    status -6).  Checked at load, and again wherever a Comm or a device is
+    set up (torch may be imported after this package)."""
+    imgs = hip_runtime_images()
+    if len(imgs) > 1:
+        raise RuntimeError(
+            "two HIP runtimes in one process (" + ", ".join(imgs) + "): import torch before "
+            "mg_ic_code_amd (the default preload does this unless MGIC_NO_TORCH_PRELOAD is set)")
+
+
+def _preload_torch() -> None:
+    """Import torch (when installed) before the library, so that libmgic.so
+    binds to torch's HIP runtime by soname instead of loading a second one
+    (check_single_hip_runtime).  MGIC_NO_TORCH_PRELOAD=1 skips it (a process
+    that never imports torch); a torch that is present but broken is not this
+    library's failure: any exception is swallowed, and the runtime check
+    still guards the process."""
+    if os.environ.get("MGIC_NO_TORCH_PRELOAD", "0") not in ("", "0"):
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:  # noqa: BLE001 -- see the docstring
+        pass
+
+
 def _load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
-    # torch (when installed) before the library: torch ships its own HIP
-    # runtime, loaded under another file name, and a process that loads
-    # libmgic.so first ends up with two HIP runtimes -- which fail at exit
-    # ("double free or corruption"); loaded second, libmgic.so binds to
-    # torch's by soname
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    _preload_torch()
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    check_single_hip_runtime()
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)  # AttributeError = missing export: fail loudly
         if argtypes is not None:

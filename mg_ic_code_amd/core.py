@@ -60,6 +60,7 @@ def _ints(vals: Iterable[int]):
 
 
 def set_device(dev: int) -> None:
+    _lib.check_single_hip_runtime()
     call("mgic_set_device", int(dev))
 
 
@@ -101,6 +102,7 @@ class Comm:
     def __init__(self, rank: int = 0, size: int = 1, unique_id: Optional[bytes] = None,
                  force_rccl: bool = False, transport: str = "rccl",
                  allgather=None, arena_bytes: int = 0):
+        _lib.check_single_hip_runtime()
         h = ctypes.c_void_p()
         self.rank, self.size = rank, size
         if transport == "ipc":
@@ -625,6 +627,29 @@ class AMRMultiGrid:
         ms, n = ctypes.c_double(), ctypes.c_int()
         call("mgic_mg_bottom_ms", self._h, ctypes.byref(ms), ctypes.byref(n))
         return ms.value, n.value
+
+    def bottom_iters(self) -> Tuple[int, float, float]:
+        """(BiCGStab iterations summed over the timed solves, smallest and
+        largest norm of the coarse residual they started from)."""
+        it, lo, hi = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
+        call("mgic_mg_bottom_iters", self._h, ctypes.byref(it), ctypes.byref(lo), ctypes.byref(hi))
+        return it.value, lo.value, hi.value
+
+    def bottom_info(self) -> Tuple[bool, int, float]:
+        """The last BiCGStab bottom solve: (ran on the device, iterations,
+        norm of the residual it started from)."""
+        dv, it, r0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        call("mgic_mg_bottom_info", self._h, ctypes.byref(dv), ctypes.byref(it), ctypes.byref(r0))
+        return bool(dv.value), it.value, r0.value
+
+    def bottom_replay(self, n: int) -> Tuple[float, int, float, int]:
+        """The last bottom solve again, n times from e = 0 on the same coarse
+        residual: (total ms, iterations per solve, residual norm, solves run;
+        0 solves on a rank that does not run the coarsest depth)."""
+        ms, it, r0, k = ctypes.c_double(), ctypes.c_int(), ctypes.c_double(), ctypes.c_int()
+        call("mgic_mg_bottom_replay", self._h, int(n), ctypes.byref(ms), ctypes.byref(it),
+             ctypes.byref(r0), ctypes.byref(k))
+        return ms.value, it.value, r0.value, k.value
 
     def fmg(self, phi: LevelData, rhs: LevelData, resid: LevelData, norm_type: int = 0,
             homogeneous: bool = False, ncycles: int = 1) -> float:

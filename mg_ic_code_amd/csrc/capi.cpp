@@ -1037,6 +1037,35 @@ MGIC_API int mgic_mg_bottom_ms(mgic_mg mg, double *ms, int *calls) {
     *ms = mg->amg.mg.bottom_ms(calls);
   });
 }
+MGIC_API int mgic_mg_bottom_iters(mgic_mg mg, long long *iters, double *r0_min,
+                                  double *r0_max) {
+  return guard([&] {
+    NEED(mg);
+    NEED(iters);
+    *iters = mg->amg.mg.bottom_iters(r0_min, r0_max);
+  });
+}
+MGIC_API int mgic_mg_bottom_info(mgic_mg mg, int *device, int *iters, double *r0) {
+  return guard([&] {
+    NEED(mg);
+    const BiCGStabSolver &b = mg->amg.mg.bottom;
+    if (device) *device = b.last_device ? 1 : 0;
+    if (iters) *iters = b.last_iters;
+    if (r0) *r0 = b.last_init_norm;
+  });
+}
+MGIC_API int mgic_mg_bottom_replay(mgic_mg mg, int n, double *ms, int *iters, double *r0,
+                                   int *solves) {
+  return guard([&] {
+    NEED(mg);
+    NEED(ms);
+    NEED(iters);
+    NEED(r0);
+    MGIC_CHECK(n >= 0, "n must be >= 0");
+    const int k = mg->amg.mg.bottom_replay(n, ms, iters, r0);
+    if (solves) *solves = k;
+  });
+}
 MGIC_API int mgic_mg_fmg(mgic_mg mg, mgic_field phi, mgic_field rhs, mgic_field resid,
                          int norm_type, int h, int ncycles, double *norm) {
   return guard([&] {

@@ -1431,6 +1431,306 @@ __global__ __launch_bounds__(256) void k_cf_interp(double *__restrict__ u,
   u[gi] = ((8.0 / 15.0) * ps + (2.0 / 3.0) * f1) + (-0.2) * f2;
 }
 
+// ---- BiCGStab on the device (the bottom solver's loop without host
+// readbacks; op.cpp BiCGStabSolver::solve_device).  The scalars the host loop
+// branches on live in a BicgState in device memory: the last block of each
+// reduction launch (told by an agent-scope counter) finishes the partials with
+// k_reduce_final's loop and tree, evaluates the host loop's tests in the same
+// order and writes alpha / omega / beta, or stops the solve (done = 1, with
+// its reason); every later launch of the batch returns at once.  Each vector
+// update fuses the reductions and the preCond scaling that follow it in the
+// host loop, with the same per-element expressions and k_reduce_partial's
+// row-to-wave deal and accumulators, so every value is the host loop's bit
+// for bit.
+
+// the launch's last block to arrive (thread 0 stored this block's partials
+// before): agent-scope release, count, acquire in the last block
+__device__ __forceinline__ bool bicg_last_block(unsigned int *cnt, unsigned int nb) {
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned int prev =
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == nb - 1;
+  }
+  __syncthreads();
+  if (!last) return false;
+  __threadfence();
+  return true;
+}
+
+__device__ __forceinline__ void bicg_store_part(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p),
+                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double bicg_load_part(const double *p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// k_reduce_final<KIND>'s loop and tree over n partials, in the last block;
+// the result in every thread
+template <int KIND>
+__device__ double bicg_final(const double *parts, int n, double *sm) {
+  double acc = red_init<KIND>();
+  for (int t = threadIdx.x; t < n; t += RB) acc = red_op<KIND>(acc, bicg_load_part(parts + t));
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = RB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
+    __syncthreads();
+  }
+  const double r = sm[0];
+  __syncthreads();
+  return r;
+}
+
+// the block's partial of reduction KIND (k_reduce_partial's tree) -> parts[blockIdx.x]
+template <int KIND>
+__device__ void bicg_block_part(const double acc[4], double *sm, double *parts) {
+  sm[threadIdx.x] = red_op<KIND>(red_op<KIND>(acc[0], acc[1]), red_op<KIND>(acc[2], acc[3]));
+  __syncthreads();
+  for (int w = RB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bicg_store_part(parts + blockIdx.x, sm[0]);
+  __syncthreads();
+}
+
+// norm_of (op.cpp): max / sum norms as reduced, the 2-norm's square root
+__device__ __forceinline__ double bicg_norm_of(int nt, double x) {
+  return nt == 1 || nt == 0 ? x : sqrt(x);
+}
+
+__device__ __forceinline__ void bicg_stop(BicgState *st, int reason) {
+  st->done = 1;
+  st->reason = reason;
+}
+
+// k_reduce_partial's row-to-wave deal: f(i, j, k, idx, q) for every cell,
+// q = the lane's accumulator
+template <class F>
+__device__ __forceinline__ void bicg_rows(const BoxArgs &g, F &&f) {
+  constexpr int W = RB / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nrows = g.ny * g.nz;
+  for (int row = blockIdx.x * W + wave; row < nrows; row += gridDim.x * W) {
+    const int k = row / g.ny, j = row - k * g.ny;
+    const long base = (long)j * g.sy + (long)k * g.sz;
+    int i = lane;
+    for (; i + 192 < g.nx; i += 256) {
+      f(i, j, k, base + i, 0);
+      f(i + 64, j, k, base + i + 64, 1);
+      f(i + 128, j, k, base + i + 128, 2);
+      f(i + 192, j, k, base + i + 192, 3);
+    }
+    for (; i < g.nx; i += 64) f(i, j, k, base + i, 0);
+  }
+}
+
+// VCCOMPUTEOP3D's value at one cell (k_apply_op's expressions)
+template <bool BC>
+__device__ __forceinline__ double bicg_apply(const double *__restrict__ u,
+                                             const double *__restrict__ a,
+                                             const double *__restrict__ b, long idx, int i, int j,
+                                             int k, const BoxArgs &g, const StencilCoefs &s) {
+  const double uc = u[idx];
+  const double lof = s.alpha * a[idx] * uc;
+  double ldpsi = lap7(u, idx, uc, i, j, k, g);
+  ldpsi = ldpsi * s.dxinv * s.beta * (BC ? s.bval : b[idx]);
+  return lof - ldpsi;
+}
+
+// P = R (first iteration after a (re)start) or ((P*beta) + c*V) + 1.0*R,
+// c = (-beta)*omega (bicgP); W = P * lambda (preCond's first pass)
+__global__ __launch_bounds__(256) void k_bicgd_p(BicgState *__restrict__ st,
+                                                double *__restrict__ p, double *__restrict__ w,
+                                                const double *__restrict__ v,
+                                                const double *__restrict__ r,
+                                                const double *__restrict__ lam, const BoxArgs g) {
+  if (st->done) return;
+  const int i = blockIdx.x * TX + threadIdx.x;
+  const int j = blockIdx.y * TY + threadIdx.y;
+  const int k = blockIdx.z;
+  if (i >= g.nx || j >= g.ny) return;
+  const long idx = (long)i + (long)j * g.sy + (long)k * g.sz;
+  double pv;
+  if (st->init) {
+    pv = r[idx];
+  } else {
+    const double beta = st->beta, c = (-beta) * st->omega;
+    double t = p[idx] * beta;
+    t = t + c * v[idx];
+    pv = t + 1.0 * r[idx];
+  }
+  p[idx] = pv;
+  w[idx] = pv * lam[idx];
+}
+
+// V = L(PT); <RT, V>; last block: m, alpha (or a restart / stop)
+template <bool BC>
+__global__ __launch_bounds__(RB) void k_bicgd_apply_dot(BicgState *__restrict__ st,
+                                                       double *__restrict__ v,
+                                                       const double *__restrict__ pt,
+                                                       const double *__restrict__ rt,
+                                                       const double *__restrict__ a,
+                                                       const double *__restrict__ b,
+                                                       const BoxArgs g, const StencilCoefs s,
+                                                       double *__restrict__ parts) {
+  __shared__ double sm[RB];
+  if (st->done) return;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  bicg_rows(g, [&](int i, int j, int k, long idx, int q) {
+    const double vv = bicg_apply<BC>(pt, a, b, idx, i, j, k, g, s);
+    v[idx] = vv;
+    acc[q] = acc[q] + rt[idx] * vv;
+  });
+  bicg_block_part<0>(acc, sm, parts);
+  if (!bicg_last_block(&st->cnt[0], gridDim.x)) return;
+  const double m = bicg_final<0>(parts, gridDim.x, sm);
+  if (threadIdx.x == 0) {
+    st->m = m;
+    st->init = 0;
+    if (fabs(m) > st->small * fabs(st->rho1)) st->alpha = st->rho1 / m;
+    else bicg_stop(st, st->restarts >= st->num_restarts ? kBicgRestartLimit : kBicgRestart);
+    __hip_atomic_store(&st->cnt[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// S = R + (-alpha) V; |S| (norm kind NK); W = S * lambda; last block: the
+// half-step stop test.  E += alpha PT is left pending (epend) for k_bicgd_r.
+template <int NK>
+__global__ __launch_bounds__(RB) void k_bicgd_s(BicgState *__restrict__ st,
+                                               double *__restrict__ s, double *__restrict__ w,
+                                               const double *__restrict__ r,
+                                               const double *__restrict__ v,
+                                               const double *__restrict__ lam, const BoxArgs g,
+                                               double *__restrict__ parts) {
+  __shared__ double sm[RB];
+  if (st->done) return;
+  const double ca = -st->alpha;
+  double acc[4] = {red_init<NK>(), red_init<NK>(), red_init<NK>(), red_init<NK>()};
+  bicg_rows(g, [&](int, int, int, long idx, int q) {
+    const double sv = r[idx] + ca * v[idx];
+    s[idx] = sv;
+    w[idx] = sv * lam[idx];
+    acc[q] = red_op<NK>(acc[q], NK == 2 ? sv * sv : fabs(sv));
+  });
+  bicg_block_part<NK>(acc, sm, parts);
+  if (!bicg_last_block(&st->cnt[1], gridDim.x)) return;
+  const double x = bicg_final<NK>(parts, gridDim.x, sm);
+  if (threadIdx.x == 0) {
+    const double nrm = bicg_norm_of(st->nt, x);
+    st->nrm = nrm;
+    st->epend = 1;
+    if (nrm <= st->eps * st->init_norm || nrm <= st->reps) bicg_stop(st, kBicgHalf);
+    __hip_atomic_store(&st->cnt[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// T = L(ST); <T, S> and <T, T>; last block: omega (or the tt == 0 stop)
+template <bool BC>
+__global__ __launch_bounds__(RB) void k_bicgd_apply_dot2(BicgState *__restrict__ st,
+                                                        double *__restrict__ t,
+                                                        const double *__restrict__ stv,
+                                                        const double *__restrict__ s,
+                                                        const double *__restrict__ a,
+                                                        const double *__restrict__ b,
+                                                        const BoxArgs g, const StencilCoefs sc,
+                                                        double *__restrict__ parts_ts,
+                                                        double *__restrict__ parts_tt) {
+  __shared__ double sm[RB];
+  if (st->done) return;
+  double aa[4] = {0.0, 0.0, 0.0, 0.0}, bb[4] = {0.0, 0.0, 0.0, 0.0};
+  bicg_rows(g, [&](int i, int j, int k, long idx, int q) {
+    const double tv = bicg_apply<BC>(stv, a, b, idx, i, j, k, g, sc);
+    t[idx] = tv;
+    aa[q] = aa[q] + tv * s[idx];
+    bb[q] = bb[q] + tv * tv;
+  });
+  bicg_block_part<0>(aa, sm, parts_ts);
+  bicg_block_part<0>(bb, sm, parts_tt);
+  if (!bicg_last_block(&st->cnt[2], gridDim.x)) return;
+  const double ts = bicg_final<0>(parts_ts, gridDim.x, sm);
+  const double tt = bicg_final<0>(parts_tt, gridDim.x, sm);
+  if (threadIdx.x == 0) {
+    st->ts = ts;
+    st->tt = tt;
+    if (tt == 0.0) bicg_stop(st, kBicgTt0);
+    else st->omega = ts / tt;
+    __hip_atomic_store(&st->cnt[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// R = S + (-omega) T; E = (E + alpha PT) + omega ST; |R| (kind NK) and
+// <RT, R>; last block: the omega == 0 stop, then the loop's head -- its test,
+// it += 1, rho1 = <RT, R>, the rho1 == 0 stop and beta
+template <int NK>
+__global__ __launch_bounds__(RB) void k_bicgd_r(BicgState *__restrict__ st,
+                                               double *__restrict__ r, double *__restrict__ e,
+                                               const double *__restrict__ s,
+                                               const double *__restrict__ t,
+                                               const double *__restrict__ pt,
+                                               const double *__restrict__ stv,
+                                               const double *__restrict__ rt, const BoxArgs g,
+                                               double *__restrict__ parts_n,
+                                               double *__restrict__ parts_d) {
+  __shared__ double sm[RB];
+  if (st->done) return;
+  const double alpha = st->alpha, omega = st->omega, ca = -omega;
+  double an[4] = {red_init<NK>(), red_init<NK>(), red_init<NK>(), red_init<NK>()};
+  double ad[4] = {0.0, 0.0, 0.0, 0.0};
+  bicg_rows(g, [&](int, int, int, long idx, int q) {
+    const double rv = s[idx] + ca * t[idx];
+    r[idx] = rv;
+    const double e1 = e[idx] + alpha * pt[idx];
+    e[idx] = e1 + omega * stv[idx];
+    an[q] = red_op<NK>(an[q], NK == 2 ? rv * rv : fabs(rv));
+    ad[q] = ad[q] + rt[idx] * rv;
+  });
+  bicg_block_part<NK>(an, sm, parts_n);
+  bicg_block_part<0>(ad, sm, parts_d);
+  if (!bicg_last_block(&st->cnt[3], gridDim.x)) return;
+  const double x = bicg_final<NK>(parts_n, gridDim.x, sm);
+  const double rho_next = bicg_final<0>(parts_d, gridDim.x, sm);
+  if (threadIdx.x == 0) {
+    const double nrm = bicg_norm_of(st->nt, x);
+    st->nrm = nrm;
+    st->rho_next = rho_next;
+    st->epend = 0;
+    if (omega == 0.0) {
+      bicg_stop(st, kBicgOmega0);
+    } else if (!(st->it < st->imax && nrm > st->eps * st->init_norm && nrm > st->reps)) {
+      bicg_stop(st, kBicgStop);
+    } else {
+      st->it += 1;
+      st->rho2 = st->rho1;
+      st->rho1 = rho_next;
+      if (rho_next == 0.0) bicg_stop(st, kBicgRho0);
+      else st->beta = (st->rho1 / st->rho2) * (st->alpha / st->omega);
+    }
+    __hip_atomic_store(&st->cnt[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// the state into pinned host memory, then the sequence number the host spins on
+__global__ void k_bicgd_publish(const BicgState *__restrict__ st, BicgState *host,
+                               unsigned long long *seq, unsigned long long seqv) {
+  if (threadIdx.x != 0) return;
+  constexpr int nw = (int)(sizeof(BicgState) / 4);
+  const unsigned int *src = reinterpret_cast<const unsigned int *>(st);
+  unsigned int *dst = reinterpret_cast<unsigned int *>(host);
+  for (int t = 0; t < nw; ++t)
+    __hip_atomic_store(dst + t, src[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(seq, seqv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
 
 void gsrb_pass(double *u, const double *rhs, const double *a, const double *b, const double *lam,
@@ -1956,6 +2256,68 @@ void incr_f(double *x, const float *y, const BoxArgs &g, hipStream_t st) {
 void copy_f(float *d, const float *s, const BoxArgs &g, hipStream_t st) {
   if (g.nx <= 0 || g.ny <= 0 || g.nz <= 0) return;
   k_copy_f<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st>>>(d, s, g);
+  check_launch();
+}
+
+
+// ---- BiCGStab on the device: launchers (kernels above; the reductions use
+// reduce_blocks(g) blocks, as the host loop's partials do)
+int bicg_dev_parts(const BoxArgs &g) { return (int)reduce_blocks(g); }
+
+void bicg_dev_p(BicgState *st, double *p, double *w, const double *v, const double *r,
+                const double *lam, const BoxArgs &g, hipStream_t st_) {
+  k_bicgd_p<<<grid_cells(g.nx, g.ny, g.nz), kBlock, 0, st_>>>(st, p, w, v, r, lam, g);
+  check_launch();
+}
+
+void bicg_dev_apply_dot(BicgState *st, double *v, const double *pt, const double *rt,
+                        const double *a, const double *b, const BoxArgs &g, const StencilCoefs &s,
+                        double *parts, hipStream_t st_) {
+  const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
+  if (s.bconst) k_bicgd_apply_dot<true><<<grid, block, 0, st_>>>(st, v, pt, rt, a, b, g, s, parts);
+  else k_bicgd_apply_dot<false><<<grid, block, 0, st_>>>(st, v, pt, rt, a, b, g, s, parts);
+  check_launch();
+}
+
+void bicg_dev_s(BicgState *st, double *s, double *w, const double *r, const double *v,
+                const double *lam, const BoxArgs &g, int norm_kind, double *parts, hipStream_t st_) {
+  const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
+  switch (norm_kind) {
+    case 1: k_bicgd_s<1><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts); break;
+    case 2: k_bicgd_s<2><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts); break;
+    case 3: k_bicgd_s<3><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts); break;
+    default: throw Error(kBadArg, "bicg_dev_s: bad norm kind");
+  }
+  check_launch();
+}
+
+void bicg_dev_apply_dot2(BicgState *st, double *t, const double *stv, const double *s,
+                         const double *a, const double *b, const BoxArgs &g, const StencilCoefs &sc,
+                         double *parts_ts, double *parts_tt, hipStream_t st_) {
+  const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
+  if (sc.bconst)
+    k_bicgd_apply_dot2<true><<<grid, block, 0, st_>>>(st, t, stv, s, a, b, g, sc, parts_ts, parts_tt);
+  else
+    k_bicgd_apply_dot2<false><<<grid, block, 0, st_>>>(st, t, stv, s, a, b, g, sc, parts_ts, parts_tt);
+  check_launch();
+}
+
+void bicg_dev_r(BicgState *st, double *r, double *e, const double *s, const double *t,
+                const double *pt, const double *stv, const double *rt, const BoxArgs &g,
+                int norm_kind, double *parts_n, double *parts_d, hipStream_t st_) {
+  const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
+  switch (norm_kind) {
+    case 1: k_bicgd_r<1><<<grid, block, 0, st_>>>(st, r, e, s, t, pt, stv, rt, g, parts_n, parts_d); break;
+    case 2: k_bicgd_r<2><<<grid, block, 0, st_>>>(st, r, e, s, t, pt, stv, rt, g, parts_n, parts_d); break;
+    case 3: k_bicgd_r<3><<<grid, block, 0, st_>>>(st, r, e, s, t, pt, stv, rt, g, parts_n, parts_d); break;
+    default: throw Error(kBadArg, "bicg_dev_r: bad norm kind");
+  }
+  check_launch();
+}
+
+void bicg_dev_publish(const BicgState *st, BicgState *host, unsigned long long *seq,
+                      unsigned long long seqv, hipStream_t st_) {
+  k_bicgd_publish<<<1, 64, 0, st_>>>(st, host, seq, seqv);
   check_launch();
 }
 

@@ -51,9 +51,11 @@ void gsrb_sweep_fused_restrict(double *u_out, double *u_in, const double *rhs, c
 // filled.  _applies also keeps boxes the 3D-block kernel takes (kind 3, or
 // kind 1 at most gsrb_block_max_cells() cells) on that kernel.
 bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind);
+// skip (device, or null): the launch returns at once when *skip != 0 (a
+// device-side solve that has stopped, BicgState::done)
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
-                    hipStream_t st);
+                    hipStream_t st, const int *skip = nullptr);
 // the same two-sweep launch on fp32 fields; acc (the fp64 phi, or null):
 // the second sweep's values are added to it as (double)e instead of stored
 void gsrb_sweep_tb2_f(float *u_out, const float *u_in, const float *rhs, const float *a,
@@ -140,6 +142,51 @@ int dot2_partial(const double *t, const double *s, const BoxArgs &g, double *pts
                  hipStream_t st);
 void bicg_p(double *p, const double *v, const double *r, double beta, double c, const BoxArgs &g,
             hipStream_t st);
+
+// ---- BiCGStab on the device (op.cpp BiCGStabSolver::solve_device): the
+// host loop's scalars, its stop tests and their outcome, in device memory.
+// Each launch below returns at once when done != 0; the last block of each
+// reduction writes the next scalars (or stops the solve).
+enum BicgReason {
+  kBicgRun = 0,
+  kBicgStop = 1,          // the loop's test (iterations, eps, reps)
+  kBicgRho0 = 2,          // rho1 == 0
+  kBicgHalf = 3,          // |S| met the tolerance (E += alpha PT pending)
+  kBicgTt0 = 4,           // <T, T> == 0 (E += alpha PT pending)
+  kBicgOmega0 = 5,        // omega == 0
+  kBicgRestart = 6,       // |m| <= small |rho1|: the host restarts the solve
+  kBicgRestartLimit = 7,  // the same with no restarts left
+};
+struct BicgState {
+  double rho1, rho2, alpha, beta, omega, nrm, init_norm, rho_next, m, ts, tt;
+  double eps, reps, small;
+  int it, imax, done, reason, epend, init, restarts, num_restarts, nt;
+  unsigned int cnt[4];  // last-block counters, one per reduction launch (0 between launches)
+  int pad;
+};
+// P = R (init) or ((P*beta) + ((-beta)*omega)*V) + 1.0*R; W = P * lambda
+void bicg_dev_p(BicgState *st, double *p, double *w, const double *v, const double *r,
+                const double *lam, const BoxArgs &g, hipStream_t st_);
+// V = L(PT) (homogeneous BC of g); alpha = rho1 / <RT, V>
+void bicg_dev_apply_dot(BicgState *st, double *v, const double *pt, const double *rt,
+                        const double *a, const double *b, const BoxArgs &g, const StencilCoefs &s,
+                        double *parts, hipStream_t st_);
+// S = R + (-alpha)V; W = S * lambda; nrm = |S|
+void bicg_dev_s(BicgState *st, double *s, double *w, const double *r, const double *v,
+                const double *lam, const BoxArgs &g, int norm_kind, double *parts, hipStream_t st_);
+// T = L(ST); omega = <T, S> / <T, T>
+void bicg_dev_apply_dot2(BicgState *st, double *t, const double *stv, const double *s,
+                         const double *a, const double *b, const BoxArgs &g, const StencilCoefs &sc,
+                         double *parts_ts, double *parts_tt, hipStream_t st_);
+// R = S + (-omega)T; E = (E + alpha PT) + omega ST; nrm = |R|; the loop head
+void bicg_dev_r(BicgState *st, double *r, double *e, const double *s, const double *t,
+                const double *pt, const double *stv, const double *rt, const BoxArgs &g,
+                int norm_kind, double *parts_n, double *parts_d, hipStream_t st_);
+// copy *st into pinned host memory, then store seqv into *seq (host-coherent)
+void bicg_dev_publish(const BicgState *st, BicgState *host, unsigned long long *seq,
+                      unsigned long long seqv, hipStream_t st_);
+// partials written by the reductions above for box g
+int bicg_dev_parts(const BoxArgs &g);
 
 // batched rectangular copies (exchange / copyTo / pack / unpack)
 void copy_items(const CopyItem *d_items, int nitems, long max_cells, double *const *src_tab,

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 namespace mgic {
 
@@ -93,6 +94,7 @@ int prof_read(double *total_ms, long *passes) {
 
 // --------------------------------------------------------------- operator
 int VariableCoeffPoissonOperator::s_maxCoarse = 2;
+static int sweeps_per_launch();
 
 void check_same_layout(const Grid &g, const LevelData &x, const char *what) {
   const Grid &h = *x.grid;
@@ -213,6 +215,21 @@ void VariableCoeffPoissonOperator::preCond(LevelData &cor, const LevelData &res)
   for (int n = 0; n < grid->nlocal(); ++n)
     kern::blas(6, cor.p[n], res.p[n], m_lambda->p[n], 0.0, 0.0, args_plain_[n], st);
   relax(cor, res, 2);  // :103
+}
+
+bool VariableCoeffPoissonOperator::preCondFromScaledApplies() {
+  if (prm.relax_mode != 1 || cf || !fusedSmootherApplies()) return false;
+  if (grid->nlocal() != 1 || grid->has_memory_faces() || sweeps_per_launch() < 2) return false;
+  const StencilCoefs s = coefs();
+  // fusedRelax(cor, res, 2) is then exactly one two-sweep launch from cor
+  return kern::gsrb_sweep_tb2_applies(args_hom_[0], s, prm.fused_smoother);
+}
+
+void VariableCoeffPoissonOperator::preCondFromScaled(LevelData &cor, const LevelData &w,
+                                                     const LevelData &res, const int *skip) {
+  const StencilCoefs s = coefs();  // resetLambda (.cpp:90)
+  kern::gsrb_sweep_tb2(cor.p[0], w.p[0], res.p[0], m_aCoef->p[0], args_hom_[0], s, false, nullptr,
+                       stream(), skip);
 }
 
 void VariableCoeffPoissonOperator::applyOpI(LevelData &lhs, LevelData &dpsi, bool homogeneous) {
@@ -915,6 +932,8 @@ std::unique_ptr<VariableCoeffPoissonOperator> VariableCoeffPoissonOperatorFactor
 // --------------------------------------------------------------- BiCGStab
 int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
                           bool hom) {
+  last_device = deviceApplies(op);
+  if (last_device) return solveDevice(op, phi, rhs, hom);
   auto &tv = temps_[op.grid.get()];
   if (tv.empty())
     for (int i = 0; i < 9; ++i) tv.push_back(op.create());
@@ -930,6 +949,7 @@ int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, cons
   op.setToZero(V);
   double rho1 = 0.0, rho2 = 0.0, alpha = 0.0, beta = 0.0, omega = 0.0;
   const double init_norm = op.norm(R, nt);
+  last_init_norm = init_norm;
   double nrm = init_norm;
   int it = 0, restarts = 0;
   bool init = true;
@@ -1015,6 +1035,168 @@ int BiCGStabSolver::solve(VariableCoeffPoissonOperator &op, LevelData &phi, cons
   op.incr(phi, E, 1.0);
   last_iters = it;
   return it;
+}
+
+
+// ------------------------------------------------------ BiCGStab on the device
+BiCGStabSolver::~BiCGStabSolver() {
+  for (auto &kv : dev_) {
+    DevWork &d = *kv.second;
+    if (d.d_st) (void)hipFree(d.d_st);
+    if (d.d_parts) (void)hipFree(d.d_parts);
+    if (d.h_pub) (void)hipHostFree(d.h_pub);
+    if (d.h_up) (void)hipHostFree(d.h_up);
+  }
+}
+
+bool BiCGStabSolver::deviceApplies(VariableCoeffPoissonOperator &op) const {
+  if (precond) return false;  // the outer solve's MG preconditioner: host loop
+  const char *e = getenv("MGIC_BICG_DEVICE");
+  if (e && atoi(e) == 0) return false;
+  const Comm &c = *op.grid->comm;
+  // one rank's reductions: a single rank, or a depth gathered onto this one
+  if (!(c.size() == 1 || op.owner_local >= 0)) return false;
+  if (op.grid->nlocal() != 1) return false;
+  const int nt = prm.normType;
+  return (nt == 0 || nt == 1 || nt == 2) && op.preCondFromScaledApplies();
+}
+
+BiCGStabSolver::DevWork &BiCGStabSolver::devWork(VariableCoeffPoissonOperator &op) {
+  auto &slot = dev_[op.grid.get()];
+  if (!slot) {
+    auto d = std::make_unique<DevWork>();
+    MGIC_HIP(hipMalloc(&d->d_st, sizeof(kern::BicgState)));
+    MGIC_HIP(hipMemset(d->d_st, 0, sizeof(kern::BicgState)));
+    const int np = kern::bicg_dev_parts(op.boxArgsPlain(0));
+    MGIC_HIP(hipMalloc(&d->d_parts, 2 * (size_t)std::max(1, np) * sizeof(double)));
+    void *p = nullptr;
+    // the published state, then the sequence number the host spins on
+    MGIC_HIP(hipHostMalloc(&p, sizeof(kern::BicgState) + 64, hipHostMallocCoherent));
+    d->h_pub = static_cast<kern::BicgState *>(p);
+    std::memset(p, 0, sizeof(kern::BicgState) + 64);
+    d->h_seq = reinterpret_cast<unsigned long long *>(static_cast<char *>(p) +
+                                                      sizeof(kern::BicgState) + 56);
+    MGIC_HIP(hipHostMalloc(&p, sizeof(kern::BicgState), hipHostMallocDefault));
+    d->h_up = static_cast<kern::BicgState *>(p);
+    d->w = op.create();
+    slot = std::move(d);
+  }
+  return *slot;
+}
+
+static int bicg_batch() {
+  const char *e = getenv("MGIC_BICG_BATCH");
+  const int b = e ? atoi(e) : 4;
+  return std::max(1, std::min(64, b));
+}
+
+// The loop of solve() with the scalars on the device.  The host runs the
+// loop's head at a (re)start -- its test, it += 1, rho1 = <RT, R> -- and
+// uploads the state; then batches of whole iterations are queued, each
+// ending in a published copy of the state, two batches ahead of the host's
+// wait.  A stop inside an iteration makes every later launch return at once.
+// On a stop the host completes E (+ alpha PT when the stop came after the
+// S update), restarts on the host when the device asks for it, and finishes
+// with phi += E, as solve() does.
+int BiCGStabSolver::solveDevice(VariableCoeffPoissonOperator &op, LevelData &phi,
+                                const LevelData &rhs, bool hom) {
+  auto &tv = temps_[op.grid.get()];
+  if (tv.empty())
+    for (int i = 0; i < 9; ++i) tv.push_back(op.create());
+  LevelData &R = *tv[0], &RT = *tv[1], &E = *tv[2], &P = *tv[3], &PT = *tv[4], &S = *tv[5],
+            &ST = *tv[6], &T = *tv[7], &V = *tv[8];
+  DevWork &dw = devWork(op);
+  LevelData &W = *dw.w;
+  const hipStream_t st = op.stream();
+  const int nt = prm.normType, nk = norm_kind(nt);
+  op.residual(R, phi, rhs, hom);
+  op.assignLocal(RT, R);
+  op.setToZero(E);
+  op.setToZero(PT);
+  op.setToZero(ST);
+  op.setToZero(P);
+  op.setToZero(V);
+  kern::BicgState h{};
+  h.init_norm = op.norm(R, nt);
+  h.nrm = h.init_norm;
+  h.eps = prm.eps;
+  h.reps = prm.reps;
+  h.small = prm.small;
+  h.imax = prm.imax;
+  h.num_restarts = prm.numRestarts;
+  h.nt = nt;
+  h.init = 1;
+  last_init_norm = h.init_norm;
+  const BoxArgs &gp = op.boxArgsPlain(0), &gh = op.boxArgs(0, true);
+  const StencilCoefs sc = op.stencil();
+  const double *lam = op.m_lambda->p[0], *a = op.m_aCoef->p[0], *b = op.m_bCoef->p[0];
+  const int np = kern::bicg_dev_parts(gp);
+  double *pa = dw.d_parts, *pb = dw.d_parts + std::max(1, np);
+  kern::BicgState *d = dw.d_st;
+  const int *skip = &d->done;
+  const int nb = bicg_batch();
+  auto batch = [&] {
+    for (int i = 0; i < nb; ++i) {
+      kern::bicg_dev_p(d, P.p[0], W.p[0], V.p[0], R.p[0], lam, gp, st);
+      op.preCondFromScaled(PT, W, P, skip);
+      kern::bicg_dev_apply_dot(d, V.p[0], PT.p[0], RT.p[0], a, b, gh, sc, pa, st);
+      kern::bicg_dev_s(d, S.p[0], W.p[0], R.p[0], V.p[0], lam, gp, nk, pa, st);
+      op.preCondFromScaled(ST, W, S, skip);
+      kern::bicg_dev_apply_dot2(d, T.p[0], ST.p[0], S.p[0], a, b, gh, sc, pa, pb, st);
+      kern::bicg_dev_r(d, R.p[0], E.p[0], S.p[0], T.p[0], PT.p[0], ST.p[0], RT.p[0], gp, nk, pa,
+                       pb, st);
+    }
+    kern::bicg_dev_publish(d, dw.h_pub, dw.h_seq, ++dw.seq, st);
+    return dw.seq;
+  };
+  auto wait = [&](unsigned long long want) {
+    for (unsigned long long i = 0;; ++i) {
+      if (__atomic_load_n(dw.h_seq, __ATOMIC_ACQUIRE) >= want) return;
+      if ((i & 1023) == 1023) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) {
+          if (__atomic_load_n(dw.h_seq, __ATOMIC_ACQUIRE) >= want) return;
+          throw Error(kState, "device BiCGStab: state was not published");
+        }
+        if (e != hipErrorNotReady) MGIC_HIP(e);
+      }
+      __builtin_ia32_pause();
+    }
+  };
+  for (;;) {
+    // the loop's head on the host (solve(): while-test, ++it, rho1)
+    if (!(h.it < prm.imax && h.nrm > prm.eps * h.init_norm && h.nrm > prm.reps)) break;
+    ++h.it;
+    h.rho2 = h.rho1;
+    h.rho1 = op.dotProduct(RT, R);
+    if (h.rho1 == 0.0) break;
+    h.done = 0;
+    h.reason = kern::kBicgRun;
+    h.epend = 0;
+    for (unsigned &c : h.cnt) c = 0;
+    *dw.h_up = h;
+    MGIC_HIP(hipMemcpyAsync(d, dw.h_up, sizeof(h), hipMemcpyHostToDevice, st));
+    unsigned long long t1 = batch(), t2 = batch();
+    for (;;) {
+      wait(t1);
+      if (__atomic_load_n(&dw.h_pub->done, __ATOMIC_ACQUIRE)) break;
+      t1 = t2;
+      t2 = batch();
+    }
+    h = *dw.h_pub;  // frozen once done: later batches skip and publish the same words
+    if (h.epend) op.incr(E, PT, h.alpha);  // the stop came after S = R - alpha V
+    if (h.reason != kern::kBicgRestart) break;
+    ++h.restarts;  // |m| <= small |rho1|: restart (solve()'s else branch)
+    op.incr(phi, E, 1.0);
+    op.residual(R, phi, rhs, hom);
+    op.assignLocal(RT, R);
+    op.setToZero(E);
+    h.nrm = op.norm(R, nt);
+    h.init = 1;
+  }
+  op.incr(phi, E, 1.0);
+  last_iters = h.it;
+  return h.it;
 }
 
 // --------------------------------------------------------------- MultiGrid
@@ -1119,6 +1301,48 @@ MultiGrid::~MultiGrid() {
 void MultiGrid::bottom_timer(bool on) {
   bt_on_ = on;
   bt_used_ = 0;
+  bt_iters_ = bt_solves_ = 0;
+  bt_r0_min_ = bt_r0_max_ = 0.0;
+}
+
+long MultiGrid::bottom_iters(double *r0_min, double *r0_max) const {
+  if (r0_min) *r0_min = bt_r0_min_;
+  if (r0_max) *r0_max = bt_r0_max_;
+  return bt_iters_;
+}
+
+int MultiGrid::bottom_replay(int n, double *ms, int *iters, double *r0) {
+  *ms = 0.0;
+  *iters = 0;
+  *r0 = 0.0;
+  const int d = (int)levels_.size() - 1;
+  if (n <= 0 || !bt_filled_ || !runs(d)) return 0;
+  VariableCoeffPoissonOperator &op = *levels_[d].op;
+  LevelData &e = *levels_[d].e, &r = *levels_[d].r;
+  const bool was_on = bt_on_;
+  const size_t used0 = bt_used_;
+  const long it0 = bt_iters_, sv0 = bt_solves_;
+  const double lo0 = bt_r0_min_, hi0 = bt_r0_max_;
+  bt_on_ = true;
+  for (int i = 0; i < n; ++i) {
+    op.setToZero(e);
+    bottom_solve(op, e, r);
+  }
+  MGIC_HIP(hipEventSynchronize(bt_ev_[bt_used_ - 1]));
+  for (size_t i = used0; i + 1 < bt_used_; i += 2) {
+    float t = 0.f;
+    MGIC_HIP(hipEventElapsedTime(&t, bt_ev_[i], bt_ev_[i + 1]));
+    *ms += t;
+  }
+  *iters = bottom.last_iters;
+  *r0 = bottom.last_init_norm;
+  bt_used_ = used0;
+  bt_on_ = was_on;
+  bt_iters_ = it0;
+  bt_solves_ = sv0;
+  bt_r0_min_ = lo0;
+  bt_r0_max_ = hi0;
+  return n;
 }
 
 double MultiGrid::bottom_ms(int *calls) {
@@ -1144,9 +1368,25 @@ void MultiGrid::bottom_solve(VariableCoeffPoissonOperator &op, LevelData &e, Lev
     }
     MGIC_HIP(hipEventRecord(bt_ev_[bt_used_++], op.stream()));
   };
-  if (bt_on_) mark();
-  bottom.solve(op, e, r, true);
-  if (bt_on_) mark();
+  bt_filled_ = true;
+  if (!bt_on_) {
+    bottom.solve(op, e, r, true);
+    return;
+  }
+  const size_t open = bt_used_;
+  mark();
+  try {
+    bottom.solve(op, e, r, true);
+  } catch (...) {
+    bt_used_ = open;  // keep the start/end pairs aligned
+    throw;
+  }
+  mark();
+  const double r0 = bottom.last_init_norm;
+  bt_r0_min_ = bt_solves_ ? std::min(bt_r0_min_, r0) : r0;
+  bt_r0_max_ = bt_solves_ ? std::max(bt_r0_max_, r0) : r0;
+  bt_iters_ += bottom.last_iters;
+  ++bt_solves_;
 }
 
 void MultiGrid::cycle(int d, LevelData &e, LevelData &r, bool e_zero, LevelData *phi_acc,

@@ -166,8 +166,18 @@ class VariableCoeffPoissonOperator {
 
  public:
   bool fusedSmootherApplies();
-  // kernel arguments for other drivers (the mixed-precision V-cycle)
+  // kernel arguments for other drivers (the mixed-precision V-cycle, the
+  // device-side BiCGStab)
   const BoxArgs &boxArgs(int n, bool homogeneous) { return args(n, homogeneous); }
+  const BoxArgs &boxArgsPlain(int n) const { return args_plain_[n]; }
+  // preCond(cor, res) as ONE two-sweep launch from w = res * lambda, which
+  // the caller has written (the device-side BiCGStab fuses that product into
+  // its vector updates): whether it applies (one box, domain faces only, the
+  // fused GSRB taking the two-sweep kernel for relax(cor, res, 2)), and the
+  // launch (skip: as gsrb_sweep_tb2's).  Bit-identical to preCond.
+  bool preCondFromScaledApplies();
+  void preCondFromScaled(LevelData &cor, const LevelData &w, const LevelData &res,
+                         const int *skip);
   StencilCoefs stencil() { return coefs(); }
   // `n` levelGSRB sweeps with the fused out-of-place kernel (alternating
   // dpsi and the scratch buffer; the result always ends in dpsi).
@@ -247,13 +257,38 @@ class BiCGStabSolver {
  public:
   BiCGStabParams prm;
   int last_iters = 0;
+  double last_init_norm = 0.0;  // norm of the residual the last solve started from
+  bool last_device = false;     // the last solve ran on the device (solveDevice)
   // preconditioner; empty = op.preCond (the bottom-solver use)
   std::function<void(LevelData &, const LevelData &)> precond;
   int solve(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
             bool homogeneous);
+  // the same loop with its scalars and stop tests on the device (one box,
+  // one rank's reductions, preCond as one two-sweep launch): batches of
+  // iterations queued without a readback, one published state per batch
+  // (MGIC_BICG_DEVICE=0: always the host loop; MGIC_BICG_BATCH: iterations
+  // per batch, default 4).  Bit-identical to the host loop.
+  bool deviceApplies(VariableCoeffPoissonOperator &op) const;
+  int solveDevice(VariableCoeffPoissonOperator &op, LevelData &phi, const LevelData &rhs,
+                  bool homogeneous);
+  BiCGStabSolver() = default;
+  BiCGStabSolver(const BiCGStabSolver &) = delete;
+  BiCGStabSolver &operator=(const BiCGStabSolver &) = delete;
+  ~BiCGStabSolver();
 
  private:
   std::map<const Grid *, std::vector<std::unique_ptr<LevelData>>> temps_;
+  struct DevWork {
+    kern::BicgState *d_st = nullptr;   // the loop's state (device)
+    kern::BicgState *h_pub = nullptr;  // published copy (pinned, host-coherent)
+    kern::BicgState *h_up = nullptr;   // upload staging (pinned)
+    unsigned long long *h_seq = nullptr;
+    unsigned long long seq = 0;
+    double *d_parts = nullptr;         // two partial arrays
+    std::unique_ptr<LevelData> w;      // res * lambda, the two-sweep launch's input
+  };
+  std::map<const Grid *, std::unique_ptr<DevWork>> dev_;
+  DevWork &devWork(VariableCoeffPoissonOperator &op);
 };
 
 struct MGParams {
@@ -315,6 +350,15 @@ class MultiGrid {
   // the last one)
   void bottom_timer(bool on);
   double bottom_ms(int *calls);
+  // BiCGStab iterations summed over the timed solves, and the smallest /
+  // largest norm of the coarse residual they started from
+  long bottom_iters(double *r0_min, double *r0_max) const;
+  // the last bottom solve again, `n` times, each from e = 0 on the same
+  // coarse residual (a fixed amount of work per solve): total ms between HIP
+  // events, iterations per solve, the residual's norm.  Returns the solves
+  // run (0 on a rank that does not own the coarsest depth, or before any
+  // V-cycle has filled it).
+  int bottom_replay(int n, double *ms, int *iters, double *r0);
   ~MultiGrid();
 
  private:
@@ -332,7 +376,10 @@ class MultiGrid {
              bool halo_out = false, const std::function<void()> *before_phi = nullptr);
   std::vector<Level> levels_;
   bool bt_on_ = false;
+  bool bt_filled_ = false;  // a bottom solve has run (bottom_replay's input exists)
   size_t bt_used_ = 0;
+  long bt_iters_ = 0, bt_solves_ = 0;
+  double bt_r0_min_ = 0.0, bt_r0_max_ = 0.0;
   std::vector<hipEvent_t> bt_ev_;
   void bottom_solve(VariableCoeffPoissonOperator &op, LevelData &e, LevelData &r);
 };

@@ -744,9 +744,10 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  const T *__restrict__ a,
                                                  const BoxArgs g, const StencilCoefs s,
                                                  const TB2Ghosts<T> gg, int kc, int ntx, int nty,
-                                                 int nblocks) {
+                                                 int nblocks, const int *__restrict__ skip) {
   using F = TB2<TX, TY, NT>;
   __shared__ T RB[F::RING];  // per ring slot: the red element of every pair, then the black
+  if (skip && *skip) return;  // a device-side solve has stopped (BicgState::done)
   const int L = sweep::xcd_tile(blockIdx.x, nblocks);
   const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
   const int z0 = (L / (ntx * nty)) * kc;
@@ -819,9 +820,14 @@ struct TB2Geom {
 
 template <class T, int TX, int TY, int NT>
 void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs &g,
-                const StencilCoefs &s, bool zero_in, double *acc, hipStream_t st) {
+                const StencilCoefs &s, bool zero_in, double *acc, hipStream_t st,
+                const int *skip = nullptr) {
   const TB2Geom<T, TX, TY, NT> G(g);
   const int ntx = G.ntx, nty = G.nty, kc = G.kc, nblocks = G.nblocks;
+  // the fp32 ACC launch stores into the fp64 phi at twice the float offsets:
+  // its planes must stay inside the buffer-offset range as doubles too
+  if (acc && (double)(g.ny + 8) * (double)g.sy * sizeof(double) >= 2147483648.0)
+    throw Error(kBadArg, "two-sweep launch: a phi plane exceeds the 2 GB buffer-offset range");
   const dim3 grid((unsigned)nblocks), block(NT);
   // FAST: the reference's constants (exact specialisation) and lambda in the
   // short reciprocal's range for T
@@ -850,10 +856,10 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   do {                                                                                             \
     if (ubc)                                                                                       \
       k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, true><<<grid, block, 0, st>>>(                           \
-          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks);                              \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
     else                                                                                           \
       k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, false><<<grid, block, 0, st>>>(                          \
-          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks);                              \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
   } while (0)
   if (acc) {
     if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");
@@ -892,8 +898,8 @@ bool gsrb_sweep_tb2_applies(const BoxArgs &g, const StencilCoefs &s, int kind) {
 // about the same whatever the tile, so wide tiles win
 void gsrb_sweep_tb2(double *u_out, const double *u_in, const double *rhs, const double *a,
                     const BoxArgs &g, const StencilCoefs &s, bool zero_in, double *acc,
-                    hipStream_t st) {
-  launch_tb2<double, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st);
+                    hipStream_t st, const int *skip) {
+  launch_tb2<double, 64, 22, 1024>(u_out, u_in, rhs, a, g, s, zero_in, acc, st, skip);
 }
 
 // fp32 (the mixed-precision V-cycle's smoother, BASELINE config C5): the same

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--agglomerate-below", type=int, default=0)
     ap.add_argument("--bottom-solver", type=int, default=0)
     ap.add_argument("--mode", choices=("vcycle", "mixed"), default="vcycle")
+    ap.add_argument("--fmg", type=int, default=0,
+                    help="vcycle mode: one fp64 FMG cycle (MultiGrid::fmg) before the iterations")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -48,7 +50,9 @@ def main():
 
     import bench
     import mg_ic_code_amd as mg
+    from mg_ic_code_amd._lib import check_single_hip_runtime
 
+    check_single_hip_runtime()  # one libamdhip64 image (the exit abort of two)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank,
                             world_size=a.world, timeout=datetime.timedelta(seconds=120))
     mg.set_device(a.device)
@@ -67,6 +71,8 @@ def main():
         norms += [amg.iteration(fphi, frhs, fres, 0) for _ in range(a.iters)]
     else:
         norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
+        if a.fmg:
+            norms.append(amg.fmg(fphi, frhs, fres, norm_type=0))
         norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(a.iters)]
     comm.synchronize()
     out = {"norms": np.array(norms), "transport": np.array(comm.transport),

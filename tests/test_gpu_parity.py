@@ -430,6 +430,62 @@ def test_bicgstab_bottom_pipelined_readbacks_bitwise(comm, rng, monkeypatch):
     assert np.array_equal(runs[0][1], runs[1][1])
 
 
+@pytest.mark.parametrize("n,nlevels", [(32, 3), (64, 3), (64, 2), (128, 2)])
+def test_bicgstab_bottom_on_device_bitwise(comm, monkeypatch, n, nlevels):
+    """The bottom BiCGStab with its scalars and stop tests on the device
+    (op.cpp BiCGStabSolver::solveDevice: fused vector updates + reductions,
+    last-block finals, batches without readbacks) equals the host loop --
+    pipelined and unpipelined -- bit for bit in phi, every residual norm and
+    the iteration count, for batch sizes that stop inside, at the end of and
+    long before the end of a batch."""
+    runs = []
+    for env in ({"MGIC_BICG_DEVICE": "0", "MGIC_BICG_PIPE": "0"},
+                {"MGIC_BICG_DEVICE": "0", "MGIC_BICG_PIPE": "1"},
+                {"MGIC_BICG_DEVICE": "1", "MGIC_BICG_BATCH": "1"},
+                {"MGIC_BICG_DEVICE": "1", "MGIC_BICG_BATCH": "3"},
+                {"MGIC_BICG_DEVICE": "1", "MGIC_BICG_BATCH": "16"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        # constant bCoef and fused_smoother 2: preCond is one two-sweep launch
+        # (alpha 0 at 128^3: a Poisson bottom of many iterations)
+        S = build_pair(comm, np.random.default_rng(7), n, (1, 1, 1), nlevels=nlevels, bottom=1,
+                       fused=2, bvar=False, alpha=0.0 if n == 128 else 1.0)
+        amg = S["amg"]
+        amg.init_residual(S["fphi"], S["frhs"], S["fres"])
+        norms, iters = [], []
+        for _ in range(3):
+            norms.append(amg.iteration(S["fphi"], S["frhs"], S["fres"], 0))
+            dev, it, _ = amg.bottom_info()
+            assert dev == (env["MGIC_BICG_DEVICE"] == "1")
+            iters.append(it)
+        runs.append((norms, iters, download_global(S["fphi"], S["grid"], (n,) * 3)))
+    for r in runs[1:]:
+        assert r[0] == runs[0][0]
+        assert r[1] == runs[0][1]
+        assert np.array_equal(r[2], runs[0][2])
+    # (the 8^3 bottom converges in one iteration, then starts converged)
+    assert max(runs[0][1]) >= (8 if n == 128 else 1), runs[0][1]
+
+
+def test_bicgstab_bottom_replay_is_repeatable(comm):
+    """bottom_replay (the bench's fixed-work bottom timing) re-solves the last
+    coarse residual from e = 0: the same iterations and the same correction
+    every time, equal to the V-cycle's own solve."""
+    S = build_pair(comm, np.random.default_rng(3), 128, (1, 1, 1), nlevels=2, bottom=1, fused=2,
+                   bvar=False, alpha=0.0)
+    amg = S["amg"]
+    amg.init_residual(S["fphi"], S["frhs"], S["fres"])
+    amg.iteration(S["fphi"], S["frhs"], S["fres"], 0)
+    dev, it, r0 = amg.bottom_info()
+    assert dev and it >= 2
+    e = amg.level_field(1, 0)
+    e0 = e.download(0).copy()
+    for _ in range(2):
+        ms, it2, r02, n = amg.bottom_replay(2)
+        assert n == 2 and ms > 0.0 and it2 == it and r02 == r0
+        assert np.array_equal(e.download(0), e0)
+
+
 def test_agglomerated_hierarchy_matches_single_box(comm, rng):
     n = 32
     S = build_pair(comm, rng, n, (2, 2, 2), nlevels=5, bottom=0, agglomerate_below=16)

@@ -32,9 +32,9 @@ def free_port():
 
 
 def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, mode="vcycle",
-                bottom_solver=0):
+                bottom_solver=0, fmg=0, env_extra=None):
     port = free_port()
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONUNBUFFERED="1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONUNBUFFERED="1", **(env_extra or {}))
     procs = []
     logs = []
     for r in range(world):
@@ -44,7 +44,7 @@ def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, 
             [sys.executable, os.path.join(ROOT, "tests", "mp_worker.py"), "--rank", str(r),
              "--world", str(world), "--port", str(port), "--n", str(n), "--levels", str(levels),
              "--agglomerate-below", str(agglomerate_below), "--out", str(tmp_path),
-             "--mode", mode, "--bottom-solver", str(bottom_solver)],
+             "--mode", mode, "--bottom-solver", str(bottom_solver), "--fmg", str(fmg)],
             stdout=log, stderr=subprocess.STDOUT, env=env))
     rcs = []
     try:
@@ -57,14 +57,15 @@ def run_workers(tmp_path, world, n, levels=3, agglomerate_below=0, timeout=240, 
                 p.wait()
         for log in logs:
             log.close()
-    if any(rcs):
-        msg = "\n".join((tmp_path / f"w{r}.log").read_text()[-3000:] for r in range(world))
+    texts = [(tmp_path / f"w{r}.log").read_text() for r in range(world)]
+    if any(rcs) or any("double free" in x or "corruption" in x for x in texts):
+        msg = "\n".join(x[-3000:] for x in texts)
         pytest.fail(f"workers exited {rcs}:\n{msg}")
     out = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
     return out
 
 
-def single_box(n, levels, iters=2, mode="vcycle", bottom_solver=0):
+def single_box(n, levels, iters=2, mode="vcycle", bottom_solver=0, fmg=0):
     import bench
     comm = mg.Comm()
     case = bench.build_case(mg, comm, 1, n, levels, 4, bottom_solver=bottom_solver)
@@ -76,12 +77,14 @@ def single_box(n, levels, iters=2, mode="vcycle", bottom_solver=0):
         norms += [amg.iteration(fphi, frhs, fres, 0) for _ in range(iters)]
     else:
         norms = [amg.init_residual(fphi, frhs, fres, norm_type=0)]
+        if fmg:
+            norms.append(amg.fmg(fphi, frhs, fres, norm_type=0))
         norms += [amg.iteration(fphi, frhs, fres, norm_type=0) for _ in range(iters)]
     return norms, fphi.download(0)
 
 
-def check(out, n, levels, iters=2, mode="vcycle", bottom_solver=0):
-    norms, phi = single_box(n, levels, iters, mode, bottom_solver)
+def check(out, n, levels, iters=2, mode="vcycle", bottom_solver=0, fmg=0):
+    norms, phi = single_box(n, levels, iters, mode, bottom_solver, fmg)
     for o in out:
         assert str(o["transport"]) == "ipc"
         assert bool(o["checked"])  # commcheck.check_transport passed on every rank
@@ -153,6 +156,65 @@ def test_bicgstab_bottom_on_rank0_bitwise(tmp_path, world):
     agg = bench.agglomerate_default(world, n, levels)
     check(run_workers(tmp_path, world, n, levels, agglomerate_below=agg, bottom_solver=1,
                       timeout=300), n, levels, bottom_solver=1)
+
+
+@pytest.mark.parametrize("agg", [0, 9])
+def test_four_processes_fp64_fmg_bitwise(tmp_path, agg):
+    # MultiGrid::fmg (fp64) between processes on bench.py's 4-rank split at
+    # 128^3, 4 levels, deep halo; agg 9: the coarsest depth gathered onto rank
+    # 0 -- the other ranks stop the FMG's restriction loop after the gather,
+    # skip the coarse solve and wait in the scatter while rank 0 runs the
+    # gathered depths -- then two V-cycles: phi and every norm bit-identical
+    # to the single box
+    n, levels = 128, 4
+    check(run_workers(tmp_path, 4, n, levels, agglomerate_below=agg, fmg=1), n, levels, fmg=1)
+
+
+def test_two_processes_distributed_bicgstab_bottom_pipelines_agree(tmp_path):
+    # the BiCGStab bottom NOT gathered (agglomerate_below 0): every rank runs
+    # the host loop on its own half of the coarsest depth, each dot product
+    # and norm an allreduce (two back-to-back ones in dot2), the preCond /
+    # applyOp exchanges queued before the loop reads the norm that decides
+    # whether they were needed (MGIC_BICG_PIPE=1) -- phi and every norm
+    # bit-identical to the loop that waits for every reduction
+    # (MGIC_BICG_PIPE=0).  Against the single box the two halves' partial sums
+    # add in another order: equal to a relative 1e-9
+    n, levels = 128, 3
+    runs = []
+    for pipe in ("1", "0"):
+        d = tmp_path / f"pipe{pipe}"
+        d.mkdir()
+        runs.append(run_workers(d, 2, n, levels, agglomerate_below=0, bottom_solver=1,
+                                env_extra={"MGIC_BICG_PIPE": pipe}))
+    for a, b in zip(runs[0], runs[1]):
+        assert list(a["norms"]) == list(b["norms"])
+        assert np.array_equal(a["phi0"], b["phi0"])
+    norms, phi = single_box(n, levels, 2, "vcycle", 1)
+    for o in runs[0]:
+        assert np.allclose(o["norms"], norms, rtol=1e-9, atol=0.0)
+        b = o["box0"]
+        ref = phi[b[2]:b[5] + 1, b[1]:b[4] + 1, b[0]:b[3] + 1]
+        assert np.linalg.norm(o["phi0"] - ref) <= 1e-9 * np.linalg.norm(ref)
+
+
+def test_two_processes_gathered_device_bicgstab_bottom_bitwise(tmp_path):
+    # bench.py's split of 512^3 over two processes with the reference's
+    # BiCGStab bottom gathered onto rank 0 (agglomerate_below 65: the two
+    # 128 x 128 x 64 halves of the coarsest depth become one 128^3 box): rank
+    # 0 runs it on the device (BiCGStabSolver::solveDevice, as the bench's
+    # 8-GPU split does) -- phi and every norm bit-identical to the single box
+    n, levels = 512, 3
+    check(run_workers(tmp_path, 2, n, levels, agglomerate_below=65, bottom_solver=1, timeout=300),
+          n, levels, bottom_solver=1)
+
+
+def test_worker_exits_cleanly_with_one_hip_runtime(tmp_path):
+    # the abort at exit of a process holding two HIP runtimes (torch's bundled
+    # libamdhip64 and /opt/rocm's, "double free or corruption", status -6):
+    # a fresh one-rank worker process maps one image (mp_worker checks it) and
+    # exits 0 with no heap-corruption message (run_workers fails on either)
+    out = run_workers(tmp_path, 1, 64, 3)
+    assert len(out) == 1 and list(out[0]["norms"])
 
 
 def test_transport_check_single_rank():
