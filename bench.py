@@ -66,7 +66,8 @@ def parse():
                     help="V-cycles timed from phi = 0 with the BiCGStab bottom (fixed, so the "
                          "bottom's work does not depend on --steps / --warmup)")
     ap.add_argument("--bottom-replays", type=int, default=10,
-                    help="replays of the last bottom solve from e = 0 on the same coarse residual")
+                    help="replays of the first V-cycle's bottom solve from e = 0 on its coarse "
+                         "residual")
     ap.add_argument("--norm-type", type=int, default=0,
                     help="per-iteration residual norm of AMRMultiGrid's stop test (params.txt:37-38, "
                          "m_normType 0 = max norm; -1 skips it)")
@@ -389,9 +390,12 @@ def bottom_timing(mg, case, args, timed, nt, gsrb_ms):
         phi.set_zero()
         amg.init_residual(phi, frhs, res, norm_type=0)
 
-    # one untimed iteration allocates the solver's temporaries
+    # one untimed iteration allocates the solver's temporaries; the first
+    # V-cycle's bottom solve (from the largest coarse residual) is then
+    # replayed from e = 0: a fixed amount of work per solve
     fresh()
     amg.iterations(phi, frhs, res, 1, norm_type=nt)
+    rep_ms, rep_iters, rep_r0, rep_n = amg.bottom_replay(args.bottom_replays)
     fresh()
     el, hist = timed(lambda: amg.iterations(phi, frhs, res, kb, norm_type=nt))
     ms = el / kb * 1e3
@@ -403,8 +407,7 @@ def bottom_timing(mg, case, args, timed, nt, gsrb_ms):
     solve_ms, solves = amg.bottom_ms()
     iters, r0_lo, r0_hi = amg.bottom_iters()
     amg.bottom_timer(False)
-    # the last solve replayed from e = 0 on its own coarse residual
-    rep_ms, rep_iters, rep_r0, rep_n = amg.bottom_replay(args.bottom_replays)
+    dev = amg.bottom_info()[0]
     out = {"solver": "BiCGStab (imax 80, eps 1e-6, reps 1e-12, restarts 5; preCond = lambda r + "
                      "2 GSRB)",
            "depth": args.levels - 1,
@@ -416,13 +419,16 @@ def bottom_timing(mg, case, args, timed, nt, gsrb_ms):
            "bottom_solves_timed_rank0": solves,
            "iterations_per_solve": round(iters / solves, 3) if solves else None,
            "coarse_residual_norm_range": [r0_lo, r0_hi] if solves else None,
+           "on_device": dev,
            "replay": ({"solves": rep_n, "ms_per_solve": round(rep_ms / rep_n, 4),
                        "iterations_per_solve": rep_iters,
                        "ms_per_iteration": round(rep_ms / rep_n / max(1, rep_iters), 5),
                        "coarse_residual_norm": rep_r0} if rep_n else None),
            "residual_norm_history": hist[-3:] if nt >= 0 else None,
            "note": "every timed solve starts from an unconverged coarse residual (the range "
-                   "above): K_b V-cycles from phi = 0, then the last solve replayed from e = 0"}
+                   "above): K_b V-cycles from phi = 0; the replay re-solves the first V-cycle's "
+                   "coarse residual from e = 0; on_device: BiCGStabSolver::solveDevice (scalars "
+                   "and stop tests on the GPU, no readback per iteration)"}
     del amg, phi, res
     return out
 

@@ -1443,21 +1443,39 @@ __global__ __launch_bounds__(256) void k_cf_interp(double *__restrict__ u,
 // row-to-wave deal and accumulators, so every value is the host loop's bit
 // for bit.
 
-// the launch's last block to arrive (thread 0 stored this block's partials
-// before): agent-scope release, count, acquire in the last block
+// The launch's last block to arrive, by counters sharded per XCD (block b
+// runs on XCD b % 8): one word takes ~88 atomic adds per us, so 2048 blocks
+// on one counter cost ~23 us; on eight shards of 256 about 3.  Thread 0 has
+// stored this block's partials write-through (sc1, agent scope) and waits for
+// them before its add (MI355X_MICROARCH.md's counter hand-off); the last
+// adder of a shard adds to the top counter, and the last adder there resets
+// it and acquires at agent scope before its block reads the partials.  cnt:
+// nine counters, each on a 128-B line of its own (32 words apart), zero
+// between launches.
+constexpr int kBicgCntStride = 32, kBicgCntWords = 9 * kBicgCntStride;
+static_assert(4 * kBicgCntWords == kBicgCounterWords, "counter block size");
 __device__ __forceinline__ bool bicg_last_block(unsigned int *cnt, unsigned int nb) {
   __shared__ int last;
   if (threadIdx.x == 0) {
-    __threadfence();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned int prev =
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == nb - 1;
+    const unsigned int g = blockIdx.x & 7u;
+    const unsigned int ng = (nb + 7u - g) / 8u;  // blocks of shard g
+    const unsigned int groups = nb < 8u ? nb : 8u;
+    unsigned int *sh = cnt + kBicgCntStride * (1 + g);
+    int l = 0;
+    if (__hip_atomic_fetch_add(sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1) {
+      __hip_atomic_store(sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          groups - 1) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        l = 1;
+      }
+    }
+    last = l;
   }
   __syncthreads();
-  if (!last) return false;
-  __threadfence();
-  return true;
+  return last != 0;
 }
 
 __device__ __forceinline__ void bicg_store_part(double *p, double v) {
@@ -1465,17 +1483,23 @@ __device__ __forceinline__ void bicg_store_part(double *p, double v) {
                      (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ double bicg_load_part(const double *p) {
-  return __longlong_as_double((long long)__hip_atomic_load(
-      reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 
-// k_reduce_final<KIND>'s loop and tree over n partials, in the last block;
-// the result in every thread
+// k_reduce_final<KIND>'s loop and tree over n partials, in the last block
+// (the first 8 * RB partials loaded together, then added in the loop's
+// order); the result in every thread
 template <int KIND>
 __device__ double bicg_final(const double *parts, int n, double *sm) {
+  double v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int t = threadIdx.x + q * RB;
+    v[q] = t < n ? parts[t] : 0.0;
+  }
   double acc = red_init<KIND>();
-  for (int t = threadIdx.x; t < n; t += RB) acc = red_op<KIND>(acc, bicg_load_part(parts + t));
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if ((int)threadIdx.x + q * RB < n) acc = red_op<KIND>(acc, v[q]);
+  for (int t = threadIdx.x + 8 * RB; t < n; t += RB) acc = red_op<KIND>(acc, parts[t]);
   sm[threadIdx.x] = acc;
   __syncthreads();
   for (int w = RB / 2; w > 0; w >>= 1) {
@@ -1579,7 +1603,8 @@ __global__ __launch_bounds__(RB) void k_bicgd_apply_dot(BicgState *__restrict__ 
                                                        const double *__restrict__ a,
                                                        const double *__restrict__ b,
                                                        const BoxArgs g, const StencilCoefs s,
-                                                       double *__restrict__ parts) {
+                                                       double *__restrict__ parts,
+                                                       unsigned int *__restrict__ cnt) {
   __shared__ double sm[RB];
   if (st->done) return;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1589,14 +1614,13 @@ __global__ __launch_bounds__(RB) void k_bicgd_apply_dot(BicgState *__restrict__ 
     acc[q] = acc[q] + rt[idx] * vv;
   });
   bicg_block_part<0>(acc, sm, parts);
-  if (!bicg_last_block(&st->cnt[0], gridDim.x)) return;
+  if (!bicg_last_block(cnt, gridDim.x)) return;
   const double m = bicg_final<0>(parts, gridDim.x, sm);
   if (threadIdx.x == 0) {
     st->m = m;
     st->init = 0;
     if (fabs(m) > st->small * fabs(st->rho1)) st->alpha = st->rho1 / m;
     else bicg_stop(st, st->restarts >= st->num_restarts ? kBicgRestartLimit : kBicgRestart);
-    __hip_atomic_store(&st->cnt[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1608,7 +1632,8 @@ __global__ __launch_bounds__(RB) void k_bicgd_s(BicgState *__restrict__ st,
                                                const double *__restrict__ r,
                                                const double *__restrict__ v,
                                                const double *__restrict__ lam, const BoxArgs g,
-                                               double *__restrict__ parts) {
+                                               double *__restrict__ parts,
+                                               unsigned int *__restrict__ cnt) {
   __shared__ double sm[RB];
   if (st->done) return;
   const double ca = -st->alpha;
@@ -1620,40 +1645,40 @@ __global__ __launch_bounds__(RB) void k_bicgd_s(BicgState *__restrict__ st,
     acc[q] = red_op<NK>(acc[q], NK == 2 ? sv * sv : fabs(sv));
   });
   bicg_block_part<NK>(acc, sm, parts);
-  if (!bicg_last_block(&st->cnt[1], gridDim.x)) return;
+  if (!bicg_last_block(cnt, gridDim.x)) return;
   const double x = bicg_final<NK>(parts, gridDim.x, sm);
   if (threadIdx.x == 0) {
     const double nrm = bicg_norm_of(st->nt, x);
     st->nrm = nrm;
     st->epend = 1;
     if (nrm <= st->eps * st->init_norm || nrm <= st->reps) bicg_stop(st, kBicgHalf);
-    __hip_atomic_store(&st->cnt[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// T = L(ST); <T, S> and <T, T>; last block: omega (or the tt == 0 stop)
+// <T, S> and <T, T> of T = L(ST), T not stored (k_bicgd_r recomputes it,
+// the same expressions on the same inputs); last block: omega (or the
+// tt == 0 stop)
 template <bool BC>
 __global__ __launch_bounds__(RB) void k_bicgd_apply_dot2(BicgState *__restrict__ st,
-                                                        double *__restrict__ t,
                                                         const double *__restrict__ stv,
                                                         const double *__restrict__ s,
                                                         const double *__restrict__ a,
                                                         const double *__restrict__ b,
                                                         const BoxArgs g, const StencilCoefs sc,
                                                         double *__restrict__ parts_ts,
-                                                        double *__restrict__ parts_tt) {
+                                                        double *__restrict__ parts_tt,
+                                                        unsigned int *__restrict__ cnt) {
   __shared__ double sm[RB];
   if (st->done) return;
   double aa[4] = {0.0, 0.0, 0.0, 0.0}, bb[4] = {0.0, 0.0, 0.0, 0.0};
   bicg_rows(g, [&](int i, int j, int k, long idx, int q) {
     const double tv = bicg_apply<BC>(stv, a, b, idx, i, j, k, g, sc);
-    t[idx] = tv;
     aa[q] = aa[q] + tv * s[idx];
     bb[q] = bb[q] + tv * tv;
   });
   bicg_block_part<0>(aa, sm, parts_ts);
   bicg_block_part<0>(bb, sm, parts_tt);
-  if (!bicg_last_block(&st->cnt[2], gridDim.x)) return;
+  if (!bicg_last_block(cnt, gridDim.x)) return;
   const double ts = bicg_final<0>(parts_ts, gridDim.x, sm);
   const double tt = bicg_final<0>(parts_tt, gridDim.x, sm);
   if (threadIdx.x == 0) {
@@ -1661,30 +1686,34 @@ __global__ __launch_bounds__(RB) void k_bicgd_apply_dot2(BicgState *__restrict__
     st->tt = tt;
     if (tt == 0.0) bicg_stop(st, kBicgTt0);
     else st->omega = ts / tt;
-    __hip_atomic_store(&st->cnt[2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// R = S + (-omega) T; E = (E + alpha PT) + omega ST; |R| (kind NK) and
-// <RT, R>; last block: the omega == 0 stop, then the loop's head -- its test,
-// it += 1, rho1 = <RT, R>, the rho1 == 0 stop and beta
-template <int NK>
+// R = S + (-omega) T with T = L(ST) recomputed; E = (E + alpha PT) + omega
+// ST; |R| (kind NK) and <RT, R>; last block: the omega == 0 stop, then the
+// loop's head -- its test, it += 1, rho1 = <RT, R>, the rho1 == 0 stop and
+// beta
+template <int NK, bool BC>
 __global__ __launch_bounds__(RB) void k_bicgd_r(BicgState *__restrict__ st,
                                                double *__restrict__ r, double *__restrict__ e,
                                                const double *__restrict__ s,
-                                               const double *__restrict__ t,
+                                               const double *__restrict__ a,
+                                               const double *__restrict__ b,
+                                               const StencilCoefs sc,
                                                const double *__restrict__ pt,
                                                const double *__restrict__ stv,
                                                const double *__restrict__ rt, const BoxArgs g,
                                                double *__restrict__ parts_n,
-                                               double *__restrict__ parts_d) {
+                                               double *__restrict__ parts_d,
+                                               unsigned int *__restrict__ cnt) {
   __shared__ double sm[RB];
   if (st->done) return;
   const double alpha = st->alpha, omega = st->omega, ca = -omega;
   double an[4] = {red_init<NK>(), red_init<NK>(), red_init<NK>(), red_init<NK>()};
   double ad[4] = {0.0, 0.0, 0.0, 0.0};
-  bicg_rows(g, [&](int, int, int, long idx, int q) {
-    const double rv = s[idx] + ca * t[idx];
+  bicg_rows(g, [&](int i, int j, int k, long idx, int q) {
+    const double tv = bicg_apply<BC>(stv, a, b, idx, i, j, k, g, sc);
+    const double rv = s[idx] + ca * tv;
     r[idx] = rv;
     const double e1 = e[idx] + alpha * pt[idx];
     e[idx] = e1 + omega * stv[idx];
@@ -1693,7 +1722,7 @@ __global__ __launch_bounds__(RB) void k_bicgd_r(BicgState *__restrict__ st,
   });
   bicg_block_part<NK>(an, sm, parts_n);
   bicg_block_part<0>(ad, sm, parts_d);
-  if (!bicg_last_block(&st->cnt[3], gridDim.x)) return;
+  if (!bicg_last_block(cnt, gridDim.x)) return;
   const double x = bicg_final<NK>(parts_n, gridDim.x, sm);
   const double rho_next = bicg_final<0>(parts_d, gridDim.x, sm);
   if (threadIdx.x == 0) {
@@ -1712,7 +1741,6 @@ __global__ __launch_bounds__(RB) void k_bicgd_r(BicgState *__restrict__ st,
       if (rho_next == 0.0) bicg_stop(st, kBicgRho0);
       else st->beta = (st->rho1 / st->rho2) * (st->alpha / st->omega);
     }
-    __hip_atomic_store(&st->cnt[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2272,46 +2300,61 @@ void bicg_dev_p(BicgState *st, double *p, double *w, const double *v, const doub
 
 void bicg_dev_apply_dot(BicgState *st, double *v, const double *pt, const double *rt,
                         const double *a, const double *b, const BoxArgs &g, const StencilCoefs &s,
-                        double *parts, hipStream_t st_) {
+                        double *parts, unsigned int *cnt, hipStream_t st_) {
   const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
-  if (s.bconst) k_bicgd_apply_dot<true><<<grid, block, 0, st_>>>(st, v, pt, rt, a, b, g, s, parts);
-  else k_bicgd_apply_dot<false><<<grid, block, 0, st_>>>(st, v, pt, rt, a, b, g, s, parts);
+  cnt += 0 * kBicgCntWords;
+  if (s.bconst) k_bicgd_apply_dot<true><<<grid, block, 0, st_>>>(st, v, pt, rt, a, b, g, s, parts, cnt);
+  else k_bicgd_apply_dot<false><<<grid, block, 0, st_>>>(st, v, pt, rt, a, b, g, s, parts, cnt);
   check_launch();
 }
 
 void bicg_dev_s(BicgState *st, double *s, double *w, const double *r, const double *v,
-                const double *lam, const BoxArgs &g, int norm_kind, double *parts, hipStream_t st_) {
+                const double *lam, const BoxArgs &g, int norm_kind, double *parts,
+                unsigned int *cnt, hipStream_t st_) {
   const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
+  cnt += 1 * kBicgCntWords;
   switch (norm_kind) {
-    case 1: k_bicgd_s<1><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts); break;
-    case 2: k_bicgd_s<2><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts); break;
-    case 3: k_bicgd_s<3><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts); break;
+    case 1: k_bicgd_s<1><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts, cnt); break;
+    case 2: k_bicgd_s<2><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts, cnt); break;
+    case 3: k_bicgd_s<3><<<grid, block, 0, st_>>>(st, s, w, r, v, lam, g, parts, cnt); break;
     default: throw Error(kBadArg, "bicg_dev_s: bad norm kind");
   }
   check_launch();
 }
 
-void bicg_dev_apply_dot2(BicgState *st, double *t, const double *stv, const double *s,
-                         const double *a, const double *b, const BoxArgs &g, const StencilCoefs &sc,
-                         double *parts_ts, double *parts_tt, hipStream_t st_) {
+void bicg_dev_apply_dot2(BicgState *st, const double *stv, const double *s, const double *a,
+                         const double *b, const BoxArgs &g, const StencilCoefs &sc,
+                         double *parts_ts, double *parts_tt, unsigned int *cnt, hipStream_t st_) {
   const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
+  cnt += 2 * kBicgCntWords;
   if (sc.bconst)
-    k_bicgd_apply_dot2<true><<<grid, block, 0, st_>>>(st, t, stv, s, a, b, g, sc, parts_ts, parts_tt);
+    k_bicgd_apply_dot2<true><<<grid, block, 0, st_>>>(st, stv, s, a, b, g, sc, parts_ts, parts_tt,
+                                                      cnt);
   else
-    k_bicgd_apply_dot2<false><<<grid, block, 0, st_>>>(st, t, stv, s, a, b, g, sc, parts_ts, parts_tt);
+    k_bicgd_apply_dot2<false><<<grid, block, 0, st_>>>(st, stv, s, a, b, g, sc, parts_ts, parts_tt,
+                                                       cnt);
   check_launch();
 }
 
-void bicg_dev_r(BicgState *st, double *r, double *e, const double *s, const double *t,
-                const double *pt, const double *stv, const double *rt, const BoxArgs &g,
-                int norm_kind, double *parts_n, double *parts_d, hipStream_t st_) {
+void bicg_dev_r(BicgState *st, double *r, double *e, const double *s, const double *a,
+                const double *b, const StencilCoefs &sc, const double *pt, const double *stv,
+                const double *rt, const BoxArgs &g, int norm_kind, double *parts_n,
+                double *parts_d, unsigned int *cnt, hipStream_t st_) {
   const dim3 grid((unsigned)reduce_blocks(g)), block(RB);
-  switch (norm_kind) {
-    case 1: k_bicgd_r<1><<<grid, block, 0, st_>>>(st, r, e, s, t, pt, stv, rt, g, parts_n, parts_d); break;
-    case 2: k_bicgd_r<2><<<grid, block, 0, st_>>>(st, r, e, s, t, pt, stv, rt, g, parts_n, parts_d); break;
-    case 3: k_bicgd_r<3><<<grid, block, 0, st_>>>(st, r, e, s, t, pt, stv, rt, g, parts_n, parts_d); break;
+  cnt += 3 * kBicgCntWords;
+#define MGIC_BICG_R(K, BC)                                                                   \
+  k_bicgd_r<K, BC><<<grid, block, 0, st_>>>(st, r, e, s, a, b, sc, pt, stv, rt, g, parts_n,  \
+                                            parts_d, cnt)
+  switch (norm_kind * 2 + (sc.bconst ? 1 : 0)) {
+    case 2: MGIC_BICG_R(1, false); break;
+    case 3: MGIC_BICG_R(1, true); break;
+    case 4: MGIC_BICG_R(2, false); break;
+    case 5: MGIC_BICG_R(2, true); break;
+    case 6: MGIC_BICG_R(3, false); break;
+    case 7: MGIC_BICG_R(3, true); break;
     default: throw Error(kBadArg, "bicg_dev_r: bad norm kind");
   }
+#undef MGIC_BICG_R
   check_launch();
 }
 

@@ -161,27 +161,31 @@ struct BicgState {
   double rho1, rho2, alpha, beta, omega, nrm, init_norm, rho_next, m, ts, tt;
   double eps, reps, small;
   int it, imax, done, reason, epend, init, restarts, num_restarts, nt;
-  unsigned int cnt[4];  // last-block counters, one per reduction launch (0 between launches)
   int pad;
 };
+// the reductions' last-block counters (device, zeroed once; each launch
+// leaves its own at zero): this many words
+constexpr int kBicgCounterWords = 4 * 9 * 32;
 // P = R (init) or ((P*beta) + ((-beta)*omega)*V) + 1.0*R; W = P * lambda
 void bicg_dev_p(BicgState *st, double *p, double *w, const double *v, const double *r,
                 const double *lam, const BoxArgs &g, hipStream_t st_);
 // V = L(PT) (homogeneous BC of g); alpha = rho1 / <RT, V>
 void bicg_dev_apply_dot(BicgState *st, double *v, const double *pt, const double *rt,
                         const double *a, const double *b, const BoxArgs &g, const StencilCoefs &s,
-                        double *parts, hipStream_t st_);
+                        double *parts, unsigned int *cnt, hipStream_t st_);
 // S = R + (-alpha)V; W = S * lambda; nrm = |S|
 void bicg_dev_s(BicgState *st, double *s, double *w, const double *r, const double *v,
-                const double *lam, const BoxArgs &g, int norm_kind, double *parts, hipStream_t st_);
-// T = L(ST); omega = <T, S> / <T, T>
-void bicg_dev_apply_dot2(BicgState *st, double *t, const double *stv, const double *s,
-                         const double *a, const double *b, const BoxArgs &g, const StencilCoefs &sc,
-                         double *parts_ts, double *parts_tt, hipStream_t st_);
-// R = S + (-omega)T; E = (E + alpha PT) + omega ST; nrm = |R|; the loop head
-void bicg_dev_r(BicgState *st, double *r, double *e, const double *s, const double *t,
-                const double *pt, const double *stv, const double *rt, const BoxArgs &g,
-                int norm_kind, double *parts_n, double *parts_d, hipStream_t st_);
+                const double *lam, const BoxArgs &g, int norm_kind, double *parts,
+                unsigned int *cnt, hipStream_t st_);
+// omega = <T, S> / <T, T>, T = L(ST) (not stored)
+void bicg_dev_apply_dot2(BicgState *st, const double *stv, const double *s, const double *a,
+                         const double *b, const BoxArgs &g, const StencilCoefs &sc,
+                         double *parts_ts, double *parts_tt, unsigned int *cnt, hipStream_t st_);
+// R = S + (-omega)L(ST); E = (E + alpha PT) + omega ST; nrm = |R|; the loop head
+void bicg_dev_r(BicgState *st, double *r, double *e, const double *s, const double *a,
+                const double *b, const StencilCoefs &sc, const double *pt, const double *stv,
+                const double *rt, const BoxArgs &g, int norm_kind, double *parts_n,
+                double *parts_d, unsigned int *cnt, hipStream_t st_);
 // copy *st into pinned host memory, then store seqv into *seq (host-coherent)
 void bicg_dev_publish(const BicgState *st, BicgState *host, unsigned long long *seq,
                       unsigned long long seqv, hipStream_t st_);

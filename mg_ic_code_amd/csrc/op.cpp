@@ -1044,6 +1044,7 @@ BiCGStabSolver::~BiCGStabSolver() {
     DevWork &d = *kv.second;
     if (d.d_st) (void)hipFree(d.d_st);
     if (d.d_parts) (void)hipFree(d.d_parts);
+    if (d.d_cnt) (void)hipFree(d.d_cnt);
     if (d.h_pub) (void)hipHostFree(d.h_pub);
     if (d.h_up) (void)hipHostFree(d.h_up);
   }
@@ -1069,6 +1070,8 @@ BiCGStabSolver::DevWork &BiCGStabSolver::devWork(VariableCoeffPoissonOperator &o
     MGIC_HIP(hipMemset(d->d_st, 0, sizeof(kern::BicgState)));
     const int np = kern::bicg_dev_parts(op.boxArgsPlain(0));
     MGIC_HIP(hipMalloc(&d->d_parts, 2 * (size_t)std::max(1, np) * sizeof(double)));
+    MGIC_HIP(hipMalloc(&d->d_cnt, kern::kBicgCounterWords * sizeof(unsigned int)));
+    MGIC_HIP(hipMemset(d->d_cnt, 0, kern::kBicgCounterWords * sizeof(unsigned int)));
     void *p = nullptr;
     // the published state, then the sequence number the host spins on
     MGIC_HIP(hipHostMalloc(&p, sizeof(kern::BicgState) + 64, hipHostMallocCoherent));
@@ -1078,7 +1081,6 @@ BiCGStabSolver::DevWork &BiCGStabSolver::devWork(VariableCoeffPoissonOperator &o
                                                       sizeof(kern::BicgState) + 56);
     MGIC_HIP(hipHostMalloc(&p, sizeof(kern::BicgState), hipHostMallocDefault));
     d->h_up = static_cast<kern::BicgState *>(p);
-    d->w = op.create();
     slot = std::move(d);
   }
   return *slot;
@@ -1106,7 +1108,7 @@ int BiCGStabSolver::solveDevice(VariableCoeffPoissonOperator &op, LevelData &phi
   LevelData &R = *tv[0], &RT = *tv[1], &E = *tv[2], &P = *tv[3], &PT = *tv[4], &S = *tv[5],
             &ST = *tv[6], &T = *tv[7], &V = *tv[8];
   DevWork &dw = devWork(op);
-  LevelData &W = *dw.w;
+  LevelData &W = T;  // res * lambda for the two-sweep launches (T itself is never stored)
   const hipStream_t st = op.stream();
   const int nt = prm.normType, nk = norm_kind(nt);
   op.residual(R, phi, rhs, hom);
@@ -1133,18 +1135,19 @@ int BiCGStabSolver::solveDevice(VariableCoeffPoissonOperator &op, LevelData &phi
   const int np = kern::bicg_dev_parts(gp);
   double *pa = dw.d_parts, *pb = dw.d_parts + std::max(1, np);
   kern::BicgState *d = dw.d_st;
+  unsigned int *cnt = dw.d_cnt;
   const int *skip = &d->done;
   const int nb = bicg_batch();
   auto batch = [&] {
     for (int i = 0; i < nb; ++i) {
       kern::bicg_dev_p(d, P.p[0], W.p[0], V.p[0], R.p[0], lam, gp, st);
       op.preCondFromScaled(PT, W, P, skip);
-      kern::bicg_dev_apply_dot(d, V.p[0], PT.p[0], RT.p[0], a, b, gh, sc, pa, st);
-      kern::bicg_dev_s(d, S.p[0], W.p[0], R.p[0], V.p[0], lam, gp, nk, pa, st);
+      kern::bicg_dev_apply_dot(d, V.p[0], PT.p[0], RT.p[0], a, b, gh, sc, pa, cnt, st);
+      kern::bicg_dev_s(d, S.p[0], W.p[0], R.p[0], V.p[0], lam, gp, nk, pa, cnt, st);
       op.preCondFromScaled(ST, W, S, skip);
-      kern::bicg_dev_apply_dot2(d, T.p[0], ST.p[0], S.p[0], a, b, gh, sc, pa, pb, st);
-      kern::bicg_dev_r(d, R.p[0], E.p[0], S.p[0], T.p[0], PT.p[0], ST.p[0], RT.p[0], gp, nk, pa,
-                       pb, st);
+      kern::bicg_dev_apply_dot2(d, ST.p[0], S.p[0], a, b, gh, sc, pa, pb, cnt, st);
+      kern::bicg_dev_r(d, R.p[0], E.p[0], S.p[0], a, b, sc, PT.p[0], ST.p[0], RT.p[0], gh, nk, pa,
+                       pb, cnt, st);
     }
     kern::bicg_dev_publish(d, dw.h_pub, dw.h_seq, ++dw.seq, st);
     return dw.seq;
@@ -1173,7 +1176,6 @@ int BiCGStabSolver::solveDevice(VariableCoeffPoissonOperator &op, LevelData &phi
     h.done = 0;
     h.reason = kern::kBicgRun;
     h.epend = 0;
-    for (unsigned &c : h.cnt) c = 0;
     *dw.h_up = h;
     MGIC_HIP(hipMemcpyAsync(d, dw.h_up, sizeof(h), hipMemcpyHostToDevice, st));
     unsigned long long t1 = batch(), t2 = batch();

@@ -285,7 +285,7 @@ class BiCGStabSolver {
     unsigned long long *h_seq = nullptr;
     unsigned long long seq = 0;
     double *d_parts = nullptr;         // two partial arrays
-    std::unique_ptr<LevelData> w;      // res * lambda, the two-sweep launch's input
+    unsigned int *d_cnt = nullptr;     // the reductions' last-block counters
   };
   std::map<const Grid *, std::unique_ptr<DevWork>> dev_;
   DevWork &devWork(VariableCoeffPoissonOperator &op);
