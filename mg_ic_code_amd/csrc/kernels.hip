@@ -1534,14 +1534,42 @@ __device__ __forceinline__ void bicg_stop(BicgState *st, int reason) {
   st->reason = reason;
 }
 
-// k_reduce_partial's row-to-wave deal: f(i, j, k, idx, q) for every cell,
-// q = the lane's accumulator
-template <class F>
-__device__ __forceinline__ void bicg_rows(const BoxArgs &g, F &&f) {
+// k_reduce_partial's row-to-wave deal: for every cell, in that deal's order,
+// v = ld(i, j, k, idx) then op(v, i, j, k, idx, q), q = the lane's
+// accumulator.  Rows of at most 128 cells (the bottom's boxes) give a lane at
+// most two cells per row, both into accumulator 0: two rows are taken at
+// once, every load of the four cells issued before the first op, so each
+// lane keeps four cells' loads in flight (the ops, and so every sum, still
+// run in the deal's order).
+template <class LD, class OP>
+__device__ __forceinline__ void bicg_rows(const BoxArgs &g, LD &&ld, OP &&op) {
   constexpr int W = RB / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nrows = g.ny * g.nz;
-  for (int row = blockIdx.x * W + wave; row < nrows; row += gridDim.x * W) {
+  const int stride = gridDim.x * W;
+  if (g.nx <= 128) {
+    const bool c0 = lane < g.nx, c1 = lane + 64 < g.nx;
+    for (int row = blockIdx.x * W + wave; row < nrows; row += 2 * stride) {
+      const int rowb = row + stride;
+      const bool rb = rowb < nrows;
+      const int k = row / g.ny, j = row - k * g.ny;
+      const int kb = rb ? rowb / g.ny : k, jb = rb ? rowb - kb * g.ny : j;
+      const long base = (long)j * g.sy + (long)k * g.sz;
+      const long baseb = (long)jb * g.sy + (long)kb * g.sz;
+      decltype(ld(0, 0, 0, 0L)) v0{}, v1{}, v2{}, v3{};
+      if (c0) v0 = ld(lane, j, k, base + lane);
+      if (c1) v1 = ld(lane + 64, j, k, base + lane + 64);
+      if (rb && c0) v2 = ld(lane, jb, kb, baseb + lane);
+      if (rb && c1) v3 = ld(lane + 64, jb, kb, baseb + lane + 64);
+      if (c0) op(v0, lane, j, k, base + lane, 0);
+      if (c1) op(v1, lane + 64, j, k, base + lane + 64, 0);
+      if (rb && c0) op(v2, lane, jb, kb, baseb + lane, 0);
+      if (rb && c1) op(v3, lane + 64, jb, kb, baseb + lane + 64, 0);
+    }
+    return;
+  }
+  auto f = [&](int i, int j, int k, long idx, int q) { op(ld(i, j, k, idx), i, j, k, idx, q); };
+  for (int row = blockIdx.x * W + wave; row < nrows; row += stride) {
     const int k = row / g.ny, j = row - k * g.ny;
     const long base = (long)j * g.sy + (long)k * g.sz;
     int i = lane;
@@ -1555,17 +1583,45 @@ __device__ __forceinline__ void bicg_rows(const BoxArgs &g, F &&f) {
   }
 }
 
-// VCCOMPUTEOP3D's value at one cell (k_apply_op's expressions)
+// VCCOMPUTEOP3D at one cell (k_apply_op's expressions, lap7's BC images),
+// split into its loads and its arithmetic for bicg_rows
+struct BicgSten {
+  double c, xm, xp, ym, yp, zm, zp, av, bv;
+};
 template <bool BC>
-__device__ __forceinline__ double bicg_apply(const double *__restrict__ u,
-                                             const double *__restrict__ a,
-                                             const double *__restrict__ b, long idx, int i, int j,
-                                             int k, const BoxArgs &g, const StencilCoefs &s) {
-  const double uc = u[idx];
-  const double lof = s.alpha * a[idx] * uc;
-  double ldpsi = lap7(u, idx, uc, i, j, k, g);
-  ldpsi = ldpsi * s.dxinv * s.beta * (BC ? s.bval : b[idx]);
-  return lof - ldpsi;
+__device__ __forceinline__ BicgSten bicg_sten_load(const double *__restrict__ u,
+                                                   const double *__restrict__ a,
+                                                   const double *__restrict__ b, long idx,
+                                                   const BoxArgs &g) {
+  BicgSten v;
+  v.c = u[idx];
+  v.xm = u[idx - 1];
+  v.xp = u[idx + 1];
+  v.ym = u[idx - g.sy];
+  v.yp = u[idx + g.sy];
+  v.zm = u[idx - g.sz];
+  v.zp = u[idx + g.sz];
+  v.av = a[idx];
+  v.bv = BC ? 0.0 : b[idx];
+  return v;
+}
+template <bool BC>
+__device__ __forceinline__ double bicg_sten_apply(BicgSten v, int i, int j, int k,
+                                                  const BoxArgs &g, const StencilCoefs &s) {
+  const double c = v.c;
+  if (i == 0 && g.bcm[0]) v.xm = ghost_of(g.bcm[0], g.bcc[0], c);
+  if (i == g.nx - 1 && g.bcm[1]) v.xp = ghost_of(g.bcm[1], g.bcc[1], c);
+  if (j == 0 && g.bcm[2]) v.ym = ghost_of(g.bcm[2], g.bcc[2], c);
+  if (j == g.ny - 1 && g.bcm[3]) v.yp = ghost_of(g.bcm[3], g.bcc[3], c);
+  if (k == 0 && g.bcm[4]) v.zm = ghost_of(g.bcm[4], g.bcc[4], c);
+  if (k == g.nz - 1 && g.bcm[5]) v.zp = ghost_of(g.bcm[5], g.bcc[5], c);
+  const double tx = (v.xp + v.xm) - 2.0 * c;
+  const double ty = (v.yp + v.ym) - 2.0 * c;
+  const double tz = (v.zp + v.zm) - 2.0 * c;
+  const double lap = (tx + ty) + tz;                  // lap7
+  const double lof = s.alpha * v.av * c;              // .ChF:211-212
+  const double ldpsi = lap * s.dxinv * s.beta * (BC ? s.bval : v.bv);  // .ChF:227
+  return lof - ldpsi;                                 // .ChF:229
 }
 
 // P = R (first iteration after a (re)start) or ((P*beta) + c*V) + 1.0*R,
@@ -1608,11 +1664,18 @@ __global__ __launch_bounds__(RB) void k_bicgd_apply_dot(BicgState *__restrict__ 
   __shared__ double sm[RB];
   if (st->done) return;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  bicg_rows(g, [&](int i, int j, int k, long idx, int q) {
-    const double vv = bicg_apply<BC>(pt, a, b, idx, i, j, k, g, s);
-    v[idx] = vv;
-    acc[q] = acc[q] + rt[idx] * vv;
-  });
+  struct L {
+    BicgSten u;
+    double rt;
+  };
+  bicg_rows(
+      g,
+      [&](int, int, int, long idx) { return L{bicg_sten_load<BC>(pt, a, b, idx, g), rt[idx]}; },
+      [&](const L &x, int i, int j, int k, long idx, int q) {
+        const double vv = bicg_sten_apply<BC>(x.u, i, j, k, g, s);
+        v[idx] = vv;
+        acc[q] = acc[q] + x.rt * vv;
+      });
   bicg_block_part<0>(acc, sm, parts);
   if (!bicg_last_block(cnt, gridDim.x)) return;
   const double m = bicg_final<0>(parts, gridDim.x, sm);
@@ -1638,12 +1701,17 @@ __global__ __launch_bounds__(RB) void k_bicgd_s(BicgState *__restrict__ st,
   if (st->done) return;
   const double ca = -st->alpha;
   double acc[4] = {red_init<NK>(), red_init<NK>(), red_init<NK>(), red_init<NK>()};
-  bicg_rows(g, [&](int, int, int, long idx, int q) {
-    const double sv = r[idx] + ca * v[idx];
-    s[idx] = sv;
-    w[idx] = sv * lam[idx];
-    acc[q] = red_op<NK>(acc[q], NK == 2 ? sv * sv : fabs(sv));
-  });
+  struct L {
+    double r, v, lam;
+  };
+  bicg_rows(
+      g, [&](int, int, int, long idx) { return L{r[idx], v[idx], lam[idx]}; },
+      [&](const L &x, int, int, int, long idx, int q) {
+        const double sv = x.r + ca * x.v;
+        s[idx] = sv;
+        w[idx] = sv * x.lam;
+        acc[q] = red_op<NK>(acc[q], NK == 2 ? sv * sv : fabs(sv));
+      });
   bicg_block_part<NK>(acc, sm, parts);
   if (!bicg_last_block(cnt, gridDim.x)) return;
   const double x = bicg_final<NK>(parts, gridDim.x, sm);
@@ -1671,11 +1739,18 @@ __global__ __launch_bounds__(RB) void k_bicgd_apply_dot2(BicgState *__restrict__
   __shared__ double sm[RB];
   if (st->done) return;
   double aa[4] = {0.0, 0.0, 0.0, 0.0}, bb[4] = {0.0, 0.0, 0.0, 0.0};
-  bicg_rows(g, [&](int i, int j, int k, long idx, int q) {
-    const double tv = bicg_apply<BC>(stv, a, b, idx, i, j, k, g, sc);
-    aa[q] = aa[q] + tv * s[idx];
-    bb[q] = bb[q] + tv * tv;
-  });
+  struct L {
+    BicgSten u;
+    double s;
+  };
+  bicg_rows(
+      g,
+      [&](int, int, int, long idx) { return L{bicg_sten_load<BC>(stv, a, b, idx, g), s[idx]}; },
+      [&](const L &x, int i, int j, int k, long, int q) {
+        const double tv = bicg_sten_apply<BC>(x.u, i, j, k, g, sc);
+        aa[q] = aa[q] + tv * x.s;
+        bb[q] = bb[q] + tv * tv;
+      });
   bicg_block_part<0>(aa, sm, parts_ts);
   bicg_block_part<0>(bb, sm, parts_tt);
   if (!bicg_last_block(cnt, gridDim.x)) return;
@@ -1711,15 +1786,24 @@ __global__ __launch_bounds__(RB) void k_bicgd_r(BicgState *__restrict__ st,
   const double alpha = st->alpha, omega = st->omega, ca = -omega;
   double an[4] = {red_init<NK>(), red_init<NK>(), red_init<NK>(), red_init<NK>()};
   double ad[4] = {0.0, 0.0, 0.0, 0.0};
-  bicg_rows(g, [&](int i, int j, int k, long idx, int q) {
-    const double tv = bicg_apply<BC>(stv, a, b, idx, i, j, k, g, sc);
-    const double rv = s[idx] + ca * tv;
-    r[idx] = rv;
-    const double e1 = e[idx] + alpha * pt[idx];
-    e[idx] = e1 + omega * stv[idx];
-    an[q] = red_op<NK>(an[q], NK == 2 ? rv * rv : fabs(rv));
-    ad[q] = ad[q] + rt[idx] * rv;
-  });
+  struct L {
+    BicgSten u;
+    double s, e, pt, rt;
+  };
+  bicg_rows(
+      g,
+      [&](int, int, int, long idx) {
+        return L{bicg_sten_load<BC>(stv, a, b, idx, g), s[idx], e[idx], pt[idx], rt[idx]};
+      },
+      [&](const L &x, int i, int j, int k, long idx, int q) {
+        const double tv = bicg_sten_apply<BC>(x.u, i, j, k, g, sc);
+        const double rv = x.s + ca * tv;
+        r[idx] = rv;
+        const double e1 = x.e + alpha * x.pt;
+        e[idx] = e1 + omega * x.u.c;  // (x.u.c: ST at the cell)
+        an[q] = red_op<NK>(an[q], NK == 2 ? rv * rv : fabs(rv));
+        ad[q] = ad[q] + x.rt * rv;
+      });
   bicg_block_part<NK>(an, sm, parts_n);
   bicg_block_part<0>(ad, sm, parts_d);
   if (!bicg_last_block(cnt, gridDim.x)) return;
