@@ -271,6 +271,52 @@ def test_mixed_vcycle_at_scale_converges_like_fp64(comm):
 
 
 @pytest.mark.gpu
+def test_c5_full_size_1024_fmg_mixed_tracks_fp64(comm):
+    # BASELINE config C5 at its own size on one GPU: the 1024^3 4-level FMG
+    # cycle and three V-cycles (SetBinaryBH source of params.txt, harmonic
+    # averaging, linear prolongation, nu = 4) in fp64 and with the mixed fp32
+    # smoother / fp64 residual.  The float32 oracle cannot run this size in a
+    # test, so the check is the size-independent property the mixed cycle
+    # promises: its residual max-norm history tracks the fp64 cycle's (within
+    # 1.5x while far above fp32 roundoff) and keeps falling; the same kernels
+    # are bit-identical to oracle/mixed.py at 128^3 (test above) and at
+    # 272x144x80 (test_mixed_streaming_multi_tile_bitwise).
+    import os
+    import mg_ic_code_amd as mg
+    from mg_ic_code_amd.params import read_params_file
+    prm = read_params_file(os.path.join(os.path.dirname(__file__), "golden", "params.txt"))
+    n = 1024
+    dom = (0, 0, 0, n - 1, n - 1, n - 1)
+    grid = mg.Grid(comm, dom, [dom], prm.L / n)
+    fa, fb, frhs, fphi, fres = (mg.LevelData(grid) for _ in range(5))
+    bh = prm.bh()
+    bh["domain_length"] = prm.L
+    mg.set_binary_bh_coefs(fa, frhs, bh)
+    fb.set_val(1.0)
+    op = mg.OperatorParams(alpha=prm.alpha, beta=prm.beta, bc_lo=tuple(prm.bc_lo),
+                           bc_hi=tuple(prm.bc_hi), bc_value=prm.bc_value,
+                           coefficient_average_type=1, prolong_type=1)
+    fac = mg.defineOperatorFactory(grid, fa, fb, op)
+    sp = mg.SolverParams(max_depth=3, n_pre=4, n_post=4, n_bottom=4, bottom_solver=0)
+    hists = []
+    for kind in ("fp64", "mixed"):
+        fphi.set_zero()
+        solver = mg.AMRMultiGrid(fac, sp) if kind == "fp64" else mg.MixedMultiGrid(fac, sp)
+        assert solver.num_depths == 4
+        h = [solver.init_residual(fphi, frhs, fres, 0), solver.fmg(fphi, frhs, fres, 0)]
+        h += [solver.iteration(fphi, frhs, fres, 0) for _ in range(3)]
+        hists.append(h)
+        del solver
+    f64, mix = hists
+    assert mix[0] == f64[0]
+    assert all(np.isfinite(mix)) and all(np.isfinite(f64))
+    for i in (1, 2, 3):
+        assert mix[i] < 1.5 * f64[i], (mix, f64)
+    for h in hists:
+        assert h[-1] < h[1] < h[0], h
+
+
+@pytest.mark.gpu
 def test_mixed_fmg_4level_multi_tile_bitwise(comm):
     # BASELINE config C5's cycle as configs states it: a 4-level FMG (then
     # V-cycles) in fp32 with the fp64 residual, at a multi-tile size: 272 x
