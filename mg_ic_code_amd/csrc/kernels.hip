@@ -1513,14 +1513,14 @@ __device__ double bicg_final(const double *parts, int n, double *sm) {
 
 // the block's partial of reduction KIND (k_reduce_partial's tree) -> parts[blockIdx.x]
 template <int KIND>
-__device__ void bicg_block_part(const double acc[4], double *sm, double *parts) {
+__device__ void bicg_block_part(const double acc[4], double *sm, double *parts, int lb) {
   sm[threadIdx.x] = red_op<KIND>(red_op<KIND>(acc[0], acc[1]), red_op<KIND>(acc[2], acc[3]));
   __syncthreads();
   for (int w = RB / 2; w > 0; w >>= 1) {
     if (threadIdx.x < w) sm[threadIdx.x] = red_op<KIND>(sm[threadIdx.x], sm[threadIdx.x + w]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) bicg_store_part(parts + blockIdx.x, sm[0]);
+  if (threadIdx.x == 0) bicg_store_part(parts + lb, sm[0]);
   __syncthreads();
 }
 
@@ -1534,6 +1534,18 @@ __device__ __forceinline__ void bicg_stop(BicgState *st, int reason) {
   st->reason = reason;
 }
 
+// The logical block whose rows (and partial) a block takes: its own index, or
+// (BicgState::xr, a grid of whole groups of 8) the XCD-contiguous deal --
+// block b runs on XCD b % 8 and takes logical block (b % 8) (nb / 8) + b / 8,
+// so an XCD streams a contiguous slab of planes (its L2 holds the y / z
+// neighbours of its rows).  The partials stay indexed by logical block, so
+// the sums, and every value, are the same either way.
+__device__ __forceinline__ int bicg_lblock(const BicgState *st) {
+  const int b = blockIdx.x, nb = gridDim.x;
+  if (!st->xr || (nb & 7)) return b;
+  return (b & 7) * (nb >> 3) + (b >> 3);
+}
+
 // k_reduce_partial's row-to-wave deal: for every cell, in that deal's order,
 // v = ld(i, j, k, idx) then op(v, i, j, k, idx, q), q = the lane's
 // accumulator.  Rows of at most 128 cells (the bottom's boxes) give a lane at
@@ -1542,14 +1554,14 @@ __device__ __forceinline__ void bicg_stop(BicgState *st, int reason) {
 // lane keeps four cells' loads in flight (the ops, and so every sum, still
 // run in the deal's order).
 template <class LD, class OP>
-__device__ __forceinline__ void bicg_rows(const BoxArgs &g, LD &&ld, OP &&op) {
+__device__ __forceinline__ void bicg_rows(const BoxArgs &g, int lb, LD &&ld, OP &&op) {
   constexpr int W = RB / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nrows = g.ny * g.nz;
   const int stride = gridDim.x * W;
   if (g.nx <= 128) {
     const bool c0 = lane < g.nx, c1 = lane + 64 < g.nx;
-    for (int row = blockIdx.x * W + wave; row < nrows; row += 2 * stride) {
+    for (int row = lb * W + wave; row < nrows; row += 2 * stride) {
       const int rowb = row + stride;
       const bool rb = rowb < nrows;
       const int k = row / g.ny, j = row - k * g.ny;
@@ -1569,7 +1581,7 @@ __device__ __forceinline__ void bicg_rows(const BoxArgs &g, LD &&ld, OP &&op) {
     return;
   }
   auto f = [&](int i, int j, int k, long idx, int q) { op(ld(i, j, k, idx), i, j, k, idx, q); };
-  for (int row = blockIdx.x * W + wave; row < nrows; row += stride) {
+  for (int row = lb * W + wave; row < nrows; row += stride) {
     const int k = row / g.ny, j = row - k * g.ny;
     const long base = (long)j * g.sy + (long)k * g.sz;
     int i = lane;
@@ -1668,15 +1680,16 @@ __global__ __launch_bounds__(RB) void k_bicgd_apply_dot(BicgState *__restrict__ 
     BicgSten u;
     double rt;
   };
+  const int lb = bicg_lblock(st);
   bicg_rows(
-      g,
+      g, lb,
       [&](int, int, int, long idx) { return L{bicg_sten_load<BC>(pt, a, b, idx, g), rt[idx]}; },
       [&](const L &x, int i, int j, int k, long idx, int q) {
         const double vv = bicg_sten_apply<BC>(x.u, i, j, k, g, s);
         v[idx] = vv;
         acc[q] = acc[q] + x.rt * vv;
       });
-  bicg_block_part<0>(acc, sm, parts);
+  bicg_block_part<0>(acc, sm, parts, lb);
   if (!bicg_last_block(cnt, gridDim.x)) return;
   const double m = bicg_final<0>(parts, gridDim.x, sm);
   if (threadIdx.x == 0) {
@@ -1704,15 +1717,16 @@ __global__ __launch_bounds__(RB) void k_bicgd_s(BicgState *__restrict__ st,
   struct L {
     double r, v, lam;
   };
+  const int lb = bicg_lblock(st);
   bicg_rows(
-      g, [&](int, int, int, long idx) { return L{r[idx], v[idx], lam[idx]}; },
+      g, lb, [&](int, int, int, long idx) { return L{r[idx], v[idx], lam[idx]}; },
       [&](const L &x, int, int, int, long idx, int q) {
         const double sv = x.r + ca * x.v;
         s[idx] = sv;
         w[idx] = sv * x.lam;
         acc[q] = red_op<NK>(acc[q], NK == 2 ? sv * sv : fabs(sv));
       });
-  bicg_block_part<NK>(acc, sm, parts);
+  bicg_block_part<NK>(acc, sm, parts, lb);
   if (!bicg_last_block(cnt, gridDim.x)) return;
   const double x = bicg_final<NK>(parts, gridDim.x, sm);
   if (threadIdx.x == 0) {
@@ -1743,16 +1757,17 @@ __global__ __launch_bounds__(RB) void k_bicgd_apply_dot2(BicgState *__restrict__
     BicgSten u;
     double s;
   };
+  const int lb = bicg_lblock(st);
   bicg_rows(
-      g,
+      g, lb,
       [&](int, int, int, long idx) { return L{bicg_sten_load<BC>(stv, a, b, idx, g), s[idx]}; },
       [&](const L &x, int i, int j, int k, long, int q) {
         const double tv = bicg_sten_apply<BC>(x.u, i, j, k, g, sc);
         aa[q] = aa[q] + tv * x.s;
         bb[q] = bb[q] + tv * tv;
       });
-  bicg_block_part<0>(aa, sm, parts_ts);
-  bicg_block_part<0>(bb, sm, parts_tt);
+  bicg_block_part<0>(aa, sm, parts_ts, lb);
+  bicg_block_part<0>(bb, sm, parts_tt, lb);
   if (!bicg_last_block(cnt, gridDim.x)) return;
   const double ts = bicg_final<0>(parts_ts, gridDim.x, sm);
   const double tt = bicg_final<0>(parts_tt, gridDim.x, sm);
@@ -1790,8 +1805,9 @@ __global__ __launch_bounds__(RB) void k_bicgd_r(BicgState *__restrict__ st,
     BicgSten u;
     double s, e, pt, rt;
   };
+  const int lb = bicg_lblock(st);
   bicg_rows(
-      g,
+      g, lb,
       [&](int, int, int, long idx) {
         return L{bicg_sten_load<BC>(stv, a, b, idx, g), s[idx], e[idx], pt[idx], rt[idx]};
       },
@@ -1804,8 +1820,8 @@ __global__ __launch_bounds__(RB) void k_bicgd_r(BicgState *__restrict__ st,
         an[q] = red_op<NK>(an[q], NK == 2 ? rv * rv : fabs(rv));
         ad[q] = ad[q] + x.rt * rv;
       });
-  bicg_block_part<NK>(an, sm, parts_n);
-  bicg_block_part<0>(ad, sm, parts_d);
+  bicg_block_part<NK>(an, sm, parts_n, lb);
+  bicg_block_part<0>(ad, sm, parts_d, lb);
   if (!bicg_last_block(cnt, gridDim.x)) return;
   const double x = bicg_final<NK>(parts_n, gridDim.x, sm);
   const double rho_next = bicg_final<0>(parts_d, gridDim.x, sm);
@@ -2057,8 +2073,15 @@ void fill_bc(double *u, const BoxArgs &g, hipStream_t st) {
 }
 
 static long reduce_blocks(const BoxArgs &g) {
+  // (MGIC_RED_MAXBLK: a lower cap, for A/Bs; the host loop and the device
+  // loop both size their partials here, so they stay bit-identical)
+  static const long cap = [] {
+    const char *e = getenv("MGIC_RED_MAXBLK");
+    const long v = e ? atol(e) : 0;
+    return v >= 8 && v <= kMaxPartsPerBox ? v : (long)kMaxPartsPerBox;
+  }();
   long nb = ((long)g.ny * g.nz + RB / 64 - 1) / (RB / 64);  // one wave per row at most
-  return nb > kMaxPartsPerBox ? kMaxPartsPerBox : nb;
+  return nb > cap ? cap : nb;
 }
 
 void blas(int kind, double *x, const double *y, const double *z, double s, double t,

@@ -161,7 +161,7 @@ struct BicgState {
   double rho1, rho2, alpha, beta, omega, nrm, init_norm, rho_next, m, ts, tt;
   double eps, reps, small;
   int it, imax, done, reason, epend, init, restarts, num_restarts, nt;
-  int pad;
+  int xr;  // bicg_lblock: the XCD-contiguous row deal (host-set)
 };
 // the reductions' last-block counters (device, zeroed once; each launch
 // leaves its own at zero): this many words

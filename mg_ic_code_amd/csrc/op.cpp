@@ -1086,6 +1086,17 @@ BiCGStabSolver::DevWork &BiCGStabSolver::devWork(VariableCoeffPoissonOperator &o
   return *slot;
 }
 
+// the reductions' XCD-contiguous row deal (kern::bicg_lblock; bit-identical
+// either way, 174.3 vs 175.9 us per 128^3 iteration, profiles/
+// r06m_bottom_deal_ab.txt): MGIC_BICG_XCD=0 turns it off
+static int bicg_xcd_deal() {
+  static const int v = [] {
+    const char *e = getenv("MGIC_BICG_XCD");
+    return e ? (atoi(e) != 0 ? 1 : 0) : 1;
+  }();
+  return v;
+}
+
 static int bicg_batch() {
   const char *e = getenv("MGIC_BICG_BATCH");
   const int b = e ? atoi(e) : 4;
@@ -1128,6 +1139,7 @@ int BiCGStabSolver::solveDevice(VariableCoeffPoissonOperator &op, LevelData &phi
   h.num_restarts = prm.numRestarts;
   h.nt = nt;
   h.init = 1;
+  h.xr = bicg_xcd_deal();
   last_init_norm = h.init_norm;
   const BoxArgs &gp = op.boxArgsPlain(0), &gh = op.boxArgs(0, true);
   const StencilCoefs sc = op.stencil();

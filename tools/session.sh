@@ -16,6 +16,7 @@
 #   proxy        tools/rank_proxy.py (PROXY_ARGS)
 #   c5           tools/bench_c5.py (C5_ARGS)
 #   kernels      tools/bench_kernels.py (KERNEL_ARGS)
+#   pmc          tools/pmc_kernels.sh (KRE, CMD, PASSES) -> pmc_summary.txt
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-s}
@@ -92,6 +93,8 @@ for s in ${STEPS:-tests smoke bench}; do
     proxy) run proxy 600 python tools/rank_proxy.py ${PROXY_ARGS:-} || exit $? ;;
     c5) run c5 600 python tools/bench_c5.py ${C5_ARGS:---vcycles 4} || exit $? ;;
     kernels) run kernels 600 python tools/bench_kernels.py ${KERNEL_ARGS:-} || exit $? ;;
+    pmc) run pmc 1000 bash tools/pmc_kernels.sh || exit $?
+         cp gpurun_out/${PMC_OUT:-pmc_k}/summary.txt "$O/pmc_summary.txt" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
