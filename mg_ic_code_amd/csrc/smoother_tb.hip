@@ -192,7 +192,7 @@ template <> struct TB2Vec<float> { using type = float2; };
 // compiled in for those; 0: an interior tile); UBC: every x / y domain face
 // of the box has the same ghost rule (one ghost per update instead of one
 // per face; without it EM is 15 and the faces come from ef).
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, int EM, bool UBC>
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, int EM, bool UBC, bool TRIM>
 __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo, double *__restrict__ acc,
                                          const T *__restrict__ ui,
                                          const T *__restrict__ rhs,
@@ -262,10 +262,50 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   // plane q's slot s0 (the steps derive every slot from one slot per step)
   auto es = [](int q) -> int { return q & 7; };
   auto eadd = [](int s0, int j) -> int { return (s0 + j) & 7; };
+  // Load offset of pair (X, X+1) in row gy.  No pass reads a ghost element of
+  // an x / y DOMAIN face (a face cell takes ghost(own value), see pass), so
+  // (TRIM) the tiles that reach one (EM != 0) load no ghost line at all: a pair
+  // wholly outside the box loads an in-box pair instead (its values are never
+  // read), a row outside the box loads the face row, and the pair that
+  // straddles the face loads the in-box pair next to it, its cell moved into
+  // place after the load (sw 1: element 1 <- the loaded element 0, at x = 0;
+  // sw 2: element 0 <- the loaded element 1, at x = nx - 1).  Interior tiles
+  // never reach a ghost line.
+  auto ld_off = [&](int X, int gy, int &sw) -> unsigned {
+    sw = 0;
+    int xl = clampi(X, -6, nx + 3), yl = clampi(gy, -4, ny + 3);
+    // (x only where the x-face code is compiled in: swz moves the straddling
+    // pair's cell, which a ring cell may read; likewise y)
+    if constexpr (TRIM && (EM & 3) != 0) {
+      if (g.bcm[0] && X < 0) {
+        sw = X == -1 ? 1 : 0;
+        xl = 0;
+      }
+      if (g.bcm[1] && X >= nx - 1) {
+        sw = X == nx - 1 ? 2 : 0;
+        xl = nx - 2;
+      }
+    }
+    if constexpr (TRIM && (EM & 12) != 0) {
+      if (g.bcm[2] && gy < 0) yl = 0;
+      if (g.bcm[3] && gy > ny - 1) yl = ny - 1;
+    }
+    return boff(xl, yl);
+  };
+  // the pair's elements from a load at ld_off (sw as set there)
+  auto swz = [](int sw, auto v) {
+    if constexpr (TRIM && (EM & 3) != 0) {
+      decltype(v) w;
+      w.x = sw == 2 ? v.y : v.x;
+      w.y = sw == 1 ? v.x : v.y;
+      return w;
+    } else {
+      return v;
+    }
+  };
   // ---- loads of u (slot c = LDS pair index), per plane parity t ----------
-  // (ghost pairs of x / y domain faces load whatever the ghost cells hold:
-  // no pass reads them, see pass)
   unsigned loff[2][NL];
+  int lsw = 0;  // sw of (t, i) at bits 2 (t NL + i)
 #pragma unroll
   for (int i = 0; i < NL; ++i) {
     const int c = tid + i * NT;
@@ -274,7 +314,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int X = x0 - 6 + 2 * m + ((gsum + gy + t) & 1);
-      loff[t][i] = c < CP ? boff(clampi(X, -6, nx + 3), clampi(gy, -4, ny + 3)) : 0u;
+      int sw;
+      const unsigned o = ld_off(X, gy, sw);
+      loff[t][i] = c < CP ? o : 0u;
+      lsw |= (c < CP ? sw : 0) << (2 * (t * NL + i));
     }
   }
   // ---- update pairs: c = tid + i * NT -> row rr (y0-3+rr), pair m ---------
@@ -306,6 +349,8 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     if ((ga < uylo || ga > uyhi) && (gb < uylo || gb > uyhi)) wthr = 4;
   }
   wthr = __builtin_amdgcn_readfirstlane(wthr);
+  // roff: the pair's load offset (ld_off; sw in rinf bits 12-13); its store
+  // offset is roff moved back by the straddle shift (st_off)
   unsigned roff[2][NP];
   // cbm: byte offset of the element before the pair's (pair index c - 1);
   // coy[t]: of its y / z neighbour column minus one row (c + s - 1 - PW, s
@@ -331,7 +376,10 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     for (int t = 0; t < 2; ++t) {
       const int sh = (gsum + gy + t) & 1;
       const int X = x0 - 6 + 2 * m + sh;
-      roff[t][i] = row_ok ? boff(clampi(X, -6, nx + 3), clampi(gy, -4, ny + 3)) : 0u;
+      int sw;
+      const unsigned lo = ld_off(X, gy, sw);
+      roff[t][i] = row_ok ? lo : 0u;
+      if (!row_ok) sw = 0;
       coy[t][i] = (unsigned)(cix + sh - 1 - PW) * ES;
       // (opaque from here on: the compiler adds each use's constant in the
       // ds instruction's offset field instead of keeping lane offset +
@@ -350,7 +398,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
         const bool st = row_ok && gy >= y0 && gy <= ty1 && gx >= x0 && gx <= tx1;
         bits |= (st ? 1 : 0) << (8 + e);
       }
-      rinf[t][i] = bits;
+      rinf[t][i] = bits | (sw << 12);
     }
   }
   // z extent of each pass: the chunk grown by the pass's ring width,
@@ -407,7 +455,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
         // loff 0 -- and put skips them, so every step issues a static number
         // of loads and the waits for the loads of two steps ago do not also
         // wait for the previous step's stores)
-        const V v = at2(pl, loff[t][i]);
+        const V v = swz((lsw >> (2 * (t * NL + i))) & 3, at2(pl, loff[t][i]));
         pu0[b][i] = v.x;
         pu1[b][i] = v.y;
       }
@@ -442,8 +490,9 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
     const char *pr = SD ? plane_u(rhs, p) : plane(rhs, p), *pa = SD ? plane_u(a, p) : plane(a, p);
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      const V vr = at2(pr, roff[t][i]);
-      const V va = at2(pa, roff[t][i]);
+      const int sw = (rinf[t][i] >> 12) & 3;
+      const V vr = swz(sw, at2(pr, roff[t][i]));
+      const V va = swz(sw, at2(pa, roff[t][i]));
       nr0[b][i] = vr.x;
       nr1[b][i] = vr.y;
       na0[b][i] = va.x;
@@ -579,6 +628,15 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   // an out-of-range offset, so every step issues exactly NP * 2 stores with
   // no branch around them and the next step waits vmcnt(2) for its loads
   // instead of vmcnt(0), which would also wait for these stores.
+  // the pair's store offset: its load offset, less the straddle shift
+  auto st_off = [&](int t, int i) -> unsigned {
+    unsigned o = roff[t][i];
+    if constexpr (TRIM && (EM & 3) != 0) {
+      const int sw = (rinf[t][i] >> 12) & 3;
+      o = sw == 1 ? o - ES : (sw == 2 ? o + ES : o);
+    }
+    return o;
+  };
   auto store = [&](int t, int k, int sl, auto sd) {  // sl = es(k)
     constexpr bool SD = decltype(sd)::value;
     const bool kin = SD || (k >= z0 && k < z1);  // uniform
@@ -600,7 +658,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
         double2 d;
         d.x = ac0[i] + (double)w.x;
         d.y = ac1[i] + (double)w.y;
-        const unsigned off = kAccScale * roff[t][i];
+        const unsigned off = kAccScale * st_off(t, i);
         const unsigned o4 = st == 3 ? off : kDrop;
         const unsigned o2 = st == 1 ? off : (st == 2 ? off + (unsigned)sizeof(double) : kDrop);
         const double e = st == 1 ? d.x : d.y;
@@ -612,7 +670,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
         w.x = ac0[i] + w.x;
         w.y = ac1[i] + w.y;
       }
-      const unsigned off = roff[t][i];
+      const unsigned off = st_off(t, i);
       // both elements (st 3) as one pair store; a single one (st 1 / 2, the
       // tile's x edges) as an element store
       const unsigned o4 = st == 3 ? off : kDrop;
@@ -667,7 +725,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
         for (int i = 0; i < NP; ++i) {
           ac0[i] = an0[i];
           ac1[i] = an1[i];
-          const double2 v = at2d(pl, kAccScale * roff[PU][i]);
+          const double2 v = swz((rinf[PU][i] >> 12) & 3, at2d(pl, kAccScale * roff[PU][i]));
           an0[i] = v.x;
           an1[i] = v.y;
         }
@@ -736,7 +794,7 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
 }
 
 
-template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool UBC>
+template <class T, int TX, int TY, int NT, bool ZIN, bool ACC, bool FAST, bool UBC, bool TRIM>
 __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  double *__restrict__ acc,
                                                  const T *__restrict__ ui,
@@ -756,8 +814,8 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
   const int ef = (g.bcm[0] && x0 <= 3 ? 1 : 0) | (g.bcm[1] && min(x0 + TX, g.nx) + 3 >= g.nx ? 2 : 0) |
                  (g.bcm[2] && y0 <= 3 ? 4 : 0) | (g.bcm[3] && min(y0 + TY, g.ny) + 3 >= g.ny ? 8 : 0);
 #define MGIC_TILE(EM)                                                                             \
-  tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, EM, UBC>(RB, uo, acc, ui, rhs, a, g, s, gg, x0, y0, z0,   \
-                                                   z1, ef)
+  tb2_tile<T, TX, TY, NT, ZIN, ACC, FAST, EM, UBC, TRIM>(RB, uo, acc, ui, rhs, a, g, s, gg, x0, y0,  \
+                                                         z0, z1, ef)
   // (uniform) an x-face or a y-face tile runs only that direction's ghost code
   if (!ef) MGIC_TILE(0);
   else if (UBC && !(ef & 12)) MGIC_TILE(UBC ? 3 : 15);
@@ -773,7 +831,7 @@ int tb2_resident_slots() {
     MGIC_HIP(hipGetDevice(&dev));
     MGIC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     MGIC_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per, k_gsrb_tb2<T, TX, TY, NT, false, false, true, true>, NT, 0));
+        &per, k_gsrb_tb2<T, TX, TY, NT, false, false, true, true, false>, NT, 0));
     return (per > 0 ? per : 1) * (ncu > 0 ? ncu : 1);
   }();
   return slots;
@@ -818,6 +876,8 @@ struct TB2Geom {
   }
 };
 
+constexpr double kTrimMinCells = 160.0 * 160.0 * 160.0;
+
 template <class T, int TX, int TY, int NT>
 void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs &g,
                 const StencilCoefs &s, bool zero_in, double *acc, hipStream_t st,
@@ -852,13 +912,30 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
     gg.sgn[0] = gg.sgn[rep];
     gg.c[0] = gg.c[rep];
   }
+  // trim: the edge tiles skip the ghost lines of x / y domain faces (TRIM in
+  // tb2_tile) -- on boxes large enough to stream from HBM (512^3 plain launch
+  // 0.941 -> 0.911 ms, profiles/r06q_ghost_trim_ab.txt); on MALL-resident
+  // ones (the 128^3 bottom) the straddle selects cost more than the lines
+  // (MGIC_TB2_TRIM: 0 never, 1 always, else by size; fp64 launches only)
+  static const int trim_env = [] {
+    const char *e = getenv("MGIC_TB2_TRIM");
+    return e ? atoi(e) : -1;
+  }();
+  // (fp64 only: the fp32 launch is not bound by its traffic, and the trimmed
+  // one ran 4.87 against 4.59 ms at 1024^3)
+  constexpr bool kDbl = std::is_same<T, double>::value;
+  const bool trim = kDbl && fast && ubc &&
+                    (trim_env == 1 || (trim_env != 0 && (double)g.nx * g.ny * g.nz >= kTrimMinCells));
 #define MGIC_TB2(Z, A, FA)                                                                         \
   do {                                                                                             \
-    if (ubc)                                                                                       \
-      k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, true><<<grid, block, 0, st>>>(                           \
+    if (ubc && FA && trim)                                                                         \
+      k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, true, FA && kDbl><<<grid, block, 0, st>>>(              \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
+    else if (ubc)                                                                                  \
+      k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, true, false><<<grid, block, 0, st>>>(                    \
           u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
     else                                                                                           \
-      k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, false><<<grid, block, 0, st>>>(                          \
+      k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, false, false><<<grid, block, 0, st>>>(                   \
           u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
   } while (0)
   if (acc) {
