@@ -410,13 +410,21 @@ __global__ __launch_bounds__(256) void k_residual_zl(RT *__restrict__ r,
   for (int h = 0; h < 2; ++h) {
     const int q = tid + 256 * h;
     const int rr = q / (kRlCols / 2), m = q - rr * (kRlCols / 2);
-    const int y = min(y0 - 1 + rr, g.ny + 1), x = min(x0 - 2 + 2 * m, g.nx & ~1);
+    int y = min(y0 - 1 + rr, g.ny + 1), x = min(x0 - 2 + 2 * m, g.nx & ~1);
+    // a ghost of a DOMAIN face is staged but replaced by its image (cell):
+    // pairs / rows wholly outside the box load an in-box one instead (no
+    // ghost line from HBM; the same for the ghost planes in fetch)
+    if (g.bcm[0] && x < 0) x = 0;
+    if (g.bcm[1] && x >= g.nx) x = (g.nx - 2) & ~1;
+    if (g.bcm[2] && y < 0) y = 0;
+    if (g.bcm[3] && y >= g.ny) y = g.ny - 1;
     poff[h] = (long)x + (long)y * g.sy;
     pl[h] = q < kRlPairs ? rr * kRlCols + 2 * m : -1;
   }
   V2<double> pre[2];
+  const int pzlo = g.bcm[4] ? 0 : -1, pzhi = g.bcm[5] ? g.nz - 1 : g.nz + 1;
   auto fetch = [&](int k) {
-    const double *p = u + (long)min(k, g.nz + 1) * g.sz;
+    const double *p = u + (long)min(max(k, pzlo), pzhi) * g.sz;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       if (pl[h] >= 0) pre[h] = ld2(p + poff[h]);
@@ -563,11 +571,18 @@ __global__ __launch_bounds__(256) void k_restrict_zl(T *__restrict__ rc, const B
   for (int i = 0; i < 3; ++i) {
     const int q = tid + 256 * i;
     const int r = q / (kRzCols / 2), m = q - r * (kRzCols / 2);
-    const int y = min(fy0 + r, fg.ny + 1), x = min(fx0 + 2 * m, fg.nx);
+    int y = min(fy0 + r, fg.ny + 1), x = min(fx0 + 2 * m, fg.nx);
+    // (domain-face ghosts are replaced by their images: no ghost line, as
+    // in k_residual_zl)
+    if (fg.bcm[0] && x < 0) x = 0;
+    if (fg.bcm[1] && x >= fg.nx) x = (fg.nx - 2) & ~1;
+    if (fg.bcm[2] && y < 0) y = 0;
+    if (fg.bcm[3] && y >= fg.ny) y = fg.ny - 1;
     poff[i] = (long)x + (long)y * fg.sy;
     pl[i] = q < kRzPairs ? r * kRzCols + 2 * m : -1;
   }
-  auto plane_ptr = [&](int k) { return u + (long)min(k, fg.nz + 1) * fg.sz; };
+  const int pzlo = fg.bcm[4] ? 0 : -1, pzhi = fg.bcm[5] ? fg.nz - 1 : fg.nz + 1;
+  auto plane_ptr = [&](int k) { return u + (long)min(max(k, pzlo), pzhi) * fg.sz; };
   V2<T> pre[2][3];
   auto fetch = [&](int k, int h) {
     const T *p = plane_ptr(k);

@@ -237,8 +237,13 @@ __device__ __forceinline__ void tb2_tile(T *__restrict__ RB, T *__restrict__ uo,
   auto plane_u = [&](const auto *f, int p) {
     return reinterpret_cast<const char *>(f + corner + (long)p * sz);
   };
-  auto plane = [&](const auto *f, int p) {  // corner of (clamped) plane p
-    return reinterpret_cast<const char *>(f + corner + (long)clampi(p, -4, nz + 3) * sz);
+  // corner of (clamped) plane p.  Beyond a z DOMAIN face no plane is read
+  // but the ghost plane, which is loaded as the plane it images (fetch_u):
+  // the fill / drain steps' loads there go to the face plane (L2 hits, no
+  // ghost lines from HBM)
+  const int pzlo = zdl ? 0 : -4, pzhi = zdh ? nz - 1 : nz + 3;
+  auto plane = [&](const auto *f, int p) {
+    return reinterpret_cast<const char *>(f + corner + (long)clampi(p, pzlo, pzhi) * sz);
   };
   // the lane offset is laundered per access: otherwise the compiler hoists
   // "array + lane offset" out of the z loop as 64-bit per-lane pointers (two
