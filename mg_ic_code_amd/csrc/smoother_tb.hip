@@ -921,16 +921,17 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   // tb2_tile) -- on boxes large enough to stream from HBM (512^3 plain launch
   // 0.941 -> 0.911 ms, profiles/r06q_ghost_trim_ab.txt); on MALL-resident
   // ones (the 128^3 bottom) the straddle selects cost more than the lines
-  // (MGIC_TB2_TRIM: 0 never, 1 always, else by size; fp64 launches only)
-  static const int trim_env = [] {
-    const char *e = getenv("MGIC_TB2_TRIM");
-    return e ? atoi(e) : -1;
+  // (MGIC_TB2_TRIM: a mask of launch kinds, for A/Bs; fp64 launches only)
+  static const int trim_mask = [] {
+    const char *e = getenv("MGIC_TB2_TRIM");  // bits: 1 ZIN, 2 plain, 4 ACC; 8 any size
+    return e ? atoi(e) : 7;
   }();
   // (fp64 only: the fp32 launch is not bound by its traffic, and the trimmed
   // one ran 4.87 against 4.59 ms at 1024^3)
   constexpr bool kDbl = std::is_same<T, double>::value;
-  const bool trim = kDbl && fast && ubc &&
-                    (trim_env == 1 || (trim_env != 0 && (double)g.nx * g.ny * g.nz >= kTrimMinCells));
+  const int kind_bit = acc ? 4 : (zero_in ? 1 : 2);
+  const bool trim = kDbl && fast && ubc && (trim_mask & kind_bit) &&
+                    ((trim_mask & 8) || (double)g.nx * g.ny * g.nz >= kTrimMinCells);
 #define MGIC_TB2(Z, A, FA)                                                                         \
   do {                                                                                             \
     if (ubc && FA && trim)                                                                         \
