@@ -807,11 +807,13 @@ __global__ __launch_bounds__(NT) void k_gsrb_tb2(T *__restrict__ uo,
                                                  const T *__restrict__ a,
                                                  const BoxArgs g, const StencilCoefs s,
                                                  const TB2Ghosts<T> gg, int kc, int ntx, int nty,
-                                                 int nblocks, const int *__restrict__ skip) {
+                                                 int nblocks, const int *__restrict__ skip,
+                                                 int rw) {
   using F = TB2<TX, TY, NT>;
   __shared__ T RB[F::RING];  // per ring slot: the red element of every pair, then the black
   if (skip && *skip) return;  // a device-side solve has stopped (BicgState::done)
-  const int L = sweep::xcd_tile(blockIdx.x, nblocks);
+  // (rw: workgroups resident per XCD for the round-major order; 0: xcd_tile)
+  const int L = rw > 0 ? sweep::round_tile(blockIdx.x, nblocks, rw) : sweep::xcd_tile(blockIdx.x, nblocks);
   const int x0 = (L % ntx) * TX, y0 = ((L / ntx) % nty) * TY;
   const int z0 = (L / (ntx * nty)) * kc;
   const int z1 = min(z0 + kc, g.nz);
@@ -922,6 +924,13 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   // 0.941 -> 0.911 ms, profiles/r06q_ghost_trim_ab.txt); on MALL-resident
   // ones (the 128^3 bottom) the straddle selects cost more than the lines
   // (MGIC_TB2_TRIM: a mask of launch kinds, for A/Bs; fp64 launches only)
+  // the tile order: round-major (sweep::round_tile) when the grid has whole
+  // dispatch rounds (MGIC_TB2_MAP: 0 xcd_tile, 1 round-major)
+  static const int map_env = [] {
+    const char *e = getenv("MGIC_TB2_MAP");
+    return e ? atoi(e) : 1;
+  }();
+  const int rw = map_env == 1 ? tb2_resident_slots<T, TX, TY, NT>() / 8 : 0;
   static const int trim_mask = [] {
     const char *e = getenv("MGIC_TB2_TRIM");  // bits: 1 ZIN, 2 plain, 4 ACC; 8 any size
     return e ? atoi(e) : 7;
@@ -936,13 +945,13 @@ void launch_tb2(T *u_out, const T *u_in, const T *rhs, const T *a, const BoxArgs
   do {                                                                                             \
     if (ubc && FA && trim)                                                                         \
       k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, true, FA && kDbl><<<grid, block, 0, st>>>(              \
-          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip, rw);                          \
     else if (ubc)                                                                                  \
       k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, true, false><<<grid, block, 0, st>>>(                    \
-          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip, rw);                          \
     else                                                                                           \
       k_gsrb_tb2<T, TX, TY, NT, Z, A, FA, false, false><<<grid, block, 0, st>>>(                   \
-          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip);                              \
+          u_out, acc, u_in, rhs, a, g, s, gg, kc, ntx, nty, nblocks, skip, rw);                          \
   } while (0)
   if (acc) {
     if (zero_in) throw Error(kBadArg, "two-sweep launch: accumulate on a zero input");

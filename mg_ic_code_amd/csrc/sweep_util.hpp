@@ -73,6 +73,22 @@ __device__ __forceinline__ int xcd_tile(int bid, int nblocks) {
   return xcd * q8 + min(xcd, r8) + i8;
 }
 
+// Round-major variant (w = workgroups resident per XCD): in each dispatch
+// round the 8 XCDs take 8 consecutive runs of w tiles of the logical order,
+// so the bands that border each other run at the same time on neighbouring
+// XCDs -- the halo rows they share are read twice at nearly the same moment
+// (the second read from the Infinity Cache) instead of one dispatch round
+// apart (twice from HBM).  Blocks past the last whole round keep xcd_tile's
+// contiguous ranges over what is left.
+__device__ __forceinline__ int round_tile(int bid, int nblocks, int w) {
+  const int full = w > 0 ? nblocks / (8 * w) * (8 * w) : 0;
+  if (bid < full) {
+    const int xcd = bid % 8, i8 = bid / 8;
+    return (i8 / w) * (8 * w) + xcd * w + i8 % w;
+  }
+  return full + xcd_tile(bid - full, nblocks - full);
+}
+
 }  // namespace sweep
 }  // namespace kern
 }  // namespace mgic
