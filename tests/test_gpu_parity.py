@@ -8,6 +8,7 @@ with a relaxation bottom.  Only the Krylov bottom solver (parallel dot
 products) is compared with a tolerance: rel-L2 <= 1e-10 (BASELINE.json).
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -1089,3 +1090,22 @@ def test_full_size_512_eight_boxes_rccl_deep_halo_bitwise():
     for r in out[1:]:
         assert out[0][0] == r[0]
         assert np.array_equal(out[0][1], r[1])
+
+
+def test_two_sweep_trim_and_round_order_match_oracle():
+    """The two-sweep launch's ghost-line trim (every launch kind, every box
+    size: MGIC_TB2_TRIM=15) and its round-major tile order with a partial
+    last round (MGIC_TB2_KC=8 on a 192 x 132 x 128 box) in a fresh process
+    (tests/trim_worker.py; the switches are read once per process): relax on
+    ragged shapes, odd offsets and every one-rule BC, and V-cycle iterations
+    (ZIN / plain / ACC launches), bit-identical to the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MGIC_TB2_TRIM="15", MGIC_TB2_KC="8", PYTHONUNBUFFERED="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "trim_worker.py")], cwd=root,
+                       env=env, capture_output=True, text=True, timeout=600)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "trim worker OK" in r.stdout, out[-3000:]
+    assert "double free" not in out and "corruption" not in out, out[-3000:]
