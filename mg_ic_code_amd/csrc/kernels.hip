@@ -540,7 +540,7 @@ __global__ __launch_bounds__(256) void k_restrict(T *__restrict__ rc, const BoxA
 // (profiles/r05q_stream_pmc.txt); short chunks (2 coarse planes) keep the
 // grid large, longer ones re-read fewer halo planes but ran slower.
 constexpr int kRzCols = 132, kRzRows = 10, kRzPairs = kRzRows * kRzCols / 2;  // 660
-template <class T, bool BC, int NT>
+template <class T, bool BC, int NT, bool PRE = false>
 __global__ __launch_bounds__(256) void k_restrict_zl(T *__restrict__ rc, const BoxArgs cg,
                                                      const T *__restrict__ u,
                                                      const T *__restrict__ rhs,
@@ -606,12 +606,28 @@ __global__ __launch_bounds__(256) void k_restrict_zl(T *__restrict__ rc, const B
   put(2 * k0 + 2, 1);
   __syncthreads();
   const T denom = (T)(2 * 2 * 2);  // .ChF:402
+  // PRE (constant bCoef): the rhs / aCoef rows of coarse plane ck + 1 are
+  // loaded while plane ck is summed (software pipelined: the waves keep a
+  // plane's worth of loads in flight instead of waiting for each plane's)
+  V2<T> crv[4], cav[4];
+  auto cload = [&](int ck, V2<T>(&rv_)[4], V2<T>(&av_)[4]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kk = q >> 1, jj = q & 1;
+      const long row = (long)(2 * ci) + (long)(2 * cj + jj) * fg.sy + (long)(2 * ck + kk) * fg.sz;
+      rv_[q] = ld2n<NT & 1>(rhs + row);
+      av_[q] = ld2n<NT & 1>(a + row);
+    }
+  };
+  if (PRE && act) cload(k0, crv, cav);
   for (int ck = k0; ck < k1; ++ck) {
     const bool more = ck + 1 < k1;
     if (more) {
       fetch(2 * ck + 3, 0);
       fetch(2 * ck + 4, 1);
     }
+    V2<T> nrv[4], nav[4];
+    if (PRE && act && more) cload(ck + 1, nrv, nav);
     if (act) {
       const long cidx = (long)ci + (long)cj * cg.sy + (long)ck * cg.sz;
       T sum = accumulate ? rc[cidx] : (T)0;
@@ -631,7 +647,8 @@ __global__ __launch_bounds__(256) void k_restrict_zl(T *__restrict__ rc, const B
           const V2<T> zp = *reinterpret_cast<const V2<T> *>(Lp + r * kRzCols + cx);
           const T xl = Lk[r * kRzCols + cx - 1], xr = Lk[r * kRzCols + cx + 2];
           const long row = (long)i0 + (long)j * fg.sy + (long)k * fg.sz;
-          const V2<T> rv = ld2n<NT & 1>(rhs + row), av = ld2n<NT & 1>(a + row);
+          const V2<T> rv = PRE ? crv[kk * 2 + jj] : ld2n<NT & 1>(rhs + row);
+          const V2<T> av = PRE ? cav[kk * 2 + jj] : ld2n<NT & 1>(a + row);
           V2<T> bv;
           if (BC) bv.x = bv.y = s.bval;
           else bv = ld2n<NT & 1>(b + row);
@@ -659,6 +676,13 @@ __global__ __launch_bounds__(256) void k_restrict_zl(T *__restrict__ rc, const B
           }
         }
       rc[cidx] = sum;
+    }
+    if (PRE && more) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        crv[q] = nrv[q];
+        cav[q] = nav[q];
+      }
     }
     if (more) {
       __syncthreads();  // every lane is done with planes 2ck-1, 2ck
@@ -2023,7 +2047,15 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
     const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
     const int kc = zl < cg.nz ? zl : cg.nz;
     const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
-    if (s.bconst)
+    // (MGIC_RESTRICT_PRE=0: rhs / aCoef loaded per plane, for A/Bs)
+    static const int pre = [] {
+      const char *e = getenv("MGIC_RESTRICT_PRE");
+      return e ? atoi(e) : 1;
+    }();
+    if (s.bconst && pre)
+      k_restrict_zl<double, true, 1, true><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc,
+                                                               ntx, nty, restrict_xcd());
+    else if (s.bconst)
       k_restrict_zl<double, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc, ntx, nty,
                                                          restrict_xcd());
     else
