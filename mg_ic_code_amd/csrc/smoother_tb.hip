@@ -845,11 +845,18 @@ int tb2_resident_slots() {
 }
 
 // z chunk per workgroup: minimise rounds(kc) * (kc + pipeline fill), the
-// fill being 7 steps rounded up with the chunk to the 2-step unroll
+// fill being 7 steps rounded up with the chunk to the 2-step unroll.  Chunks
+// go down to 4 planes (MGIC_TB2_KCMIN, for A/Bs): a 128^3 box of 12 tiles
+// then takes 19 chunks of 7 (228 workgroups, one round) instead of 15 of 9
 int tb2_choose_kc(int tiles, int nz, int slots) {
+  static const int kc_min = [] {
+    const char *e = getenv("MGIC_TB2_KCMIN");
+    const int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : v;
+  }();
   int best = nz;
   double best_cost = 1e300;
-  for (int kc = nz; kc >= 8; --kc) {
+  for (int kc = nz; kc >= kc_min; --kc) {
     const long nb = (long)tiles * ((nz + kc - 1) / kc);
     const long rounds = (nb + slots - 1) / slots;
     const double cost = (double)rounds * (double)(((kc + 7 + 1) / 2) * 2);
@@ -877,7 +884,7 @@ struct TB2Geom {
       const char *e = getenv("MGIC_TB2_KC");
       return e ? atoi(e) : 0;
     }();
-    kc = kc_env >= 8 ? (kc_env < g.nz ? kc_env : g.nz)
+    kc = kc_env >= 1 ? (kc_env < g.nz ? kc_env : g.nz)
                      : tb2_choose_kc(ntx * nty, g.nz, tb2_resident_slots<T, TX, TY, NT>());
     nblocks = ntx * nty * ((g.nz + kc - 1) / kc);
   }

@@ -1092,17 +1092,20 @@ def test_full_size_512_eight_boxes_rccl_deep_halo_bitwise():
         assert np.array_equal(out[0][1], r[1])
 
 
-def test_two_sweep_trim_and_round_order_match_oracle():
+@pytest.mark.parametrize("kc", ["8", "5"])
+def test_two_sweep_trim_and_round_order_match_oracle(kc):
     """The two-sweep launch's ghost-line trim (every launch kind, every box
     size: MGIC_TB2_TRIM=15) and its round-major tile order with a partial
     last round (MGIC_TB2_KC=8 on a 192 x 132 x 128 box) in a fresh process
     (tests/trim_worker.py; the switches are read once per process): relax on
     ragged shapes, odd offsets and every one-rule BC, and V-cycle iterations
-    (ZIN / plain / ACC launches), bit-identical to the oracle."""
+    (ZIN / plain / ACC launches), bit-identical to the oracle.  KC=5: the
+    short chunks the chooser now picks for small boxes (a 128^3 box takes
+    chunks of 7), every chunk boundary inside the 8-slot ring's fill."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MGIC_TB2_TRIM="15", MGIC_TB2_KC="8", PYTHONUNBUFFERED="1")
+    env = dict(os.environ, MGIC_TB2_TRIM="15", MGIC_TB2_KC=kc, PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, os.path.join(root, "tests", "trim_worker.py")], cwd=root,
                        env=env, capture_output=True, text=True, timeout=600)
     out = r.stdout + r.stderr
