@@ -1295,6 +1295,18 @@ inline void check_launch() {
 // 3.41 GB per 512^3 launch (1.19x -> 1.06x the compulsory reads) at the
 // same time (profiles/r05ah_restrict_chunk_band.txt: it is not bound by its
 // HBM bytes); the fp32 one keeps the dispatch order (MGIC_RESTRICT_F_XCD)
+// MGIC_RESTRICT_PRE (mask, 1 fp64 / 2 fp32, default 1): the LDS-staged
+// restriction with constant bCoef loads the next coarse plane's rhs / aCoef
+// rows while it sums the current one; 0 loads them per plane (A/Bs).  fp64:
+// 0.638 -> 0.615 ms at 512^3; fp32 (two coarse planes per workgroup): 1024^3
+// mixed V-cycle 31.05 -> 31.50 ms, so off (profiles/r06zh_restrict_f_pre_ab.txt)
+static int restrict_pre() {
+  static const int v = [] {
+    const char *e = getenv("MGIC_RESTRICT_PRE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
 static int residual_xcd() {
   static const int v = [] {
     const char *e = getenv("MGIC_RESIDUAL_XCD");
@@ -2047,12 +2059,7 @@ void restrict_residual(double *rc, const BoxArgs &cg, const double *u, const dou
     const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
     const int kc = zl < cg.nz ? zl : cg.nz;
     const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
-    // (MGIC_RESTRICT_PRE=0: rhs / aCoef loaded per plane, for A/Bs)
-    static const int pre = [] {
-      const char *e = getenv("MGIC_RESTRICT_PRE");
-      return e ? atoi(e) : 1;
-    }();
-    if (s.bconst && pre)
+    if (s.bconst && (restrict_pre() & 1))
       k_restrict_zl<double, true, 1, true><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, accu, kc,
                                                                ntx, nty, restrict_xcd());
     else if (s.bconst)
@@ -2361,7 +2368,10 @@ void restrict_residual_f(float *rc, const BoxArgs &cg, const float *u, const flo
     const int ntx = (cg.nx + TX - 1) / TX, nty = (cg.ny + 3) / 4;
     const int kc = fzl < cg.nz ? fzl : cg.nz;
     const int nb = ntx * nty * ((cg.nz + kc - 1) / kc);
-    if (s.bconst)
+    if (s.bconst && (restrict_pre() & 2))
+      k_restrict_zl<float, true, 1, true><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx,
+                                                              nty, restrict_f_xcd());
+    else if (s.bconst)
       k_restrict_zl<float, true, 1><<<nb, 256, 0, st>>>(rc, cg, u, rhs, a, b, fg, s, 0, kc, ntx, nty,
                                                         restrict_f_xcd());
     else

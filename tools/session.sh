@@ -15,6 +15,7 @@
 #   trace_bottom rocprofv3 kernel trace of bench_bottom.py -> summary + timeline of its tail
 #   proxy        tools/rank_proxy.py (PROXY_ARGS)
 #   c5           tools/bench_c5.py (C5_ARGS)
+#   c5ab         bench_c5.py interleaved over C5_ENVS ("X=1,X=0"), C5_REPS rounds (C5_ARGS)
 #   kernels      tools/bench_kernels.py (KERNEL_ARGS)
 #   pmc          tools/pmc_kernels.sh (KRE, CMD, PASSES) -> pmc_summary.txt
 set -u
@@ -92,6 +93,16 @@ for s in ${STEPS:-tests smoke bench}; do
                   trace_sum "$O/tb" trace_bottom ;;
     proxy) run proxy 600 python tools/rank_proxy.py ${PROXY_ARGS:-} || exit $? ;;
     c5) run c5 600 python tools/bench_c5.py ${C5_ARGS:---vcycles 4} || exit $? ;;
+    c5ab)
+      IFS=',' read -r -a sets <<< "${C5_ENVS:-MGIC_NONE=1}"
+      for rep in $(seq 1 "${C5_REPS:-2}"); do
+        i=0
+        for e in "${sets[@]}"; do
+          envrun "c5_${rep}_$i" 400 "$e" python tools/bench_c5.py ${C5_ARGS:---vcycles 4} || exit $?
+          echo "$e $(tail -n 1 "$O/c5_${rep}_$i.log")" >> "$O/c5ab.txt"
+          i=$((i + 1))
+        done
+      done ;;
     kernels) run kernels 600 python tools/bench_kernels.py ${KERNEL_ARGS:-} || exit $? ;;
     pmc) run pmc 1000 bash tools/pmc_kernels.sh || exit $?
          cp gpurun_out/${PMC_OUT:-pmc_k}/summary.txt "$O/pmc_summary.txt" ;;
