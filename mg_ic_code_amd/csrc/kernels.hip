@@ -1996,10 +1996,14 @@ void residual(double *r, const double *u, const double *rhs, const double *a, co
   check_launch();
 }
 
+// z chunk of the fp64 residual (MGIC_RESIDUAL_KC): 16 planes for both forms
+// (LDS-staged: 0.749 -> 0.737 ms at 512^3 against 32 with the XCD bands,
+// V-cycle +0.6%, profiles/r06zq_residual_chunk_ab.jsonl; the max-norm
+// partials are order-free, so the norm is the same whatever the chunk)
 static int residual_kc_env() {
   static const int mode = [] {
     const char *e = getenv("MGIC_RESIDUAL_KC");
-    return e ? atoi(e) : (residual_lds() ? 32 : 16);
+    return e ? atoi(e) : 16;
   }();
   return mode;
 }
